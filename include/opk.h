@@ -1,0 +1,158 @@
+/*
+ * opk.h -- C-ABI of libopk_hip.so, the MI355X (gfx950) implementation of OpenPose's per-frame
+ * body hot path: BODY_25 CNN forward -> resizeAndMerge -> NMS -> bodyPartConnector.
+ *
+ * Plain C: pointers, sizes and int status codes, no C++ or torch types.  Every function returns
+ * OPK_OK (0) or an error code; opk_last_error() returns the calling thread's message (the C++ shim
+ * in include/openpose_amd/ converts it into op::error(), the reference's error convention,
+ * errorAndLog.cpp:158-233).  "dev" pointers are device (HBM) pointers; "host" pointers host memory.
+ * All device work is enqueued on the context's hipStream_t; functions that hand results to the host
+ * synchronise that stream (the points where the reference reads cpu_data()).
+ *
+ * Each entry point names the reference interface it replaces (paths under /root/reference/).
+ */
+#ifndef OPK_H
+#define OPK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define OPK_OK 0
+#define OPK_ERR_ARG 1      /* invalid argument (reference: op::error(...) sanity checks)       */
+#define OPK_ERR_HIP 2      /* HIP runtime error (reference: cudaCheck, gpu/cuda.cpp:18-26)      */
+#define OPK_ERR_STATE 3    /* call out of order (e.g. forward before weights)                   */
+#define OPK_ERR_UNSUPPORTED 4
+
+/* PoseModel values (include/openpose/pose/enumClasses.hpp:9-30) */
+#define OPK_BODY_25 0
+#define OPK_COCO_18 1
+#define OPK_MPI_15 2
+#define OPK_MPI_15_4 3
+
+const char* opk_last_error(void);
+int opk_version(void);
+
+/* ---- context: one per GPU worker thread (reference: one PoseExtractorCaffe per GPU thread,
+ *      wrapperAuxiliary.hpp:328-337; device bound at init like Caffe::SetDevice, netCaffe.cpp:169) */
+typedef struct opk_ctx opk_ctx;
+int opk_ctx_create(int device, void* hip_stream /* NULL: the context creates its own */,
+                   opk_ctx** out);
+int opk_ctx_destroy(opk_ctx* ctx);
+int opk_ctx_stream(opk_ctx* ctx, void** hip_stream);
+int opk_sync(opk_ctx* ctx);
+int opk_malloc(opk_ctx* ctx, void** dev, size_t bytes);
+int opk_free(opk_ctx* ctx, void* dev);
+int opk_memset(opk_ctx* ctx, void* dev, int value, size_t bytes);
+int opk_memcpy_h2d(opk_ctx* ctx, void* dev_dst, const void* host_src, size_t bytes);
+int opk_memcpy_d2h(opk_ctx* ctx, void* host_dst, const void* dev_src, size_t bytes); /* syncs */
+
+/* ---- resizeAndMerge: replaces op::resizeAndMergeGpu<float>
+ *      (include/openpose/net/resizeAndMergeBase.hpp:17-20) with resizeAndMergeCpu numerics
+ *      (src/openpose/net/resizeAndMergeBase.cpp:9-113: cv::resize INTER_CUBIC per plane, then the
+ *      multi-scale average).  target_size / source_sizes are NCHW {N, C, H, W}; N frames are
+ *      processed as a batch (the reference merges N into one frame only for N == 1 per scale).
+ *      scale_ratios is accepted for signature parity and ignored, as in the CPU path (:18). */
+int opk_resize_and_merge(opk_ctx* ctx, float* target_dev, const float* const* sources_dev,
+                         int num_sources, const int target_size[4], const int* source_sizes,
+                         const float* scale_ratios);
+
+/* ---- NMS: replaces op::nmsGpu<float> (include/openpose/net/nmsBase.hpp:14-16) with nmsCpu
+ *      numerics (src/openpose/net/nmsBase.cpp:7-170).  target_size = {N, parts, maxPeaks+1, 3},
+ *      source_size = {N, C, H, W}; only the first `parts` planes of each frame are scanned.
+ *      kernel_scratch (the reference's int peak map) may be NULL: this implementation compacts
+ *      peaks in-kernel and never materialises it. */
+int opk_nms(opk_ctx* ctx, float* target_dev, int* kernel_scratch_dev, const float* source_dev,
+            float threshold, const int target_size[4], const int source_size[4],
+            float offset_x, float offset_y);
+
+/* ---- PAF pair scores: the pafScoreKernel stage of op::connectBodyPartsGpu
+ *      (src/openpose/net/bodyPartConnectorBase.cu:107-145) computed with the CPU path's getScoreAB
+ *      numerics (bodyPartConnectorBase.cpp:12-75: clamp to the map, 0 on rejection).
+ *      pair_scores_dev: [N][numPairs][maxPeaks][maxPeaks]; only i < nA, j < nB are written.
+ *      heat: [N][heat_channels][heat_h][heat_w]; peaks: [N][parts][maxPeaks+1][3]. */
+int opk_paf_scores(opk_ctx* ctx, float* pair_scores_dev, const float* heat_dev,
+                   const float* peaks_dev, int num_frames, int pose_model, int heat_channels,
+                   int heat_h, int heat_w, int max_peaks, float inter_threshold,
+                   float inter_min_above_threshold, float default_nms_threshold);
+
+/* ---- connectBodyParts: replaces op::connectBodyPartsGpu<float>
+ *      (include/openpose/net/bodyPartConnectorBase.hpp:17-24) with connectBodyPartsCpu semantics
+ *      (bodyPartConnectorBase.cpp:1327-1377): GPU pair scores + host people assembly.
+ *      keypoints_host [max_people][parts][3], scores_host [max_people]; *num_people gets the true
+ *      count (rows beyond max_people are dropped). */
+int opk_connect_body_parts(opk_ctx* ctx, float* keypoints_host, float* scores_host,
+                           int max_people, int* num_people, const float* heat_dev,
+                           const float* peaks_dev, int pose_model, int heat_channels, int heat_h,
+                           int heat_w, int max_peaks, float inter_min_above_threshold,
+                           float inter_threshold, int min_subset_cnt, float min_subset_score,
+                           float default_nms_threshold, float scale_factor,
+                           int maximize_positives);
+
+/* Host-only people assembly from host peaks + host dense pair scores
+ * (createPeopleVector's precomputed-score input, bodyPartConnectorBase.cpp:321-340, then
+ * removePeopleBelowThresholdsAndFillFaces + peopleVectorToPeopleArray :720-934). */
+int opk_assemble_people(float* keypoints_host, float* scores_host, int max_people,
+                        int* num_people, const float* pair_scores_host,
+                        const float* peaks_host, int pose_model, int max_peaks,
+                        int min_subset_cnt, float min_subset_score, float scale_factor,
+                        int maximize_positives);
+
+/* ---- Net: replaces op::Net / op::NetCaffe (include/openpose/net/net.hpp:8-18,
+ *      netCaffe.hpp:12-13).  prototxt: a Caffe prototxt path, or "builtin:BODY_25".
+ *      caffemodel: path or NULL (then weights must be supplied with opk_net_set_conv). */
+typedef struct opk_net opk_net;
+int opk_net_create(opk_ctx* ctx, const char* prototxt, const char* caffemodel, opk_net** out);
+int opk_net_destroy(opk_net* net);
+int opk_net_num_convs(opk_net* net);
+/* name buffer >= 64 bytes; act: 0 none, 1 ReLU, 2 PReLU */
+int opk_net_conv_info(opk_net* net, int index, char* name, int* cin, int* cout, int* kernel,
+                      int* act);
+/* Caffe layouts: weights [cout][cin][k][k], bias [cout], slope [cout] (NULL unless PReLU) */
+int opk_net_set_conv(opk_net* net, const char* name, const float* weights_host,
+                     const float* bias_host, const float* slope_host);
+/* input NCHW fp32 on device: [n][3][h][w] (the net input blob, netCaffe.cpp:230-247) */
+int opk_net_forward(opk_net* net, const float* input_dev, int n, int h, int w);
+/* device pointer + NCHW shape of the last forward's net_output blob */
+int opk_net_output(opk_net* net, float** output_dev, int shape[4]);
+
+/* ---- Pose extractor: replaces op::PoseExtractorCaffe::forwardPass
+ *      (src/openpose/pose/poseExtractorCaffe.cpp:200-334) for a batch of frames:
+ *      net -> resizeAndMerge -> NMS -> connector, one result set per frame. */
+typedef struct opk_pose opk_pose;
+/* PoseProperty (enumClasses.hpp:32-40) */
+#define OPK_PROP_NMS_THRESHOLD 0
+#define OPK_PROP_INTER_MIN_ABOVE_THRESHOLD 1
+#define OPK_PROP_INTER_THRESHOLD 2
+#define OPK_PROP_MIN_SUBSET_CNT 3
+#define OPK_PROP_MIN_SUBSET_SCORE 4
+int opk_pose_create(opk_ctx* ctx, opk_net* net /* may be NULL: net output injected */,
+                    int maximize_positives, opk_pose** out);
+int opk_pose_destroy(opk_pose* pose);
+int opk_pose_set_property(opk_pose* pose, int property, double value);
+/* frames: [n][3][net_h][net_w] device fp32; producer_w/h: original frame size (for
+ * scaleNetToOutput, poseExtractorCaffe.cpp:306-310) */
+int opk_pose_forward(opk_pose* pose, const float* frames_dev, int n, int net_h, int net_w,
+                     int producer_w, int producer_h);
+/* heat-map injection (poseNetOutput path, poseExtractorCaffe.cpp:249-262): net output on device
+ * [n][78][h][w]; net_h/net_w = the net input size it corresponds to */
+int opk_pose_forward_net_output(opk_pose* pose, const float* net_output_dev, int n, int out_h,
+                                int out_w, int net_h, int net_w, int producer_w, int producer_h);
+/* optional additive overlay on the net output before resize (synthetic-people workloads):
+ * [n][78][out_h][out_w] device fp32, NULL to disable */
+int opk_pose_set_overlay(opk_pose* pose, const float* overlay_dev);
+int opk_pose_num_people(opk_pose* pose, int frame);
+int opk_pose_keypoints(opk_pose* pose, int frame, float* keypoints_host, float* scores_host,
+                       int max_people);
+/* device pointers of the last forward's heatmaps [n][78][H][W] and peaks [n][25][128][3] */
+int opk_pose_heatmaps(opk_pose* pose, float** heat_dev, int shape[4]);
+int opk_pose_peaks(opk_pose* pose, float** peaks_dev, int shape[4]);
+float opk_pose_scale_net_to_output(opk_pose* pose);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* OPK_H */

@@ -1,0 +1,94 @@
+"""ctypes binding of libopk_hip.so (C-ABI: include/opk.h).
+
+The library is REQUIRED: importing the product API without it raises -- there is no CPU or
+PyTorch fallback anywhere in the product path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libopk_hip.so")
+
+_c = ctypes
+_p = _c.c_void_p
+_i = _c.c_int
+_f = _c.c_float
+_d = _c.c_double
+_ip = _c.POINTER(_c.c_int)
+_fp = _c.POINTER(_c.c_float)
+
+# name: (restype, argtypes)
+_SIGS = {
+    "opk_last_error": (_c.c_char_p, []),
+    "opk_version": (_i, []),
+    "opk_ctx_create": (_i, [_i, _p, _c.POINTER(_p)]),
+    "opk_ctx_destroy": (_i, [_p]),
+    "opk_ctx_stream": (_i, [_p, _c.POINTER(_p)]),
+    "opk_sync": (_i, [_p]),
+    "opk_malloc": (_i, [_p, _c.POINTER(_p), _c.c_size_t]),
+    "opk_free": (_i, [_p, _p]),
+    "opk_memset": (_i, [_p, _p, _i, _c.c_size_t]),
+    "opk_memcpy_h2d": (_i, [_p, _p, _p, _c.c_size_t]),
+    "opk_memcpy_d2h": (_i, [_p, _p, _p, _c.c_size_t]),
+    "opk_resize_and_merge": (_i, [_p, _p, _c.POINTER(_p), _i, _ip, _ip, _fp]),
+    "opk_nms": (_i, [_p, _p, _p, _p, _f, _ip, _ip, _f, _f]),
+    "opk_paf_scores": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _f, _f, _f]),
+    "opk_connect_body_parts": (_i, [_p, _p, _p, _i, _ip, _p, _p, _i, _i, _i, _i, _i, _f, _f, _i,
+                                    _f, _f, _f, _i]),
+    "opk_assemble_people": (_i, [_p, _p, _i, _ip, _p, _p, _i, _i, _i, _f, _f, _i]),
+    "opk_net_create": (_i, [_p, _c.c_char_p, _c.c_char_p, _c.POINTER(_p)]),
+    "opk_net_destroy": (_i, [_p]),
+    "opk_net_num_convs": (_i, [_p]),
+    "opk_net_conv_info": (_i, [_p, _i, _c.c_char_p, _ip, _ip, _ip, _ip]),
+    "opk_net_set_conv": (_i, [_p, _c.c_char_p, _p, _p, _p]),
+    "opk_net_forward": (_i, [_p, _p, _i, _i, _i]),
+    "opk_net_output": (_i, [_p, _c.POINTER(_p), _ip]),
+    "opk_pose_create": (_i, [_p, _p, _i, _c.POINTER(_p)]),
+    "opk_pose_destroy": (_i, [_p]),
+    "opk_pose_set_property": (_i, [_p, _i, _d]),
+    "opk_pose_forward": (_i, [_p, _p, _i, _i, _i, _i, _i]),
+    "opk_pose_forward_net_output": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i]),
+    "opk_pose_set_overlay": (_i, [_p, _p]),
+    "opk_pose_num_people": (_i, [_p, _i]),
+    "opk_pose_keypoints": (_i, [_p, _i, _p, _p, _i]),
+    "opk_pose_heatmaps": (_i, [_p, _c.POINTER(_p), _ip]),
+    "opk_pose_peaks": (_i, [_p, _c.POINTER(_p), _ip]),
+    "opk_pose_scale_net_to_output": (_f, [_p]),
+}
+
+_LIB = None
+
+
+class OpkError(RuntimeError):
+    pass
+
+
+def load():
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise OpkError("libopk_hip.so not built (run `python -m openpose_amd.build`); the "
+                           "product has no fallback path")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name, None)
+            if fn is None:       # reported by tests/test_abi.py::test_exports_every_symbol
+                continue
+            fn.restype = res
+            fn.argtypes = args
+        _LIB = L
+    return _LIB
+
+
+def exported_symbols():
+    return list(_SIGS)
+
+
+def check(rc):
+    if rc != 0:
+        raise OpkError("opk error %d: %s" % (rc, load().opk_last_error().decode()))
+    return rc
+
+
+def int4(v):
+    return (ctypes.c_int * 4)(*[int(x) for x in v])

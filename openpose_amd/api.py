@@ -1,0 +1,110 @@
+"""Python front end over the C-ABI (used by tests and bench.py).
+
+Device memory is handed over as torch CUDA tensors (PyTorch is plumbing here: allocation, streams,
+torch.distributed); every computation runs in libopk_hip.so.  The function names mirror the
+reference operators they replace (include/opk.h lists the reference file:line of each).
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, int4
+from .pose_tables import (BODY_25, CONNECT_INTER_MIN_ABOVE_THRESHOLD, CONNECT_INTER_THRESHOLD,
+                          CONNECT_MIN_SUBSET_CNT, CONNECT_MIN_SUBSET_SCORE, NMS_THRESHOLD)
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    assert t.is_cuda and t.is_contiguous(), "device tensors must be contiguous CUDA tensors"
+    return ctypes.c_void_p(t.data_ptr())
+
+
+class Context:
+    """One opk_ctx bound to a device; runs on torch's current stream of that device."""
+
+    def __init__(self, device=0, stream=None):
+        self.L = _lib.load()
+        self.device = device
+        torch.cuda.set_device(device)
+        s = stream if stream is not None else torch.cuda.current_stream(device)
+        self.torch_stream = s
+        h = ctypes.c_void_p()
+        check(self.L.opk_ctx_create(device, ctypes.c_void_p(s.cuda_stream), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.L.opk_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self):
+        check(self.L.opk_sync(self.h))
+
+    # ---- operators ---------------------------------------------------------------------------
+    def resize_and_merge(self, target, sources):
+        """target [N,C,H,W] fp32 CUDA; sources list of [N,C,h,w] (resizeAndMergeGpu)."""
+        n = len(sources)
+        ptrs = (ctypes.c_void_p * n)(*[s.data_ptr() for s in sources])
+        sizes = (ctypes.c_int * (4 * n))(*[int(v) for s in sources for v in s.shape])
+        check(self.L.opk_resize_and_merge(self.h, _ptr(target), ptrs, n, int4(target.shape), sizes,
+                                          None))
+
+    def nms(self, peaks, heat, threshold=NMS_THRESHOLD, offset=(0.0, 0.0)):
+        """peaks [N,parts,maxPeaks+1,3]; heat [N,C,H,W] (nmsGpu)."""
+        check(self.L.opk_nms(self.h, _ptr(peaks), None, _ptr(heat), threshold, int4(peaks.shape),
+                             int4(heat.shape), offset[0], offset[1]))
+
+    def paf_scores(self, scores, heat, peaks, pose_model=BODY_25, inter_th=CONNECT_INTER_THRESHOLD,
+                   inter_min_above=CONNECT_INTER_MIN_ABOVE_THRESHOLD, nms_th=NMS_THRESHOLD):
+        n, c, h, w = heat.shape
+        check(self.L.opk_paf_scores(self.h, _ptr(scores), _ptr(heat), _ptr(peaks), n, pose_model, c,
+                                    h, w, peaks.shape[2] - 1, inter_th, inter_min_above, nms_th))
+
+    def connect_body_parts(self, heat, peaks, pose_model=BODY_25, scale=1.0, max_people=512,
+                           inter_min_above=CONNECT_INTER_MIN_ABOVE_THRESHOLD,
+                           inter_th=CONNECT_INTER_THRESHOLD, min_subset_cnt=CONNECT_MIN_SUBSET_CNT,
+                           min_subset_score=CONNECT_MIN_SUBSET_SCORE, nms_th=NMS_THRESHOLD,
+                           maximize_positives=False):
+        """One frame: heat [C,H,W] / [1,C,H,W], peaks [parts,maxPeaks+1,3] (connectBodyPartsGpu)."""
+        c, h, w = heat.shape[-3:]
+        parts = peaks.shape[-3]
+        kp = np.zeros((max_people, parts, 3), np.float32)
+        ks = np.zeros(max_people, np.float32)
+        n = ctypes.c_int()
+        check(self.L.opk_connect_body_parts(
+            self.h, kp.ctypes.data_as(ctypes.c_void_p), ks.ctypes.data_as(ctypes.c_void_p),
+            max_people, ctypes.byref(n), _ptr(heat), _ptr(peaks), pose_model, c, h, w,
+            peaks.shape[-2] - 1, inter_min_above, inter_th, min_subset_cnt, min_subset_score,
+            nms_th, scale, int(maximize_positives)))
+        k = min(n.value, max_people)
+        return kp[:k].copy(), ks[:k].copy()
+
+
+def assemble_people(pair_scores, peaks, pose_model=BODY_25, scale=1.0, max_people=512,
+                    min_subset_cnt=CONNECT_MIN_SUBSET_CNT, min_subset_score=CONNECT_MIN_SUBSET_SCORE,
+                    maximize_positives=False):
+    """Host-only assembly from numpy pair scores [npairs,mp,mp] + peaks [parts,mp+1,3]."""
+    L = _lib.load()
+    pair_scores = np.ascontiguousarray(pair_scores, np.float32)
+    peaks = np.ascontiguousarray(peaks, np.float32)
+    parts = peaks.shape[0]
+    kp = np.zeros((max_people, parts, 3), np.float32)
+    ks = np.zeros(max_people, np.float32)
+    n = ctypes.c_int()
+    check(L.opk_assemble_people(kp.ctypes.data_as(ctypes.c_void_p),
+                                ks.ctypes.data_as(ctypes.c_void_p), max_people, ctypes.byref(n),
+                                pair_scores.ctypes.data_as(ctypes.c_void_p),
+                                peaks.ctypes.data_as(ctypes.c_void_p), pose_model,
+                                peaks.shape[1] - 1, min_subset_cnt, min_subset_score, scale,
+                                int(maximize_positives)))
+    k = min(n.value, max_people)
+    return kp[:k].copy(), ks[:k].copy()

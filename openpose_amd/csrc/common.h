@@ -1,0 +1,68 @@
+// common.h -- internal helpers shared by the HIP kernels and the C++ host of libopk_hip.so.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace opk {
+
+// Thread-local error message behind opk_last_error() (C-ABI error convention, include/opk.h).
+void set_error(const std::string& msg);
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define OPK_CHECK_ARG(cond, msg)                                                              \
+    do {                                                                                      \
+        if (!(cond)) throw ::opk::Error(1, std::string(__func__) + ": " + (msg));             \
+    } while (0)
+
+#define OPK_HIP(call)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (call);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            throw ::opk::Error(2, std::string(#call) + " failed: " + hipGetErrorString(e_) +   \
+                                      " (" + __FILE__ + ":" + std::to_string(__LINE__) + ")");  \
+    } while (0)
+
+// after a kernel launch (reference: cudaCheck -> cudaPeekAtLastError, gpu/cuda.cpp:18-26)
+#define OPK_LAUNCH_CHECK() OPK_HIP(hipPeekAtLastError())
+
+// Device scratch that only grows (one per context and purpose); never freed inside a launch
+// sequence so the launch functions stay graph-capturable.
+struct DevBuf {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    void* get(size_t need) {
+        if (need > bytes) {
+            if (ptr) OPK_HIP(hipFree(ptr));
+            ptr = nullptr;
+            OPK_HIP(hipMalloc(&ptr, need));
+            bytes = need;
+        }
+        return ptr;
+    }
+    ~DevBuf() { if (ptr) (void)hipFree(ptr); }
+};
+
+struct HostBuf {   // pinned host staging
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    void* get(size_t need) {
+        if (need > bytes) {
+            if (ptr) OPK_HIP(hipHostFree(ptr));
+            ptr = nullptr;
+            OPK_HIP(hipHostMalloc(&ptr, need, hipHostMallocDefault));
+            bytes = need;
+        }
+        return ptr;
+    }
+    ~HostBuf() { if (ptr) (void)hipHostFree(ptr); }
+};
+
+}  // namespace opk

@@ -1,0 +1,253 @@
+// api.cpp -- C-ABI (include/opk.h): context, memory, resizeAndMerge, NMS, PAF scores, connector.
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "../../../include/opk.h"
+#include "connector.h"
+#include "context.h"
+
+namespace opk {
+
+static thread_local std::string g_error;
+void set_error(const std::string& msg) { g_error = msg; }
+
+template <class F>
+static int guarded(F&& f)
+{
+    try {
+        f();
+        return OPK_OK;
+    } catch (const Error& e) {
+        set_error(e.what());
+        return e.code;
+    } catch (const std::exception& e) {
+        set_error(e.what());
+        return OPK_ERR_STATE;
+    }
+}
+
+}  // namespace opk
+
+using opk::Context;
+using opk::guarded;
+
+struct opk_ctx : Context {};
+
+extern "C" {
+
+const char* opk_last_error(void) { return opk::g_error.c_str(); }
+int opk_version(void) { return 1; }
+
+int opk_ctx_create(int device, void* stream, opk_ctx** out)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(out != nullptr, "out is NULL");
+        int n = 0;
+        OPK_HIP(hipGetDeviceCount(&n));
+        OPK_CHECK_ARG(device >= 0 && device < n, "device " + std::to_string(device) + " of " +
+                                                     std::to_string(n));
+        auto* c = new opk_ctx();
+        c->device = device;
+        c->bind();
+        if (stream) {
+            c->stream = static_cast<hipStream_t>(stream);
+        } else {
+            OPK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+            c->owns_stream = true;
+        }
+        *out = c;
+    });
+}
+
+int opk_ctx_destroy(opk_ctx* ctx)
+{
+    return guarded([&] {
+        if (!ctx) return;
+        ctx->bind();
+        if (ctx->owns_stream) (void)hipStreamDestroy(ctx->stream);
+        delete ctx;
+    });
+}
+
+int opk_ctx_stream(opk_ctx* ctx, void** s)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx && s, "NULL argument");
+        *s = ctx->stream;
+    });
+}
+
+int opk_sync(opk_ctx* ctx)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx, "NULL ctx");
+        ctx->bind();
+        OPK_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+int opk_malloc(opk_ctx* ctx, void** p, size_t bytes)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx && p, "NULL argument");
+        ctx->bind();
+        OPK_HIP(hipMalloc(p, bytes ? bytes : 1));
+    });
+}
+
+int opk_free(opk_ctx* ctx, void* p)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx, "NULL ctx");
+        ctx->bind();
+        if (p) OPK_HIP(hipFree(p));
+    });
+}
+
+int opk_memset(opk_ctx* ctx, void* p, int v, size_t bytes)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx && p, "NULL argument");
+        ctx->bind();
+        OPK_HIP(hipMemsetAsync(p, v, bytes, ctx->stream));
+    });
+}
+
+int opk_memcpy_h2d(opk_ctx* ctx, void* dst, const void* src, size_t bytes)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx && dst && src, "NULL argument");
+        ctx->bind();
+        OPK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+        OPK_HIP(hipStreamSynchronize(ctx->stream));   // caller may free src on return
+    });
+}
+
+int opk_memcpy_d2h(opk_ctx* ctx, void* dst, const void* src, size_t bytes)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx && dst && src, "NULL argument");
+        ctx->bind();
+        OPK_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+        OPK_HIP(hipStreamSynchronize(ctx->stream));
+    });
+}
+
+// resizeAndMergeCpu sanity checks (resizeAndMergeBase.cpp:21-41) + the batched HIP kernel
+int opk_resize_and_merge(opk_ctx* ctx, float* target, const float* const* sources, int nsrc,
+                         const int ts[4], const int* ss, const float* scale_ratios)
+{
+    (void)scale_ratios;   // unused by the CPU-path semantics (resizeAndMergeBase.cpp:18)
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx && target && sources && ts && ss, "NULL argument");
+        OPK_CHECK_ARG(nsrc >= 1, "sourceSizes cannot be empty.");
+        OPK_CHECK_ARG(nsrc <= opk::kMaxResizeSources, "at most 8 scales");
+        ctx->bind();
+        opk::ResizeSource rs[opk::kMaxResizeSources];
+        for (int i = 0; i < nsrc; ++i) {
+            const int* s = ss + 4 * i;
+            OPK_CHECK_ARG(s[0] == ts[0] && s[1] == ts[1],
+                          "source " + std::to_string(i) + " frames/channels differ from target");
+            OPK_CHECK_ARG(sources[i] != nullptr && s[2] > 0 && s[3] > 0, "empty source");
+            const auto& t = ctx->tables(s[2], s[3], ts[2], ts[3]);
+            rs[i] = opk::ResizeSource{sources[i], s[2], s[3], t.yofs, t.ycoef, t.xofs, t.xcoef};
+        }
+        opk::launch_resize_merge(target, rs, nsrc, ts[0] * ts[1], ts[2], ts[3], ctx->stream);
+    });
+}
+
+// nmsCpu sanity checks (nmsBase.cpp:116-122) + the batched HIP kernel
+int opk_nms(opk_ctx* ctx, float* target, int* kernel_scratch, const float* source, float th,
+            const int ts[4], const int ss[4], float offx, float offy)
+{
+    (void)kernel_scratch;
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx && target && source && ts && ss, "NULL argument");
+        OPK_CHECK_ARG(!(th < 0 || th > 1.0), "threshold value invalid.");
+        OPK_CHECK_ARG(ts[0] == ss[0], "frame count of target and source differ");
+        OPK_CHECK_ARG(ts[3] == 3, "target peak vector must be 3 (x, y, score)");
+        OPK_CHECK_ARG(ts[1] <= ss[1], "more target parts than source channels");
+        ctx->bind();
+        opk::launch_nms(target, source, ts[0], ss[1], ts[1], ss[2], ss[3], ts[2], th, offx, offy,
+                        ctx->stream);
+    });
+}
+
+int opk_paf_scores(opk_ctx* ctx, float* pair_scores, const float* heat, const float* peaks,
+                   int frames, int pose_model, int heat_channels, int heat_h, int heat_w,
+                   int max_peaks, float inter_th, float inter_min_above, float default_nms_th)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx && pair_scores && heat && peaks, "NULL argument");
+        const auto& m = opk::pose_model(pose_model);
+        OPK_CHECK_ARG(heat_channels >= m.heat_channels(), "too few heat-map channels");
+        ctx->bind();
+        const auto& t = ctx->pose_table(pose_model);
+        const double near = std::sqrt((double)(heat_w * heat_h)) / 150;
+        const float reject = float(default_nms_th + 1e-6);
+        opk::launch_paf_scores(pair_scores, heat, peaks, frames, heat_channels, heat_h, heat_w,
+                               max_peaks, t, inter_th, inter_min_above, reject, near, ctx->stream);
+    });
+}
+
+int opk_assemble_people(float* kp_out, float* ks_out, int max_people, int* num_people,
+                        const float* pair_scores, const float* peaks, int pose_model,
+                        int max_peaks, int min_cnt, float min_score, float scale, int maxpos)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(pair_scores && peaks && num_people, "NULL argument");
+        const auto& m = opk::pose_model(pose_model);
+        opk::PairScores ps;
+        ps.data = pair_scores;
+        ps.max_peaks = max_peaks;
+        opk::ConnectParams p{min_cnt, min_score, scale, maxpos != 0};
+        std::vector<float> kp, ks;
+        const int n = opk::assemble_people(m, peaks, max_peaks, ps, p, kp, ks);
+        *num_people = n;
+        const int w = std::min(n, max_people);
+        if (w > 0 && kp_out) std::memcpy(kp_out, kp.data(), sizeof(float) * (size_t)w * m.parts * 3);
+        if (w > 0 && ks_out) std::memcpy(ks_out, ks.data(), sizeof(float) * w);
+    });
+}
+
+int opk_connect_body_parts(opk_ctx* ctx, float* kp_out, float* ks_out, int max_people,
+                           int* num_people, const float* heat, const float* peaks_dev,
+                           int pose_model, int heat_channels, int heat_h, int heat_w,
+                           int max_peaks, float inter_min_above, float inter_th, int min_cnt,
+                           float min_score, float nms_th, float scale, int maxpos)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx && heat && peaks_dev && num_people, "NULL argument");
+        const auto& m = opk::pose_model(pose_model);
+        OPK_CHECK_ARG(heat_channels >= m.heat_channels(), "too few heat-map channels");
+        ctx->bind();
+        const size_t score_floats = (size_t)m.npairs() * max_peaks * max_peaks;
+        const size_t peak_floats = (size_t)m.parts * (max_peaks + 1) * 3;
+        auto* dscores = static_cast<float*>(ctx->scratch_scores.get(score_floats * sizeof(float)));
+        const auto& t = ctx->pose_table(pose_model);
+        const double near = std::sqrt((double)(heat_w * heat_h)) / 150;
+        opk::launch_paf_scores(dscores, heat, peaks_dev, 1, heat_channels, heat_h, heat_w,
+                               max_peaks, t, inter_th, inter_min_above, float(nms_th + 1e-6),
+                               near, ctx->stream);
+        auto* hpk = static_cast<float*>(ctx->host_peaks.get(peak_floats * sizeof(float)));
+        auto* hsc = static_cast<float*>(ctx->host_scores.get(score_floats * sizeof(float)));
+        OPK_HIP(hipMemcpyAsync(hpk, peaks_dev, peak_floats * sizeof(float), hipMemcpyDeviceToHost,
+                               ctx->stream));
+        OPK_HIP(hipMemcpyAsync(hsc, dscores, score_floats * sizeof(float), hipMemcpyDeviceToHost,
+                               ctx->stream));
+        OPK_HIP(hipStreamSynchronize(ctx->stream));
+        opk::PairScores ps;
+        ps.data = hsc;
+        ps.max_peaks = max_peaks;
+        opk::ConnectParams p{min_cnt, min_score, scale, maxpos != 0};
+        std::vector<float> kp, ks;
+        const int n = opk::assemble_people(m, hpk, max_peaks, ps, p, kp, ks);
+        *num_people = n;
+        const int w = std::min(n, max_people);
+        if (w > 0 && kp_out) std::memcpy(kp_out, kp.data(), sizeof(float) * (size_t)w * m.parts * 3);
+        if (w > 0 && ks_out) std::memcpy(ks_out, ks.data(), sizeof(float) * w);
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,40 @@
+// context.h -- per-GPU-thread context behind opk_ctx (internal).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <memory>
+#include <tuple>
+#include <vector>
+
+#include "../common.h"
+#include "../kernels/kernels.h"
+#include "pose_model.h"
+
+namespace opk {
+
+// OpenCV-style cubic tables for one (source size -> target size) axis (host/resize_tables.cpp)
+void cubic_tables(int s, int d, int* ofs, float* coef);
+
+struct Context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool owns_stream = false;
+
+    // device copies of cubic tables, keyed by (sh, sw, dh, dw)
+    struct Tables { DevBuf buf; const int* yofs; const float* ycoef; const int* xofs; const float* xcoef; };
+    std::map<std::tuple<int, int, int, int>, std::unique_ptr<Tables>> resize_tables;
+    const Tables& tables(int sh, int sw, int dh, int dw);
+
+    // device pose tables for the PAF kernel
+    struct PoseDev { DevBuf buf; PafPairTable t; };
+    std::map<int, std::unique_ptr<PoseDev>> pose_dev;
+    const PafPairTable& pose_table(int model);
+
+    DevBuf scratch_scores;   // dense pair scores for opk_connect_body_parts
+    HostBuf host_peaks, host_scores;
+
+    void bind() const { OPK_HIP(hipSetDevice(device)); }
+};
+
+}  // namespace opk

@@ -1,0 +1,53 @@
+// kernels.h -- launchers of the gfx950 kernels in this directory (internal to libopk_hip.so).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace opk {
+
+// ---- resize (resize.hip) -------------------------------------------------------------------
+// One source of a resize/merge: [planes][sh][sw] fp32 and its cubic tables on device.
+struct ResizeSource {
+    const float* src;
+    int sh, sw;
+    const int* yofs;     // [dh]
+    const float* ycoef;  // [dh][4]
+    const int* xofs;     // [dw]
+    const float* xcoef;  // [dw][4]
+};
+constexpr int kMaxResizeSources = 8;
+// dst [planes][dh][dw]; planes = frames * channels; all sources share the plane count.
+void launch_resize_merge(float* dst, const ResizeSource* srcs, int nsrc, int planes, int dh,
+                         int dw, hipStream_t stream);
+
+// ---- NMS (nms.hip) ----------------------------------------------------------------------------
+// peaks [frames][parts][maxPeaks1][3]; heat [frames][channels][h][w]
+void launch_nms(float* peaks, const float* heat, int frames, int channels, int parts, int h, int w,
+                int max_peaks1, float threshold, float offx, float offy, hipStream_t stream);
+
+// ---- PAF scores (paf.hip) --------------------------------------------------------------------
+struct PafPairTable {
+    int npairs;
+    int nparts;
+    const int* pairs;    // device [2*npairs] (part A, part B)
+    const int* mapx;     // device [npairs] heat channel of the x PAF
+    const int* mapy;     // device [npairs]
+};
+// dense: scores [frames][npairs][maxPeaks][maxPeaks]
+void launch_paf_scores(float* scores, const float* heat, const float* peaks, int frames,
+                       int heat_channels, int h, int w, int max_peaks, const PafPairTable& t,
+                       float inter_th, float inter_min_above, float reject_score,
+                       double near_dist, hipStream_t stream);
+// compact: per frame a record of `rec_floats` floats: [0] = number of scores (or -1 when it did
+// not fit), then the nA*nB scores of pair 0, pair 1, ... (row-major i, j).
+void launch_paf_scores_compact(float* records, int rec_floats, const float* heat,
+                               const float* peaks, int frames, int heat_channels, int h, int w,
+                               int max_peaks, const PafPairTable& t, float inter_th,
+                               float inter_min_above, float reject_score, double near_dist,
+                               hipStream_t stream);
+
+// ---- elementwise helpers (misc.hip) -----------------------------------------------------------
+void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stream);
+
+}  // namespace opk

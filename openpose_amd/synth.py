@@ -1,0 +1,124 @@
+"""Synthetic BODY_25 inputs: people overlays (heatmaps + PAFs), net input frames, weights.
+
+There are no trained weights or datasets in this environment, so every workload is
+synthetic and deterministic in a seed:
+
+* ``people(n, h, w, seed)``      -- n skeletons in BODY_25 layout inside an h x w map
+* ``render_field(...)``          -- net-output-like field [78, h, w]: 25 Gaussian heatmaps, the
+  background channel, and 26 unit-vector PAF strips, laid out exactly as the reference's
+  net_output blob (heatmaps, background, PAFs indexed by POSE_MAP_INDEX;
+  /root/reference/src/openpose/pose/poseParameters.cpp:253-256, bodyPartConnectorBase.cpp:299-302)
+* ``he_weights(layers, seed)``   -- per-layer seeded He-normal conv weights, zero bias, PReLU 0.25
+"""
+import numpy as np
+
+from .pose_tables import BODY25_PAIRS, BODY25_MAP_IDX
+
+# approximate BODY_25 skeleton in a unit-height box centred on the mid hip (x right, y down)
+_TEMPLATE = np.array([
+    (0.00, -0.42), (0.00, -0.32), (-0.12, -0.31), (-0.16, -0.15), (-0.18, 0.00),
+    (0.12, -0.31), (0.16, -0.15), (0.18, 0.00), (0.00, 0.02), (-0.07, 0.02),
+    (-0.08, 0.24), (-0.08, 0.45), (0.07, 0.02), (0.08, 0.24), (0.08, 0.45),
+    (-0.03, -0.45), (0.03, -0.45), (-0.06, -0.43), (0.06, -0.43), (0.11, 0.50),
+    (0.13, 0.49), (0.07, 0.47), (-0.11, 0.50), (-0.13, 0.49), (-0.07, 0.47)], np.float64)
+
+
+def people(n, h, w, seed, min_height=0.35, max_height=0.9):
+    """n random skeletons [n, 25, 2] (x, y) in pixel units of an h x w map."""
+    rng = np.random.default_rng(seed)
+    out = np.zeros((n, 25, 2), np.float64)
+    for p in range(n):
+        ph = h * rng.uniform(min_height, max_height) / max(1.0, np.sqrt(n) / 2)
+        cx = rng.uniform(0.1 * w, 0.9 * w)
+        cy = rng.uniform(0.3 * h, 0.7 * h)
+        pts = _TEMPLATE * ph + (cx, cy)
+        pts += rng.normal(0, ph * 0.01, pts.shape)
+        out[p] = pts
+    return out
+
+
+def render_field(skeletons, h, w, sigma, paf_width, background=True):
+    """Render [78, h, w] float32 (BODY_25 net_output layout) from skeletons [n, 25, 2]."""
+    field = np.zeros((78, h, w), np.float32)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    rad = int(np.ceil(4 * sigma))
+    for sk in skeletons:
+        for k in range(25):
+            x, y = sk[k]
+            x0, x1 = max(0, int(x) - rad), min(w, int(x) + rad + 2)
+            y0, y1 = max(0, int(y) - rad), min(h, int(y) + rad + 2)
+            if x0 >= x1 or y0 >= y1:
+                continue
+            d2 = (xx[y0:y1, x0:x1] - x) ** 2 + (yy[y0:y1, x0:x1] - y) ** 2
+            g = np.exp(-d2 / (2 * sigma * sigma)).astype(np.float32)
+            np.maximum(field[k, y0:y1, x0:x1], g, out=field[k, y0:y1, x0:x1])
+    if background:
+        field[25] = 1.0 - field[:25].max(axis=0)
+    count = np.zeros((26, h, w), np.float32)
+    for sk in skeletons:
+        for q in range(26):
+            a, b = sk[BODY25_PAIRS[2 * q]], sk[BODY25_PAIRS[2 * q + 1]]
+            v = b - a
+            length = float(np.hypot(*v))
+            if length < 1e-6:
+                continue
+            u = v / length
+            x0 = max(0, int(min(a[0], b[0]) - paf_width - 1))
+            x1 = min(w, int(max(a[0], b[0]) + paf_width + 2))
+            y0 = max(0, int(min(a[1], b[1]) - paf_width - 1))
+            y1 = min(h, int(max(a[1], b[1]) + paf_width + 2))
+            if x0 >= x1 or y0 >= y1:
+                continue
+            px = xx[y0:y1, x0:x1] - a[0]
+            py = yy[y0:y1, x0:x1] - a[1]
+            along = px * u[0] + py * u[1]
+            across = np.abs(px * u[1] - py * u[0])
+            m = (along >= 0) & (along <= length) & (across <= paf_width)
+            cx = 26 + BODY25_MAP_IDX[2 * q]
+            cy = 26 + BODY25_MAP_IDX[2 * q + 1]
+            field[cx, y0:y1, x0:x1][m] += u[0]
+            field[cy, y0:y1, x0:x1][m] += u[1]
+            count[q, y0:y1, x0:x1][m] += 1
+    for q in range(26):
+        c = np.maximum(count[q], 1)
+        field[26 + BODY25_MAP_IDX[2 * q]] /= c
+        field[26 + BODY25_MAP_IDX[2 * q + 1]] /= c
+    return field
+
+
+def overlay(n_people, h, w, seed):
+    """Net-output-resolution overlay: sigma 1 px Gaussians, 1 px PAF strips."""
+    return render_field(people(n_people, h, w, seed), h, w, sigma=1.0, paf_width=1.0)
+
+
+def fnv1a(name):
+    h = 0xcbf29ce484222325
+    for ch in name.encode():
+        h ^= ch
+        h = (h * 0x100000001b3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def he_weights(layers, seed=0, out_scale=1.0):
+    """Seeded He-normal weights per conv layer: {name: (w [co,ci,k,k], bias [co], slope [co]|None)}.
+
+    ``layers`` is the list of layer dicts of ``openpose_amd.graph`` (or oracle.body25).  The seed of
+    a layer is FNV-1a(layer name) ^ seed.  ``out_scale`` multiplies the weights of the last conv of
+    every stage (the Mconv7 layers) -- used to keep the synthetic net output small so a people
+    overlay dominates post-processing.
+    """
+    params = {}
+    slopes = {l["bottom"][0]: True for l in layers if l["type"] == "PReLU"}
+    for l in layers:
+        if l["type"] != "Convolution":
+            continue
+        rng = np.random.default_rng(fnv1a(l["name"]) ^ seed)
+        co, ci, k = l["num_output"], l["cin"], l["kernel_size"]
+        std = np.sqrt(2.0 / (ci * k * k))
+        wt = rng.normal(0.0, std, (co, ci, k, k)).astype(np.float32)
+        if l["name"].startswith("Mconv7"):
+            wt *= np.float32(out_scale)
+        b = np.zeros(co, np.float32)
+        s = np.full(co, 0.25, np.float32) if l["top"][0] in slopes else None
+        params[l["name"]] = (wt, b, s)
+    return params

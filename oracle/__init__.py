@@ -1,0 +1,203 @@
+"""CPU oracle for the OpenPose BODY_25 hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this package, and
+only as the checker or the timed CPU baseline.  The product (libopk_hip.so / openpose_amd) never
+imports it.  See oracle/oracle.h for what each function restates and its pinning status:
+the connector is pinned against the reference's own compiled code (oracle/_ref); NMS, the OpenCV
+bicubic resize and the Caffe layers are "parity unpinned" restatements (their reference code needs
+OpenCV / Caffe, which this image does not have).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+_REF = None
+
+_f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+_i32p = np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")
+_i = ctypes.c_int
+_f = ctypes.c_float
+
+
+def build(ref=True):
+    """Compile liboracle.so (and oracle/_ref when /root/reference exists)."""
+    subprocess.run(["make", "-s", "-C", _HERE, "all"], check=True)
+    if ref and os.path.isdir("/root/reference"):
+        subprocess.run(["make", "-s", "-C", _HERE, "ref"], check=True)
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build(ref=False)
+        L = ctypes.CDLL(path)
+        L.orc_nms.argtypes = [_f32p, _f32p, _f, _i, _i, _i, _i, _f, _f]
+        L.orc_resize_cubic.argtypes = [_f32p, _f32p, _i, _i, _i, _i]
+        L.orc_resize_merge.argtypes = [_f32p, ctypes.POINTER(ctypes.c_void_p), _i, _i, _i32p, _i, _i]
+        L.orc_cubic_tables.argtypes = [_i, _i, _i32p, _f32p]
+        L.orc_paf_score.restype = _f
+        L.orc_paf_score.argtypes = [_f32p, _f32p, _f32p, _f32p, _i, _i, _f, _f, _f]
+        L.orc_connect_body_parts.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _i, _f,
+                                             _f, _i, _f, _f, _f, _i]
+        L.orc_connect_from_scores.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _f, _f, _i]
+        L.orc_connect_gpu_semantics.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _f, _f,
+                                                _i]
+        L.orc_conv2d.argtypes = [_f32p, _f32p, _f32p, _f32p, _i, _i, _i, _i, _i, _i, _i, _i]
+        L.orc_prelu.argtypes = [_f32p, _f32p, _i, _i, _i]
+        L.orc_relu.argtypes = [_f32p, ctypes.c_long]
+        L.orc_maxpool.argtypes = [_f32p, _f32p, _i, _i, _i, _i, _i, _i, _i, _i]
+        _LIB = L
+    return _LIB
+
+
+def ref_lib():
+    """The reference's own connector (compiled from /root/reference), or None if unavailable."""
+    global _REF
+    if _REF is None:
+        path = os.path.join(_HERE, "_ref", "libref_connector.so")
+        if not os.path.exists(path):
+            if not os.path.isdir("/root/reference"):
+                return None
+            build(ref=True)
+        R = ctypes.CDLL(path, mode=os.RTLD_LAZY)  # OpenCV-only symbols stay unresolved
+        R.ref_connect_cpu.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _i, _f, _f, _i,
+                                      _f, _f, _f, _i]
+        _REF = R
+    return _REF
+
+
+# ---- numpy front ends -------------------------------------------------------------------------
+def nms(heat, threshold, max_peaks1=128, offset=(0.0, 0.0), channels=25):
+    heat = np.ascontiguousarray(heat, np.float32)
+    c, h, w = heat.shape
+    channels = min(channels, c)
+    out = np.zeros((channels, max_peaks1, 3), np.float32)
+    lib().orc_nms(out, heat, threshold, channels, max_peaks1, h, w, offset[0], offset[1])
+    return out
+
+
+def resize_cubic(src, dh, dw):
+    src = np.ascontiguousarray(src, np.float32)
+    out = np.empty((dh, dw), np.float32)
+    lib().orc_resize_cubic(out, src, src.shape[0], src.shape[1], dh, dw)
+    return out
+
+
+def resize_merge(srcs, dh, dw):
+    """srcs: list of [C, h_i, w_i] arrays -> [C, dh, dw] (resizeAndMergeCpu semantics)."""
+    srcs = [np.ascontiguousarray(s, np.float32) for s in srcs]
+    c = srcs[0].shape[0]
+    out = np.empty((c, dh, dw), np.float32)
+    ptrs = (ctypes.c_void_p * len(srcs))(*[s.ctypes.data for s in srcs])
+    hw = np.array([[s.shape[1], s.shape[2]] for s in srcs], np.int32).ravel()
+    lib().orc_resize_merge(out, ptrs, len(srcs), c, hw, dh, dw)
+    return out
+
+
+def cubic_tables(s, d):
+    ofs = np.empty(d, np.int32)
+    coef = np.empty((d, 4), np.float32)
+    lib().orc_cubic_tables(s, d, ofs, coef)
+    return ofs, coef
+
+
+def _connect_args(params):
+    p = dict(inter_min_above=0.95, inter_th=0.05, min_subset_cnt=3, min_subset_score=0.4,
+             nms_th=0.05, scale=1.0, maximize_positives=False, pose_model=0, max_people=512)
+    p.update(params)
+    return p
+
+
+def connect(heat, peaks, use_reference=False, **params):
+    """connectBodyPartsCpu semantics -> (keypoints [P, parts, 3], scores [P])."""
+    p = _connect_args(params)
+    heat = np.ascontiguousarray(heat, np.float32)
+    peaks = np.ascontiguousarray(peaks, np.float32)
+    nparts = peaks.shape[0]
+    kp = np.zeros((p["max_people"], nparts, 3), np.float32)
+    ks = np.zeros(p["max_people"], np.float32)
+    fn = ref_lib().ref_connect_cpu if use_reference else lib().orc_connect_body_parts
+    n = fn(kp, ks, p["max_people"], heat, peaks, p["pose_model"], heat.shape[2], heat.shape[1],
+           peaks.shape[1] - 1, p["inter_min_above"], p["inter_th"], p["min_subset_cnt"],
+           p["min_subset_score"], p["nms_th"], p["scale"], int(p["maximize_positives"]))
+    if n < 0:
+        raise RuntimeError("oracle connector rejected the model")
+    n = min(n, p["max_people"])
+    return kp[:n].copy(), ks[:n].copy()
+
+
+def connect_from_scores(pair_scores, peaks, gpu_semantics=False, **params):
+    p = _connect_args(params)
+    pair_scores = np.ascontiguousarray(pair_scores, np.float32)
+    peaks = np.ascontiguousarray(peaks, np.float32)
+    nparts = peaks.shape[0]
+    kp = np.zeros((p["max_people"], nparts, 3), np.float32)
+    ks = np.zeros(p["max_people"], np.float32)
+    fn = lib().orc_connect_gpu_semantics if gpu_semantics else lib().orc_connect_from_scores
+    n = fn(kp, ks, p["max_people"], pair_scores, peaks, p["pose_model"], peaks.shape[1] - 1,
+           p["min_subset_cnt"], p["min_subset_score"], p["scale"], int(p["maximize_positives"]))
+    n = min(n, p["max_people"])
+    return kp[:n].copy(), ks[:n].copy()
+
+
+def paf_score(a, b, mapx, mapy, inter_th=0.05, inter_min_above=0.95, nms_th=0.05):
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    mapx = np.ascontiguousarray(mapx, np.float32)
+    mapy = np.ascontiguousarray(mapy, np.float32)
+    return lib().orc_paf_score(a, b, mapx, mapy, mapx.shape[1], mapx.shape[0], inter_th,
+                               inter_min_above, nms_th)
+
+
+def pair_scores(heat, peaks, pairs, map_idx, nparts=25, **kw):
+    """Full [npairs, maxPeaks, maxPeaks] score table via getScoreAB (0 for absent peaks)."""
+    mp = peaks.shape[1] - 1
+    npairs = len(pairs) // 2
+    out = np.zeros((npairs, mp, mp), np.float32)
+    for q in range(npairs):
+        pa, pb = pairs[2 * q], pairs[2 * q + 1]
+        na, nb = int(peaks[pa, 0, 0] + 0.5), int(peaks[pb, 0, 0] + 0.5)
+        mx = heat[nparts + 1 + map_idx[2 * q]]
+        my = heat[nparts + 1 + map_idx[2 * q + 1]]
+        for i in range(na):
+            for j in range(nb):
+                out[q, i, j] = paf_score(peaks[pa, i + 1], peaks[pb, j + 1], mx, my, **kw)
+    return out
+
+
+# ---- Caffe layers -----------------------------------------------------------------------------
+def conv2d(x, w, b, pad, nthreads=None):
+    x = np.ascontiguousarray(x, np.float32)
+    w = np.ascontiguousarray(w, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    n, ci, h, wd = x.shape
+    co, _, k, _ = w.shape
+    out = np.empty((n, co, h, wd), np.float32)
+    lib().orc_conv2d(out, x, w, b, n, ci, h, wd, co, k, pad, nthreads or os.cpu_count() or 1)
+    return out
+
+
+def prelu(x, slope):
+    n, c, h, w = x.shape
+    lib().orc_prelu(x, np.ascontiguousarray(slope, np.float32), n, c, h * w)
+    return x
+
+
+def relu(x):
+    lib().orc_relu(x, x.size)
+    return x
+
+
+def maxpool(x, k=2, s=2):
+    n, c, h, w = x.shape
+    oh = -(-(h - k) // s) + 1
+    ow = -(-(w - k) // s) + 1
+    out = np.empty((n, c, oh, ow), np.float32)
+    lib().orc_maxpool(out, np.ascontiguousarray(x), n, c, h, w, k, s, oh, ow)
+    return out

@@ -1,0 +1,100 @@
+/*
+ * oracle.h -- CPU oracle for the OpenPose BODY_25 hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing under oracle/ is part of the product: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load liboracle.so, and only as
+ * the checker / the timed CPU baseline.  The product path (libopk_hip.so) never links it.
+ *
+ * Every function restates the reference CPU path (CPU_ONLY build) of zengjianping/openpose.
+ * Citations are to /root/reference/<file>:<line>.
+ *
+ * Pinning status (see DESIGN.md "Oracle"):
+ *   - connector (orc_connect_body_parts)     : pinned against the reference's own
+ *     bodyPartConnectorBase.cpp compiled from source into oracle/_ref (tests/test_oracle_ref.py)
+ *   - NMS (orc_nms)                          : parity unpinned (nmsBase.cpp needs OpenCV headers,
+ *     absent from the image -> reference unbuildable here); restatement + known-answer tests
+ *   - resize (orc_resize_cubic/merge)        : parity unpinned (OpenCV cv::resize is a third-party
+ *     dependency absent from the image); restatement of OpenCV's generic float INTER_CUBIC path
+ *   - CNN layers (orc_conv2d, ...)           : parity unpinned (Caffe absent); restatement of Caffe
+ *     layer semantics, cross-checked against torch CPU fp32 in tests
+ *
+ * Float semantics: the reference CPU build uses -O3 without -march (CMakeLists.txt:103-137,
+ * INSTRUCTION_SET NONE), i.e. SSE float arithmetic, no FMA contraction.  Every file here except
+ * the GEMM is compiled with -ffp-contract=off to keep that operation order.
+ */
+#ifndef OPK_ORACLE_H
+#define OPK_ORACLE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- NMS: restates op::nmsCpu (src/openpose/net/nmsBase.cpp:109-170) ----------------------
+ * peaks   : [channels][max_peaks1][3]  (slot 0 = {count, -, -}; max_peaks1 = targetSize[2] = 128)
+ * heat    : [channels][h][w]
+ * Only the first `channels` planes of `heat` are read.                                       */
+void orc_nms(float* peaks, const float* heat, float threshold, int channels, int max_peaks1,
+             int h, int w, float offset_x, float offset_y);
+
+/* ---- bicubic resize: restates cv::resize(..., INTER_CUBIC) as called by
+ * op::resizeAndMergeCpu (src/openpose/net/resizeAndMergeBase.cpp:45-52) --------------------- */
+void orc_resize_cubic(float* dst, const float* src, int sh, int sw, int dh, int dw);
+/* multi-scale: resizeAndMergeBase.cpp:55-106 (each source to the full target, sum, average) */
+void orc_resize_merge(float* dst, const float* const* srcs, int nsrc, int channels,
+                      const int* src_hw /* nsrc*2 */, int dh, int dw);
+/* the tables the cubic resize uses (for kernel cross-checks) */
+void orc_cubic_tables(int s, int d, int* ofs /* d */, float* coef /* d*4 */);
+
+/* ---- PAF score: restates getScoreAB (src/openpose/net/bodyPartConnectorBase.cpp:12-75) ----- */
+float orc_paf_score(const float* candA, const float* candB /* (x,y,score) */,
+                    const float* mapX, const float* mapY, int hm_w, int hm_h,
+                    float inter_th, float inter_min_above, float default_nms_th);
+
+/* ---- connector: restates op::connectBodyPartsCpu (bodyPartConnectorBase.cpp:1327-1377) ------
+ * heat    : [nparts+1+2*npairs][hm_h][hm_w]   (BODY_25: 78 planes)
+ * peaks   : [nparts][max_peaks+1][3]
+ * out_keypoints: [max_people][nparts][3], out_scores [max_people]; returns number of people
+ * (or -1 on error).  If the true count exceeds max_people, only max_people rows are written
+ * but the true count is returned.
+ * pose_model: 0 = BODY_25, 1 = COCO_18, 2 = MPI_15, 3 = MPI_15_4 (enumClasses.hpp:9-30)    */
+int orc_connect_body_parts(float* out_keypoints, float* out_scores, int max_people,
+                           const float* heat, const float* peaks, int pose_model,
+                           int hm_w, int hm_h, int max_peaks, float inter_min_above,
+                           float inter_th, int min_subset_cnt, float min_subset_score,
+                           float default_nms_th, float scale_factor, int maximize_positives);
+/* same, but fed by precomputed pair scores [npairs][max_peaks][max_peaks] (the reference's
+ * alternate createPeopleVector input, bodyPartConnectorBase.cpp:321-340)                    */
+int orc_connect_from_scores(float* out_keypoints, float* out_scores, int max_people,
+                            const float* pair_scores, const float* peaks, int pose_model,
+                            int max_peaks, int min_subset_cnt, float min_subset_score,
+                            float scale_factor, int maximize_positives);
+/* GPU-path assembly (pafPtrIntoVector + pafVectorIntoPeopleVector, bodyPartConnectorBase.cpp
+ * :474-718) followed by the same threshold/array stages; used for models the CPU path rejects */
+int orc_connect_gpu_semantics(float* out_keypoints, float* out_scores, int max_people,
+                              const float* pair_scores, const float* peaks, int pose_model,
+                              int max_peaks, int min_subset_cnt, float min_subset_score,
+                              float scale_factor, int maximize_positives);
+/* pose tables (poseParameters.cpp:253-256,413-419) */
+int orc_pose_num_parts(int pose_model);
+int orc_pose_num_pairs(int pose_model);
+const unsigned* orc_pose_pairs(int pose_model);
+const unsigned* orc_pose_map_idx(int pose_model);
+
+/* ---- Caffe layer semantics for the BODY_25 prototxt (NCHW fp32, batch n) ------------------ */
+/* Convolution: cross-correlation, zero pad, stride 1, bias (Caffe ConvolutionLayer) */
+void orc_conv2d(float* out, const float* in, const float* w /* [co][ci][k][k] */,
+                const float* bias, int n, int ci, int h, int wd, int co, int k, int pad,
+                int nthreads);
+/* PReLU, per channel slope (Caffe PReLULayer, channel_shared=false) -- in place */
+void orc_prelu(float* x, const float* slope, int n, int c, int hw);
+void orc_relu(float* x, long count);
+/* MaxPool kernel k stride s, pad 0, ceil sizing (Caffe PoolingLayer) */
+void orc_maxpool(float* out, const float* in, int n, int c, int h, int w, int k, int s,
+                 int oh, int ow);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

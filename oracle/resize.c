@@ -1,0 +1,101 @@
+/*
+ * resize.c -- CPU oracle: bicubic resize + multi-scale merge (TEST INFRASTRUCTURE, see oracle.h).
+ *
+ * Reference call sites: /root/reference/src/openpose/net/resizeAndMergeBase.cpp
+ *   :45-52   single scale: per channel cv::resize(src, dst, {W,H}, 0, 0, CV_INTER_CUBIC)
+ *   :55-106  multi-scale: resize every source to the full target, add into scale 0, then /= N
+ * The arithmetic lives in OpenCV (third-party, absent from this image; Ubuntu libopencv-dev 4.2 per
+ * .github/workflows/main.yml:58-72).  Restated here: OpenCV's generic float INTER_CUBIC path
+ *   scale = 1 / ((double)dsize / ssize);  f = (float)((d + 0.5) * scale - 0.5);  s0 = floor(f);
+ *   t = f - s0;  taps s0-1 .. s0+2 clamped to the image (BORDER_REPLICATE);
+ *   coefficients: Keys cubic with A = -0.75 (interpolateCubic);
+ *   horizontal pass first (one row buffer per source row), then vertical.
+ * Summation order: taps left to right (t0 + t1) + t2) + t3, horizontal then vertical.  OpenCV's
+ * SSE vertical kernel may sum in a different order (<= 2 ulp difference): parity with OpenCV
+ * itself is therefore unpinned; the HIP kernel matches THIS restatement bit for bit.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include "oracle.h"
+
+static void keys_cubic(float x, float c[4])
+{
+    const float A = -0.75f;
+    c[0] = ((A * (x + 1) - 5 * A) * (x + 1) + 8 * A) * (x + 1) - 4 * A;
+    c[1] = ((A + 2) * x - (A + 3)) * x * x + 1;
+    c[2] = ((A + 2) * (1 - x) - (A + 3)) * (1 - x) * (1 - x) + 1;
+    c[3] = 1.f - c[0] - c[1] - c[2];
+}
+
+void orc_cubic_tables(int s, int d, int* ofs, float* coef)
+{
+    const double scale = 1. / ((double)d / s);
+    for (int i = 0; i < d; ++i) {
+        float f = (float)((i + 0.5) * scale - 0.5);
+        const int s0 = (int)floorf(f);
+        f -= (float)s0;
+        ofs[i] = s0;
+        keys_cubic(f, coef + 4 * i);
+    }
+}
+
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+void orc_resize_cubic(float* dst, const float* src, int sh, int sw, int dh, int dw)
+{
+    int* xo = (int*)malloc(sizeof(int) * dw);
+    int* yo = (int*)malloc(sizeof(int) * dh);
+    float* xa = (float*)malloc(sizeof(float) * 4 * dw);
+    float* yb = (float*)malloc(sizeof(float) * 4 * dh);
+    float* rows = (float*)malloc(sizeof(float) * 4 * dw);
+    orc_cubic_tables(sw, dw, xo, xa);
+    orc_cubic_tables(sh, dh, yo, yb);
+    for (int y = 0; y < dh; ++y) {
+        for (int k = 0; k < 4; ++k) {
+            const float* srow = src + (long)clampi(yo[y] - 1 + k, 0, sh - 1) * sw;
+            float* r = rows + (long)k * dw;
+            for (int x = 0; x < dw; ++x) {
+                const float* a = xa + 4 * x;
+                const int b = xo[x] - 1;
+                r[x] = srow[clampi(b, 0, sw - 1)] * a[0] + srow[clampi(b + 1, 0, sw - 1)] * a[1]
+                     + srow[clampi(b + 2, 0, sw - 1)] * a[2] + srow[clampi(b + 3, 0, sw - 1)] * a[3];
+            }
+        }
+        const float* be = yb + 4 * y;
+        float* o = dst + (long)y * dw;
+        for (int x = 0; x < dw; ++x)
+            o[x] = rows[x] * be[0] + rows[dw + x] * be[1] + rows[2 * dw + x] * be[2]
+                 + rows[3 * dw + x] * be[3];
+    }
+    free(xo); free(yo); free(xa); free(yb); free(rows);
+}
+
+void orc_resize_merge(float* dst, const float* const* srcs, int nsrc, int channels,
+                      const int* src_hw, int dh, int dw)
+{
+    const long tplane = (long)dh * dw;
+    if (nsrc == 1) {
+        const long splane = (long)src_hw[0] * src_hw[1];
+        for (int c = 0; c < channels; ++c)
+            orc_resize_cubic(dst + c * tplane, srcs[0] + c * splane, src_hw[0], src_hw[1], dh, dw);
+        return;
+    }
+    float* tmp = (float*)malloc(sizeof(float) * tplane);
+    for (int n = 0; n < nsrc; ++n) {
+        const long splane = (long)src_hw[2 * n] * src_hw[2 * n + 1];
+        for (int c = 0; c < channels; ++c) {
+            float* acc = dst + c * tplane;
+            if (n == 0) {
+                orc_resize_cubic(acc, srcs[0] + c * splane, src_hw[0], src_hw[1], dh, dw);
+            } else {
+                orc_resize_cubic(tmp, srcs[n] + c * splane, src_hw[2 * n], src_hw[2 * n + 1], dh, dw);
+                for (long i = 0; i < tplane; ++i) acc[i] = tmp[i] + acc[i];    /* cv::add */
+            }
+        }
+    }
+    /* Mat /= N  ->  convertTo(alpha = 1/N): float multiply by (float)(1./N) */
+    const float inv = (float)(1. / (double)nsrc);
+    for (long i = 0; i < (long)channels * tplane; ++i) dst[i] = dst[i] * inv;
+    free(tmp);
+}
