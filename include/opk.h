@@ -39,8 +39,11 @@ int opk_version(void);
 /* ---- context: one per GPU worker thread (reference: one PoseExtractorCaffe per GPU thread,
  *      wrapperAuxiliary.hpp:328-337; device bound at init like Caffe::SetDevice, netCaffe.cpp:169) */
 typedef struct opk_ctx opk_ctx;
-int opk_ctx_create(int device, void* hip_stream /* NULL: the context creates its own */,
+/* device -1: host-only context (graph planning, opk_net_conv_info; no device work) */
+int opk_ctx_create(int device, void* hip_stream /* used as given; NULL = the null stream */,
                    opk_ctx** out);
+/* same, with a private non-blocking stream owned (and destroyed) by the context */
+int opk_ctx_create_private_stream(int device, opk_ctx** out);
 int opk_ctx_destroy(opk_ctx* ctx);
 int opk_ctx_stream(opk_ctx* ctx, void** hip_stream);
 int opk_sync(opk_ctx* ctx);

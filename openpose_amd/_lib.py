@@ -22,6 +22,7 @@ _SIGS = {
     "opk_last_error": (_c.c_char_p, []),
     "opk_version": (_i, []),
     "opk_ctx_create": (_i, [_i, _p, _c.POINTER(_p)]),
+    "opk_ctx_create_private_stream": (_i, [_i, _c.POINTER(_p)]),
     "opk_ctx_destroy": (_i, [_p]),
     "opk_ctx_stream": (_i, [_p, _c.POINTER(_p)]),
     "opk_sync": (_i, [_p]),

@@ -49,6 +49,18 @@ class Context:
     def sync(self):
         check(self.L.opk_sync(self.h))
 
+    @classmethod
+    def host_only(cls):
+        """A device-less context (-1): graph planning and conv listing only."""
+        self = cls.__new__(cls)
+        self.L = _lib.load()
+        self.device = -1
+        self.torch_stream = None
+        h = ctypes.c_void_p()
+        check(self.L.opk_ctx_create(-1, None, ctypes.byref(h)))
+        self.h = h
+        return self
+
     # ---- operators ---------------------------------------------------------------------------
     def resize_and_merge(self, target, sources):
         """target [N,C,H,W] fp32 CUDA; sources list of [N,C,h,w] (resizeAndMergeGpu)."""
@@ -108,3 +120,145 @@ def assemble_people(pair_scores, peaks, pose_model=BODY_25, scale=1.0, max_peopl
                                 int(maximize_positives)))
     k = min(n.value, max_people)
     return kp[:k].copy(), ks[:k].copy()
+
+
+class Net:
+    """op::NetCaffe replacement (NetHip): prototxt path or "builtin:BODY_25"."""
+
+    def __init__(self, ctx, prototxt="builtin:BODY_25"):
+        self.ctx = ctx
+        self.L = ctx.L
+        h = ctypes.c_void_p()
+        check(self.L.opk_net_create(ctx.h, prototxt.encode(), None, ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if self.h:
+            self.L.opk_net_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def convs(self):
+        """[{name, cin, num_output, kernel_size, act}] in execution order."""
+        out = []
+        name = ctypes.create_string_buffer(64)
+        cin, cout, k, act = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        for i in range(self.L.opk_net_num_convs(self.h)):
+            check(self.L.opk_net_conv_info(self.h, i, name, ctypes.byref(cin), ctypes.byref(cout),
+                                           ctypes.byref(k), ctypes.byref(act)))
+            out.append(dict(name=name.value.decode(), cin=cin.value, num_output=cout.value,
+                            kernel_size=k.value, act=act.value))
+        return out
+
+    def set_params(self, params):
+        """params: {conv name: (w [co,ci,k,k], bias [co], slope [co] | None)} fp32 numpy."""
+        for c in self.convs():
+            w, b, s = params[c["name"]]
+            w = np.ascontiguousarray(w, np.float32)
+            b = np.ascontiguousarray(b, np.float32)
+            sp = None
+            if s is not None:
+                s = np.ascontiguousarray(s, np.float32)
+                sp = s.ctypes.data_as(ctypes.c_void_p)
+            check(self.L.opk_net_set_conv(self.h, c["name"].encode(),
+                                          w.ctypes.data_as(ctypes.c_void_p),
+                                          b.ctypes.data_as(ctypes.c_void_p), sp))
+
+    def forward(self, x):
+        """x: [n, 3, h, w] fp32 CUDA tensor. Returns (device pointer, shape) of net_output."""
+        n, c, h, w = x.shape
+        check(self.L.opk_net_forward(self.h, _ptr(x), n, h, w))
+        return self.output()
+
+    def output(self):
+        p = ctypes.c_void_p()
+        shape = (ctypes.c_int * 4)()
+        check(self.L.opk_net_output(self.h, ctypes.byref(p), shape))
+        return p.value, tuple(shape)
+
+    def output_numpy(self):
+        p, shape = self.output()
+        out = np.empty(shape, np.float32)
+        check(self.L.opk_memcpy_d2h(self.ctx.h, out.ctypes.data_as(ctypes.c_void_p),
+                                    ctypes.c_void_p(p), out.nbytes))
+        return out
+
+
+class PoseExtractor:
+    """op::PoseExtractorCaffe replacement for batches of frames (PoseHip)."""
+
+    def __init__(self, ctx, net=None, maximize_positives=False):
+        self.ctx = ctx
+        self.L = ctx.L
+        h = ctypes.c_void_p()
+        check(self.L.opk_pose_create(ctx.h, net.h if net is not None else None,
+                                     int(maximize_positives), ctypes.byref(h)))
+        self.h = h
+        self.net = net
+
+    def close(self):
+        if self.h:
+            self.L.opk_pose_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_property(self, prop, value):
+        check(self.L.opk_pose_set_property(self.h, prop, float(value)))
+
+    def set_overlay(self, overlay):
+        self._overlay = overlay   # keep the tensor alive
+        check(self.L.opk_pose_set_overlay(self.h, _ptr(overlay) if overlay is not None else None))
+
+    def forward(self, frames, producer_size):
+        n, _, h, w = frames.shape
+        check(self.L.opk_pose_forward(self.h, _ptr(frames), n, h, w, producer_size[0],
+                                      producer_size[1]))
+
+    def forward_net_output(self, net_output, net_size, producer_size):
+        """net_output: [n, 78, h, w] CUDA tensor (or (ptr, shape)); net_size = (w, h)."""
+        if isinstance(net_output, tuple):
+            ptr, shape = net_output
+            ptr = ctypes.c_void_p(ptr)
+        else:
+            ptr, shape = _ptr(net_output), net_output.shape
+        check(self.L.opk_pose_forward_net_output(self.h, ptr, shape[0], shape[2], shape[3],
+                                                 net_size[1], net_size[0], producer_size[0],
+                                                 producer_size[1]))
+
+    def num_people(self, frame):
+        return self.L.opk_pose_num_people(self.h, frame)
+
+    def keypoints(self, frame):
+        n = self.num_people(frame)
+        kp = np.zeros((max(n, 1), 25, 3), np.float32)
+        ks = np.zeros(max(n, 1), np.float32)
+        check(self.L.opk_pose_keypoints(self.h, frame, kp.ctypes.data_as(ctypes.c_void_p),
+                                        ks.ctypes.data_as(ctypes.c_void_p), n))
+        return kp[:n], ks[:n]
+
+    def scale_net_to_output(self):
+        return self.L.opk_pose_scale_net_to_output(self.h)
+
+    def _dev_array(self, fn):
+        p = ctypes.c_void_p()
+        shape = (ctypes.c_int * 4)()
+        check(fn(self.h, ctypes.byref(p), shape))
+        out = np.empty(tuple(shape), np.float32)
+        check(self.L.opk_memcpy_d2h(self.ctx.h, out.ctypes.data_as(ctypes.c_void_p), p, out.nbytes))
+        return out
+
+    def heatmaps_numpy(self):
+        return self._dev_array(self.L.opk_pose_heatmaps)
+
+    def peaks_numpy(self):
+        return self._dev_array(self.L.opk_pose_peaks)

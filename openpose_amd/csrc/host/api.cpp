@@ -39,10 +39,16 @@ extern "C" {
 const char* opk_last_error(void) { return opk::g_error.c_str(); }
 int opk_version(void) { return 1; }
 
-int opk_ctx_create(int device, void* stream, opk_ctx** out)
+static int ctx_create(int device, void* stream, bool own, opk_ctx** out)
 {
     return guarded([&] {
         OPK_CHECK_ARG(out != nullptr, "out is NULL");
+        if (device == -1 && !own) {   // host-only context
+            auto* c = new opk_ctx();
+            c->device = -1;
+            *out = c;
+            return;
+        }
         int n = 0;
         OPK_HIP(hipGetDeviceCount(&n));
         OPK_CHECK_ARG(device >= 0 && device < n, "device " + std::to_string(device) + " of " +
@@ -50,21 +56,31 @@ int opk_ctx_create(int device, void* stream, opk_ctx** out)
         auto* c = new opk_ctx();
         c->device = device;
         c->bind();
-        if (stream) {
-            c->stream = static_cast<hipStream_t>(stream);
-        } else {
+        if (own) {
             OPK_HIP(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
             c->owns_stream = true;
+        } else {
+            c->stream = static_cast<hipStream_t>(stream);
         }
         *out = c;
     });
+}
+
+int opk_ctx_create(int device, void* stream, opk_ctx** out)
+{
+    return ctx_create(device, stream, false, out);
+}
+
+int opk_ctx_create_private_stream(int device, opk_ctx** out)
+{
+    return ctx_create(device, nullptr, true, out);
 }
 
 int opk_ctx_destroy(opk_ctx* ctx)
 {
     return guarded([&] {
         if (!ctx) return;
-        ctx->bind();
+        if (ctx->device >= 0) ctx->bind();
         if (ctx->owns_stream) (void)hipStreamDestroy(ctx->stream);
         delete ctx;
     });

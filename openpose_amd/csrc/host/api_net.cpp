@@ -1,0 +1,205 @@
+// api_net.cpp -- C-ABI (include/opk.h): NetHip (op::NetCaffe) and PoseHip
+// (op::PoseExtractorCaffe) entry points.
+#include <cstring>
+#include <memory>
+#include <string>
+
+#include "../../../include/opk.h"
+#include "net.h"
+#include "pose.h"
+
+namespace opk {
+template <class F>
+static int guarded_net(F&& f)
+{
+    try {
+        f();
+        return OPK_OK;
+    } catch (const Error& e) {
+        set_error(e.what());
+        return e.code;
+    } catch (const std::exception& e) {
+        set_error(e.what());
+        return OPK_ERR_STATE;
+    }
+}
+}  // namespace opk
+
+struct opk_ctx : opk::Context {};
+struct opk_net {
+    opk_ctx* ctx;
+    std::unique_ptr<opk::NetHip> net;
+};
+struct opk_pose {
+    opk_ctx* ctx;
+    std::unique_ptr<opk::PoseHip> pose;
+};
+
+using opk::guarded_net;
+
+extern "C" {
+
+int opk_net_create(opk_ctx* ctx, const char* prototxt, const char* caffemodel, opk_net** out)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ctx && prototxt && out, "NULL argument");
+        OPK_CHECK_ARG(caffemodel == nullptr || caffemodel[0] == 0,
+                      "caffemodel loading is not implemented yet: supply weights with "
+                      "opk_net_set_conv");
+        const std::string p(prototxt);
+        std::vector<opk::LayerDesc> layers =
+            p == "builtin:BODY_25" ? opk::builtin_body25() : opk::load_prototxt(p);
+        auto* n = new opk_net{ctx, std::make_unique<opk::NetHip>(ctx, std::move(layers))};
+        *out = n;
+    });
+}
+
+int opk_net_destroy(opk_net* net)
+{
+    return guarded_net([&] {
+        if (!net) return;
+        if (net->ctx->device >= 0) net->ctx->bind();
+        delete net;
+    });
+}
+
+int opk_net_num_convs(opk_net* net)
+{
+    if (!net) return -1;
+    return (int)net->net->convs().size();
+}
+
+int opk_net_conv_info(opk_net* net, int i, char* name, int* cin, int* cout, int* k, int* act)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net && i >= 0 && i < (int)net->net->convs().size(), "bad index");
+        const auto& c = net->net->convs()[i];
+        if (name) {
+            std::strncpy(name, c.name.c_str(), 63);
+            name[63] = 0;
+        }
+        if (cin) *cin = c.cin;
+        if (cout) *cout = c.cout;
+        if (k) *k = c.k;
+        if (act) *act = c.act;
+    });
+}
+
+int opk_net_set_conv(opk_net* net, const char* name, const float* w, const float* b,
+                     const float* slope)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net && name, "NULL argument");
+        net->net->set_conv(name, w, b, slope);
+    });
+}
+
+int opk_net_forward(opk_net* net, const float* input, int n, int h, int w)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net, "NULL net");
+        net->net->forward(input, n, h, w);
+    });
+}
+
+int opk_net_output(opk_net* net, float** out, int shape[4])
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net && out && shape, "NULL argument");
+        OPK_CHECK_ARG(net->net->frames() > 0, "no forward pass yet");
+        *out = net->net->output();
+        shape[0] = net->net->frames();
+        shape[1] = net->net->out_channels();
+        shape[2] = net->net->out_h();
+        shape[3] = net->net->out_w();
+    });
+}
+
+int opk_pose_create(opk_ctx* ctx, opk_net* net, int maxpos, opk_pose** out)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ctx && out, "NULL argument");
+        *out = new opk_pose{ctx, std::make_unique<opk::PoseHip>(ctx, net ? net->net.get() : nullptr,
+                                                                maxpos != 0)};
+    });
+}
+
+int opk_pose_destroy(opk_pose* p)
+{
+    return guarded_net([&] {
+        if (!p) return;
+        if (p->ctx->device >= 0) p->ctx->bind();
+        delete p;
+    });
+}
+
+int opk_pose_set_property(opk_pose* p, int prop, double v)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->set_property(prop, v);
+    });
+}
+
+int opk_pose_forward(opk_pose* p, const float* frames, int n, int net_h, int net_w, int pw, int ph)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->forward(frames, n, net_h, net_w, pw, ph);
+    });
+}
+
+int opk_pose_forward_net_output(opk_pose* p, const float* out, int n, int oh, int ow, int net_h,
+                                int net_w, int pw, int ph)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->forward_net_output(out, n, oh, ow, net_h, net_w, pw, ph);
+    });
+}
+
+int opk_pose_set_overlay(opk_pose* p, const float* overlay)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->set_overlay(overlay);
+    });
+}
+
+int opk_pose_num_people(opk_pose* p, int frame)
+{
+    if (!p || frame < 0 || frame >= p->pose->frames()) return -1;
+    return p->pose->num_people(frame);
+}
+
+int opk_pose_keypoints(opk_pose* p, int frame, float* kp, float* ks, int max_people)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p && frame >= 0 && frame < p->pose->frames(), "bad frame");
+        const int n = std::min(max_people, p->pose->num_people(frame));
+        const auto& k = p->pose->keypoints(frame);
+        const auto& s = p->pose->scores(frame);
+        if (kp && n > 0) std::memcpy(kp, k.data(), sizeof(float) * n * 25 * 3);
+        if (ks && n > 0) std::memcpy(ks, s.data(), sizeof(float) * n);
+    });
+}
+
+int opk_pose_heatmaps(opk_pose* p, float** heat, int shape[4])
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p && heat && shape, "NULL argument");
+        *heat = p->pose->heatmaps(shape);
+    });
+}
+
+int opk_pose_peaks(opk_pose* p, float** peaks, int shape[4])
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p && peaks && shape, "NULL argument");
+        *peaks = p->pose->peaks(shape);
+    });
+}
+
+float opk_pose_scale_net_to_output(opk_pose* p) { return p ? p->pose->scale_net_to_output() : 0.f; }
+
+}  // extern "C"

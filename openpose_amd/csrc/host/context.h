@@ -34,7 +34,12 @@ struct Context {
     DevBuf scratch_scores;   // dense pair scores for opk_connect_body_parts
     HostBuf host_peaks, host_scores;
 
-    void bind() const { OPK_HIP(hipSetDevice(device)); }
+    // device < 0: host-only context (graph planning / host assembly; no device calls)
+    void bind() const
+    {
+        if (device < 0) throw Error(3, "host-only context (device -1) cannot run device work");
+        OPK_HIP(hipSetDevice(device));
+    }
 };
 
 }  // namespace opk

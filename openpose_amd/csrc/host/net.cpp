@@ -1,0 +1,333 @@
+// net.cpp -- NetHip: plans a Caffe pose graph onto padded-NHWC fp16 buffers and runs it with the
+// gfx950 kernels of kernels/conv.hip.
+//
+// Reference behaviour replaced: op::NetCaffe (src/openpose/net/netCaffe.cpp:27-279): build the
+// caffe::Net from the prototxt, load weights, reshape the input blob when the size changes
+// (:224-228), ForwardFrom(0) (:248), expose the `net_output` blob (:193-195).
+// Planning (once per graph):
+//   * ReLU/PReLU layers applied in place to a conv's top are fused into that conv's epilogue;
+//   * every Concat gets one buffer; its bottoms are written straight into their channel slices
+//     (a conv may write up to six such slices), so Concat costs nothing at run time;
+//   * the output Concat (net_output) is an fp32 NCHW buffer written by the final 1x1 convs;
+//   * the first conv (3 input channels) reads a 27-value im2col image (K = 32, one GEMM step).
+// Buffers are allocated per input shape (frames x h x w) and kept; borders stay zero.
+#include "net.h"
+
+#include <algorithm>
+#include <set>
+
+namespace opk {
+
+namespace {
+int round_up(int v, int m) { return (v + m - 1) / m * m; }
+int pick_bn(int cout)
+{
+    if (cout <= 32) return 32;
+    if (cout <= 64) return 64;
+    if (cout <= 96) return 96;
+    return 128;
+}
+}  // namespace
+
+NetHip::NetHip(Context* ctx, std::vector<LayerDesc> layers, const std::string& output_blob)
+    : ctx_(ctx), output_blob_(output_blob)
+{
+    plan(layers);
+}
+
+void NetHip::plan(const std::vector<LayerDesc>& layers)
+{
+    struct Blob { int ch = 0; int level = 0; int conv = -1; std::vector<Placement> places; };
+    std::map<std::string, Blob> blobs;
+    blobs["image"] = Blob{3, 0, -1, {}};
+    std::map<std::string, int> convs_reading, pools_reading;   // consumers (besides concat)
+    const LayerDesc* out_concat = nullptr;
+
+    // pass 1: shapes, fused activations, conv/pool records
+    for (size_t li = 0; li < layers.size(); ++li) {
+        const LayerDesc& L = layers[li];
+        if (L.type == "Input") continue;
+        if (L.type == "Convolution") {
+            OPK_CHECK_ARG(L.bottom.size() == 1 && L.top.size() == 1, L.name + ": one bottom/top");
+            auto it = blobs.find(L.bottom[0]);
+            OPK_CHECK_ARG(it != blobs.end(), L.name + ": unknown bottom " + L.bottom[0]);
+            OPK_CHECK_ARG(L.stride == 1, L.name + ": only stride 1 convolutions");
+            OPK_CHECK_ARG((L.kernel_size == 3 && L.pad == 1) || (L.kernel_size == 1 && L.pad == 0),
+                          L.name + ": only 3x3/pad1 and 1x1/pad0 convolutions");
+            ConvPlan c;
+            c.info = ConvInfo{L.name, it->second.ch, L.num_output, L.kernel_size, 0};
+            c.in_blob = L.bottom[0];
+            c.level = it->second.level;
+            c.from_image = L.bottom[0] == "image";
+            OPK_CHECK_ARG(!c.from_image || (L.kernel_size == 3 && it->second.ch == 3),
+                          L.name + ": the input conv must be 3x3 over 3 channels");
+            // in-place activation directly after the conv
+            if (li + 1 < layers.size()) {
+                const LayerDesc& A = layers[li + 1];
+                if ((A.type == "ReLU" || A.type == "PReLU") && A.bottom.size() == 1 &&
+                    A.bottom[0] == L.top[0] && A.top.size() == 1 && A.top[0] == L.top[0])
+                    c.info.act = A.type == "ReLU" ? 1 : 2;
+            }
+            if (!c.from_image) convs_reading[L.bottom[0]]++;
+            blobs[L.top[0]] = Blob{L.num_output, c.level, (int)convs_.size(), {}};
+            conv_by_name_[L.name] = (int)convs_.size();
+            convs_.push_back(std::move(c));
+            steps_.push_back({true, (int)convs_.size() - 1});
+        } else if (L.type == "ReLU" || L.type == "PReLU") {
+            auto it = blobs.find(L.bottom[0]);
+            OPK_CHECK_ARG(it != blobs.end() && it->second.conv >= 0 &&
+                              convs_[it->second.conv].info.act != 0 && L.top[0] == L.bottom[0],
+                          L.name + ": only in-place activations directly after a conv");
+        } else if (L.type == "Pooling") {
+            auto it = blobs.find(L.bottom[0]);
+            OPK_CHECK_ARG(it != blobs.end() && it->second.conv >= 0, L.name + ": pool of a conv");
+            OPK_CHECK_ARG(L.pool == "MAX" && L.kernel_size == 2 && L.stride == 2 && L.pad == 0,
+                          L.name + ": only 2x2/2 max pooling");
+            pools_reading[L.bottom[0]]++;
+            blobs[L.top[0]] = Blob{it->second.ch, it->second.level + 1, -1, {}};
+            pools_.push_back(PoolPlan{-1, -1, it->second.level, it->second.ch});
+            steps_.push_back({false, (int)pools_.size() - 1});
+            nlevels_ = std::max(nlevels_, it->second.level + 2);
+        } else if (L.type == "Concat") {
+            OPK_CHECK_ARG(L.concat_axis == 1, L.name + ": channel concat only");
+            int ch = 0, level = -1;
+            for (const auto& b : L.bottom) {
+                auto it = blobs.find(b);
+                OPK_CHECK_ARG(it != blobs.end() && it->second.conv >= 0,
+                              L.name + ": concat bottoms must be conv outputs");
+                OPK_CHECK_ARG(level < 0 || level == it->second.level, L.name + ": mixed sizes");
+                level = it->second.level;
+                ch += it->second.ch;
+            }
+            blobs[L.top[0]] = Blob{ch, level, -1, {}};
+            if (L.top[0] == output_blob_) out_concat = &L;
+        } else {
+            throw Error(4, "layer type " + L.type + " (" + L.name + ") not supported by NetHip");
+        }
+    }
+    OPK_CHECK_ARG(out_concat != nullptr, "output blob " + output_blob_ + " not produced by a Concat");
+
+    // pass 2: concat buffers and placements
+    for (const auto& L : layers) {
+        if (L.type != "Concat") continue;
+        const Blob& top = blobs[L.top[0]];
+        int off = 0;
+        if (&L == out_concat) {
+            out_level_ = top.level;
+            out_c_ = top.ch;
+            for (const auto& b : L.bottom) {
+                ConvPlan& c = convs_[blobs[b].conv];
+                c.out32_coff = off;
+                off += blobs[b].ch;
+            }
+            continue;
+        }
+        const int buf = (int)bufs_.size();
+        bufs_.push_back(BufSpec{top.level, round_up(top.ch, 32)});
+        blobs[L.top[0]].places.push_back(Placement{buf, 0});
+        for (const auto& b : L.bottom) {
+            blobs[b].places.push_back(Placement{buf, off});
+            off += blobs[b].ch;
+        }
+    }
+    // pass 3: conv outputs that something reads directly need a readable placement
+    for (auto& kv : blobs) {
+        Blob& B = kv.second;
+        if (B.conv < 0) continue;
+        const bool pooled = pools_reading.count(kv.first) > 0;
+        const bool read = convs_reading.count(kv.first) > 0;
+        const int need = round_up(B.ch, 32);
+        bool have = false;
+        for (const auto& p : B.places)
+            if (p.coff % 8 == 0 && p.coff + need <= bufs_[p.buf].cs) have = true;
+        if (pooled || (read && !have) || (B.places.empty() && convs_[B.conv].out32_coff < 0)) {
+            const int buf = (int)bufs_.size();
+            bufs_.push_back(BufSpec{B.level, pooled ? round_up(B.ch, 8) : need});
+            B.places.insert(B.places.begin(), Placement{buf, 0});
+        }
+        ConvPlan& c = convs_[B.conv];
+        c.outs = B.places;
+        OPK_CHECK_ARG(c.outs.size() <= (size_t)kConvMaxDst, c.info.name + ": too many consumers");
+    }
+    // pass 4: pool output buffers, then conv inputs and GEMM geometry
+    int pi = 0;
+    for (const auto& L : layers) {
+        if (L.type != "Pooling") continue;
+        PoolPlan& p = pools_[pi++];
+        p.in_buf = blobs[L.bottom[0]].places.at(0).buf;
+        OPK_CHECK_ARG(bufs_[p.in_buf].cs == round_up(p.channels, 8),
+                      L.name + ": pool input must own its buffer");
+        const int buf = (int)bufs_.size();
+        bufs_.push_back(BufSpec{p.level_in + 1, round_up(p.channels, 8)});
+        blobs[L.top[0]].places.push_back(Placement{buf, 0});
+        p.out_buf = buf;
+    }
+    image_buf_ = (int)bufs_.size();
+    bufs_.push_back(BufSpec{0, 32});
+    for (auto& c : convs_) {
+        if (c.from_image) {
+            c.in = Placement{image_buf_, 0};
+            c.cin_pad = 32;
+            c.ntaps = 1;
+        } else {
+            const Blob& B = blobs[c.in_blob];
+            c.cin_pad = round_up(B.ch, 32);
+            c.ntaps = c.info.k == 3 ? 9 : 1;
+            bool found = false;
+            for (const auto& p : B.places)
+                if (p.coff % 8 == 0 && p.coff + c.cin_pad <= bufs_[p.buf].cs) {
+                    c.in = p;
+                    found = true;
+                    break;
+                }
+            OPK_CHECK_ARG(found, c.info.name + ": no readable placement of " + c.in_blob);
+        }
+        c.ksteps = (c.ntaps * c.cin_pad + kConvBK - 1) / kConvBK;
+        c.bn = pick_bn(c.info.cout);
+        c.cout_pad = round_up(c.info.cout, c.bn);
+        info_.push_back(c.info);
+    }
+}
+
+void NetHip::set_conv(const std::string& name, const float* w, const float* b, const float* slope)
+{
+    auto it = conv_by_name_.find(name);
+    OPK_CHECK_ARG(it != conv_by_name_.end(), "no convolution named " + name);
+    ConvPlan& c = convs_[it->second];
+    OPK_CHECK_ARG(w && b, name + ": weights and bias required");
+    OPK_CHECK_ARG(c.info.act != 2 || slope, name + ": PReLU slopes required");
+    const int K = c.ksteps * kConvBK;
+    const int cin = c.info.cin, k = c.info.k;
+    std::vector<uint16_t> packed((size_t)c.cout_pad * K, 0);
+    auto f2h = [](float v) { _Float16 h = (_Float16)v; return __builtin_bit_cast(uint16_t, h); };
+    for (int co = 0; co < c.info.cout; ++co) {
+        uint16_t* dst = packed.data() + (size_t)co * K;
+        if (c.from_image) {   // K index (ky*3 + kx)*3 + ci, matching launch_im2col3
+            for (int ci = 0; ci < 3; ++ci)
+                for (int ky = 0; ky < 3; ++ky)
+                    for (int kx = 0; kx < 3; ++kx)
+                        dst[(ky * 3 + kx) * 3 + ci] = f2h(w[(((size_t)co * 3 + ci) * 3 + ky) * 3 + kx]);
+            continue;
+        }
+        for (int t = 0; t < c.ntaps; ++t) {
+            const int ky = k == 3 ? t / 3 : 0, kx = k == 3 ? t % 3 : 0;
+            for (int ci = 0; ci < cin; ++ci)
+                dst[t * c.cin_pad + ci] = f2h(w[(((size_t)co * cin + ci) * k + ky) * k + kx]);
+        }
+    }
+    std::vector<float> bias(c.info.cout), sl(c.info.cout, 0.f);
+    std::copy(b, b + c.info.cout, bias.begin());
+    if (slope) std::copy(slope, slope + c.info.cout, sl.begin());
+    ctx_->bind();
+    void* dw = c.w.get(packed.size() * 2);
+    void* db = c.bias.get(bias.size() * 4);
+    void* ds = c.slope.get(sl.size() * 4);
+    OPK_HIP(hipMemcpyAsync(dw, packed.data(), packed.size() * 2, hipMemcpyHostToDevice, ctx_->stream));
+    OPK_HIP(hipMemcpyAsync(db, bias.data(), bias.size() * 4, hipMemcpyHostToDevice, ctx_->stream));
+    OPK_HIP(hipMemcpyAsync(ds, sl.data(), sl.size() * 4, hipMemcpyHostToDevice, ctx_->stream));
+    OPK_HIP(hipStreamSynchronize(ctx_->stream));
+    c.loaded = true;
+    n_ = 0;   // re-derive launch arguments
+}
+
+bool NetHip::ready() const
+{
+    for (const auto& c : convs_) if (!c.loaded) return false;
+    return true;
+}
+
+double NetHip::flops_per_frame() const
+{
+    double f = 0;
+    for (const auto& c : convs_)
+        f += 2.0 * lh_[c.level] * lw_[c.level] * c.info.cout * c.info.cin * c.info.k * c.info.k;
+    return f;
+}
+
+void NetHip::reshape(int n, int h, int w)
+{
+    lh_.assign(nlevels_, 0);
+    lw_.assign(nlevels_, 0);
+    lh_[0] = h;
+    lw_[0] = w;
+    for (int l = 1; l < nlevels_; ++l) {   // Caffe ceil sizing for 2x2/2 pooling
+        lh_[l] = (lh_[l - 1] - 2 + 1) / 2 + 1;
+        lw_[l] = (lw_[l - 1] - 2 + 1) / 2 + 1;
+    }
+    mem_.clear();
+    std::vector<uint16_t*> ptr(bufs_.size());
+    for (size_t i = 0; i < bufs_.size(); ++i) {
+        const int L = bufs_[i].level;
+        const size_t pos = (size_t)n * (lh_[L] + 2) * (lw_[L] + 2) + (lw_[L] + 2) + 64;
+        const size_t bytes = pos * bufs_[i].cs * 2;
+        OPK_CHECK_ARG(pos * bufs_[i].cs < (size_t)1 << 31, "activation buffer exceeds 2^31 elements");
+        mem_.push_back(std::make_unique<DevBuf>());
+        ptr[i] = static_cast<uint16_t*>(mem_.back()->get(bytes));
+        OPK_HIP(hipMemsetAsync(ptr[i], 0, bytes, ctx_->stream));
+    }
+    const size_t out_bytes = (size_t)n * out_c_ * lh_[out_level_] * lw_[out_level_] * 4;
+    out32_ = static_cast<float*>(out_mem_.get(out_bytes));
+    for (auto& c : convs_) {
+        ConvArgs& a = c.args;
+        a = ConvArgs{};
+        const int H = lh_[c.level], W = lw_[c.level], Wp = W + 2;
+        a.in = ptr[c.in.buf];
+        a.in_cs = bufs_[c.in.buf].cs;
+        a.in_coff = c.in.coff;
+        a.cin_pad = c.cin_pad;
+        a.ntaps = c.ntaps;
+        if (c.ntaps == 9)
+            for (int t = 0; t < 9; ++t) a.tapoff[t] = (t / 3) * Wp + (t % 3);
+        else
+            a.tapoff[0] = Wp + 1;
+        a.ksteps = c.ksteps;
+        a.w = static_cast<const uint16_t*>(c.w.ptr);
+        a.bias = static_cast<const float*>(c.bias.ptr);
+        a.slope = static_cast<const float*>(c.slope.ptr);
+        a.act = c.info.act;
+        a.frames = n;
+        a.H = H;
+        a.W = W;
+        a.M = n * H * Wp;
+        a.cout = c.info.cout;
+        a.ndst = (int)c.outs.size();
+        for (size_t d = 0; d < c.outs.size(); ++d) {
+            a.dst[d] = ptr[c.outs[d].buf];
+            a.dst_cs[d] = bufs_[c.outs[d].buf].cs;
+            a.dst_coff[d] = c.outs[d].coff;
+        }
+        if (c.out32_coff >= 0) {
+            OPK_CHECK_ARG(c.level == out_level_, c.info.name + ": output at another resolution");
+            a.out32 = out32_;
+            a.out32_c = out_c_;
+            a.out32_coff = c.out32_coff;
+        }
+    }
+    n_ = n;
+    h_ = h;
+    w_ = w;
+}
+
+void NetHip::forward(const float* input, int n, int h, int w)
+{
+    OPK_CHECK_ARG(input && n > 0 && h > 0 && w > 0, "empty input");
+    OPK_CHECK_ARG(ready(), "weights not loaded for every convolution");
+    ctx_->bind();
+    if (n != n_ || h != h_ || w != w_) reshape(n, h, w);
+    std::vector<uint16_t*> ptr(bufs_.size());
+    for (size_t i = 0; i < bufs_.size(); ++i) ptr[i] = static_cast<uint16_t*>(mem_[i]->ptr);
+    launch_im2col3(ptr[image_buf_], input, n, h, w, ctx_->stream);
+    for (const auto& s : steps_) {
+        if (s.conv) {
+            const ConvPlan& c = convs_[s.idx];
+            launch_conv(c.args, c.bn, ctx_->stream);
+        } else {
+            const PoolPlan& p = pools_[s.idx];
+            const int L = p.level_in;
+            launch_maxpool2(ptr[p.out_buf], ptr[p.in_buf], n, lh_[L], lw_[L],
+                            bufs_[p.in_buf].cs, lh_[L + 1], lw_[L + 1], ctx_->stream);
+        }
+    }
+}
+
+}  // namespace opk

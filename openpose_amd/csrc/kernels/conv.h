@@ -1,0 +1,52 @@
+// conv.h -- implicit-GEMM convolution on gfx950 MFMA (fp16 operands, fp32 accumulate).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace opk {
+
+// Activation layout everywhere in the net: NHWC fp16 with a one-pixel zero border,
+// [frames][H+2][W+2][cs] ("padded image"), cs = channel stride of the buffer.
+// GEMM view of a conv over such images:
+//   M = frames * H * (W+2) virtual positions (the two extra columns per row are computed and
+//       discarded: every 3x3 tap is then a constant shift of the whole tile),
+//   N = output channels, K = taps * cin_pad (tap-major, channels inner, 32-channel chunks).
+constexpr int kConvMaxDst = 6;
+constexpr int kConvBM = 128;
+constexpr int kConvBK = 64;
+
+struct ConvArgs {
+    const uint16_t* in;   // fp16 bits, padded image
+    int in_cs, in_coff;   // channel stride and first channel of the input slice
+    int cin_pad;          // channels read per tap (multiple of 32)
+    int ntaps;            // 9 (3x3) or 1 (1x1 / pre-packed)
+    int tapoff[9];        // position offset of each tap from the window's top-left position
+    int ksteps;           // ceil(ntaps * cin_pad / 64)
+    const uint16_t* w;    // [cout_pad][ksteps*64] fp16 bits
+    const float* bias;    // [cout]
+    const float* slope;   // [cout] PReLU slopes (act == 2)
+    int act;              // 0 none, 1 ReLU, 2 PReLU
+    int frames, H, W;     // interior size (input and output share it)
+    int M;                // frames * H * (W+2)
+    int cout;
+    int ndst;
+    uint16_t* dst[kConvMaxDst];
+    int dst_cs[kConvMaxDst], dst_coff[kConvMaxDst];
+    float* out32;         // optional NCHW fp32 [frames][out32_c][H][W]
+    int out32_c, out32_coff;
+};
+
+// bn: 32, 64, 96 or 128 output channels per workgroup
+void launch_conv(const ConvArgs& a, int bn, hipStream_t stream);
+
+// NCHW fp32 [frames][3][H][W] -> padded NHWC fp16 [frames][H+2][W+2][32] holding, at each pixel,
+// the 27 values of its 3x3x3 window (channel q = (ky*3+kx)*3 + ci), then zeros: conv1_1 becomes
+// a 1-tap GEMM with K = 32.
+void launch_im2col3(uint16_t* out, const float* in, int frames, int H, int W, hipStream_t stream);
+
+// 2x2 stride-2 max pool with Caffe ceil sizing, padded NHWC fp16 -> padded NHWC fp16.
+void launch_maxpool2(uint16_t* out, const uint16_t* in, int frames, int H, int W, int C, int OH,
+                     int OW, hipStream_t stream);
+
+}  // namespace opk
