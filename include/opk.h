@@ -119,6 +119,8 @@ int opk_net_set_conv(opk_net* net, const char* name, const float* weights_host,
                      const float* bias_host, const float* slope_host);
 /* input NCHW fp32 on device: [n][3][h][w] (the net input blob, netCaffe.cpp:230-247) */
 int opk_net_forward(opk_net* net, const float* input_dev, int n, int h, int w);
+/* useful (unpadded) convolution FLOPs of one frame of h x w (2 * MACs, all conv layers) */
+int opk_net_flops_per_frame(opk_net* net, int h, int w, double* flops);
 /* device pointer + NCHW shape of the last forward's net_output blob */
 int opk_net_output(opk_net* net, float** output_dev, int shape[4]);
 

@@ -43,6 +43,7 @@ _SIGS = {
     "opk_net_conv_info": (_i, [_p, _i, _c.c_char_p, _ip, _ip, _ip, _ip]),
     "opk_net_set_conv": (_i, [_p, _c.c_char_p, _p, _p, _p]),
     "opk_net_forward": (_i, [_p, _p, _i, _i, _i]),
+    "opk_net_flops_per_frame": (_i, [_p, _i, _i, _c.POINTER(_d)]),
     "opk_net_output": (_i, [_p, _c.POINTER(_p), _ip]),
     "opk_pose_create": (_i, [_p, _p, _i, _c.POINTER(_p)]),
     "opk_pose_destroy": (_i, [_p]),

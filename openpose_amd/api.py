@@ -175,6 +175,11 @@ class Net:
         check(self.L.opk_net_forward(self.h, _ptr(x), n, h, w))
         return self.output()
 
+    def flops_per_frame(self, h, w):
+        f = ctypes.c_double()
+        check(self.L.opk_net_flops_per_frame(self.h, h, w, ctypes.byref(f)))
+        return f.value
+
     def output(self):
         p = ctypes.c_void_p()
         shape = (ctypes.c_int * 4)()

@@ -102,6 +102,14 @@ int opk_net_forward(opk_net* net, const float* input, int n, int h, int w)
     });
 }
 
+int opk_net_flops_per_frame(opk_net* net, int h, int w, double* flops)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net && flops && h > 0 && w > 0, "bad argument");
+        *flops = net->net->flops_per_frame(h, w);
+    });
+}
+
 int opk_net_output(opk_net* net, float** out, int shape[4])
 {
     return guarded_net([&] {

@@ -236,11 +236,18 @@ bool NetHip::ready() const
     return true;
 }
 
-double NetHip::flops_per_frame() const
+double NetHip::flops_per_frame(int h, int w) const
 {
+    std::vector<int> H(nlevels_), W(nlevels_);
+    H[0] = h;
+    W[0] = w;
+    for (int l = 1; l < nlevels_; ++l) {
+        H[l] = (H[l - 1] - 2 + 1) / 2 + 1;
+        W[l] = (W[l - 1] - 2 + 1) / 2 + 1;
+    }
     double f = 0;
     for (const auto& c : convs_)
-        f += 2.0 * lh_[c.level] * lw_[c.level] * c.info.cout * c.info.cin * c.info.k * c.info.k;
+        f += 2.0 * H[c.level] * W[c.level] * c.info.cout * c.info.cin * c.info.k * c.info.k;
     return f;
 }
 

@@ -30,7 +30,7 @@ public:
     int out_h() const { return lh_.empty() ? 0 : lh_[out_level_]; }
     int out_w() const { return lw_.empty() ? 0 : lw_[out_level_]; }
     int frames() const { return n_; }
-    double flops_per_frame() const;   // useful (unpadded) conv FLOPs at the current shape
+    double flops_per_frame(int h, int w) const;   // useful (unpadded) conv FLOPs
 
 private:
     struct Placement { int buf; int coff; };

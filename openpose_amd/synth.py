@@ -108,10 +108,13 @@ def he_weights(layers, seed=0, out_scale=1.0):
     overlay dominates post-processing.
     """
     params = {}
-    slopes = {l["bottom"][0]: True for l in layers if l["type"] == "PReLU"}
+    slopes = {l["bottom"][0]: True for l in layers if l.get("type") == "PReLU"}
     for l in layers:
-        if l["type"] != "Convolution":
+        if l.get("type", "Convolution") != "Convolution":
             continue
+        if l.get("act") == 2:
+            slopes[l["name"]] = True
+        l = dict(l, top=l.get("top", [l["name"]]))
         rng = np.random.default_rng(fnv1a(l["name"]) ^ seed)
         co, ci, k = l["num_output"], l["cin"], l["kernel_size"]
         std = np.sqrt(2.0 / (ci * k * k))
