@@ -67,26 +67,34 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(const ConvArgs a)
     const uint16_t* in = a.in + a.in_coff + (p & 3) * 8;
     const uint16_t* wrow = a.w + (size_t)(n0 + rsub) * kpad + p * 8;
 
-    uint4 ra[4], rb[BP];
-    auto gload = [&](int s) {
-        int c = 2 * s + (p >> 2);
-        if (c >= nchunks) c = 0;            // zero weights cover the padded tail of K
-        const int tap = c / cpt;
-        const int off = a.tapoff[tap];
-        const uint16_t* src = in + (c - tap * cpt) * 32;
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-            ra[i] = *reinterpret_cast<const uint4*>(src + (size_t)(abase[i] + off) * a.in_cs);
-#pragma unroll
-        for (int j = 0; j < BP; ++j)
-            rb[j] = *reinterpret_cast<const uint4*>(wrow + (size_t)(32 * j) * kpad + s * 64);
-    };
-    auto swrite = [&](int buf) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) lds[buf][swz(rsub + 32 * i, p)] = ra[i];
-#pragma unroll
-        for (int j = 0; j < BP; ++j) lds[buf][BM * 8 + swz(rsub + 32 * j, p)] = rb[j];
-    };
+    uint4 ra0, ra1, ra2, ra3, rb0, rb1, rb2, rb3;
+#define OPK_GLOAD(s_)                                                                         \
+    do {                                                                                      \
+        int c_ = 2 * (s_) + (p >> 2);                                                         \
+        if (c_ >= nchunks) c_ = 0; /* zero weights cover the padded tail of K */              \
+        const int tap_ = c_ / cpt;                                                            \
+        const uint16_t* src_ = in + (c_ - tap_ * cpt) * 32 + (size_t)a.tapoff[tap_] * a.in_cs; \
+        ra0 = *reinterpret_cast<const uint4*>(src_ + (size_t)abase[0] * a.in_cs);             \
+        ra1 = *reinterpret_cast<const uint4*>(src_ + (size_t)abase[1] * a.in_cs);             \
+        ra2 = *reinterpret_cast<const uint4*>(src_ + (size_t)abase[2] * a.in_cs);             \
+        ra3 = *reinterpret_cast<const uint4*>(src_ + (size_t)abase[3] * a.in_cs);             \
+        const uint16_t* w_ = wrow + (s_) * 64;                                                \
+        rb0 = *reinterpret_cast<const uint4*>(w_);                                            \
+        if constexpr (BP > 1) rb1 = *reinterpret_cast<const uint4*>(w_ + (size_t)32 * kpad);  \
+        if constexpr (BP > 2) rb2 = *reinterpret_cast<const uint4*>(w_ + (size_t)64 * kpad);  \
+        if constexpr (BP > 3) rb3 = *reinterpret_cast<const uint4*>(w_ + (size_t)96 * kpad);  \
+    } while (0)
+#define OPK_SWRITE(buf_)                                                                      \
+    do {                                                                                      \
+        lds[buf_][swz(rsub, p)] = ra0;                                                        \
+        lds[buf_][swz(rsub + 32, p)] = ra1;                                                   \
+        lds[buf_][swz(rsub + 64, p)] = ra2;                                                   \
+        lds[buf_][swz(rsub + 96, p)] = ra3;                                                   \
+        lds[buf_][BM * 8 + swz(rsub, p)] = rb0;                                               \
+        if constexpr (BP > 1) lds[buf_][BM * 8 + swz(rsub + 32, p)] = rb1;                    \
+        if constexpr (BP > 2) lds[buf_][BM * 8 + swz(rsub + 64, p)] = rb2;                    \
+        if constexpr (BP > 3) lds[buf_][BM * 8 + swz(rsub + 96, p)] = rb3;                    \
+    } while (0)
 
     float4_t acc[MF][NF];
 #pragma unroll
@@ -94,13 +102,13 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(const ConvArgs a)
 #pragma unroll
         for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
-    gload(0);
-    swrite(0);
+    OPK_GLOAD(0);
+    OPK_SWRITE(0);
     __syncthreads();
     const int r16 = lane & 15, q = lane >> 4;
     for (int s = 0; s < a.ksteps; ++s) {
         const int cur = s & 1;
-        if (s + 1 < a.ksteps) gload(s + 1);
+        if (s + 1 < a.ksteps) OPK_GLOAD(s + 1);
 #pragma unroll
         for (int kk = 0; kk < 2; ++kk) {
             half8_t af[MF], bf[NF];
@@ -121,9 +129,12 @@ __global__ __launch_bounds__(256, 2) void conv_kernel(const ConvArgs a)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0,
                                                                        0, 0);
         }
-        if (s + 1 < a.ksteps) swrite(cur ^ 1);
+        if (s + 1 < a.ksteps) OPK_SWRITE(cur ^ 1);
         __syncthreads();
     }
+
+#undef OPK_GLOAD
+#undef OPK_SWRITE
 
     // ---- epilogue: bias + activation, fp16 NHWC stores (+ fp32 NCHW net_output) -----------
     float bias[NF], slope[NF];
