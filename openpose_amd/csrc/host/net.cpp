@@ -14,6 +14,7 @@
 #include "net.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <set>
 
 namespace opk {
@@ -32,6 +33,8 @@ int pick_bn(int cout)
 NetHip::NetHip(Context* ctx, std::vector<LayerDesc> layers, const std::string& output_blob)
     : ctx_(ctx), output_blob_(output_blob)
 {
+    const char* v = std::getenv("OPK_CONV_V1");   // A/B switch to the v1 kernel (dev only)
+    conv_v1_ = v && v[0] == '1';
     plan(layers);
 }
 
@@ -327,7 +330,8 @@ void NetHip::forward(const float* input, int n, int h, int w)
     for (const auto& s : steps_) {
         if (s.conv) {
             const ConvPlan& c = convs_[s.idx];
-            launch_conv(c.args, c.bn, ctx_->stream);
+            if (conv_v1_) launch_conv(c.args, c.bn > 128 ? 128 : c.bn, ctx_->stream);
+            else launch_conv2(c.args, c.bn, ctx_->stream);
         } else {
             const PoolPlan& p = pools_[s.idx];
             const int L = p.level_in;

@@ -64,6 +64,7 @@ private:
     std::vector<BufSpec> bufs_;
     int out_level_ = 0, out_c_ = 0, nlevels_ = 1;
     int image_buf_ = -1;
+    bool conv_v1_ = false;
 
     // shape-dependent state
     int n_ = 0, h_ = 0, w_ = 0;

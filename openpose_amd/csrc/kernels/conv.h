@@ -37,8 +37,10 @@ struct ConvArgs {
     int out32_c, out32_coff;
 };
 
-// bn: 32, 64, 96 or 128 output channels per workgroup
+// v1 (conv.hip): 256 lanes, 128 x bn tile, register-staged; bn: 32, 64, 96 or 128
 void launch_conv(const ConvArgs& a, int bn, hipStream_t stream);
+// v2 (conv2.hip): 512 lanes, 256 x bn tile, LDS-DMA 3-slot ring; bn: 32, 64, 96, 128 or 256
+void launch_conv2(const ConvArgs& a, int bn, hipStream_t stream);
 
 // NCHW fp32 [frames][3][H][W] -> padded NHWC fp16 [frames][H+2][W+2][32] holding, at each pixel,
 // the 27 values of its 3x3x3 window (channel q = (ky*3+kx)*3 + ci), then zeros: conv1_1 becomes

@@ -172,6 +172,14 @@ def pair_scores(heat, peaks, pairs, map_idx, nparts=25, **kw):
 
 
 # ---- Caffe layers -----------------------------------------------------------------------------
+def default_threads():
+    """OMP_NUM_THREADS if set (16 on the GPU box: its CPU share), else min(16, cpu_count)."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return max(1, min(16, os.cpu_count() or 1))
+
+
 def conv2d(x, w, b, pad, nthreads=None):
     x = np.ascontiguousarray(x, np.float32)
     w = np.ascontiguousarray(w, np.float32)
@@ -179,7 +187,7 @@ def conv2d(x, w, b, pad, nthreads=None):
     n, ci, h, wd = x.shape
     co, _, k, _ = w.shape
     out = np.empty((n, co, h, wd), np.float32)
-    lib().orc_conv2d(out, x, w, b, n, ci, h, wd, co, k, pad, nthreads or os.cpu_count() or 1)
+    lib().orc_conv2d(out, x, w, b, n, ci, h, wd, co, k, pad, nthreads or default_threads())
     return out
 
 
