@@ -1,0 +1,98 @@
+"""Generate the committed golden fixtures under tests/golden/ (run in the build container).
+
+    PYTHONPATH=. python tests/golden/make_golden.py
+
+connector_*.npz  -- expected keypoints/scores computed by the REFERENCE's own connector code
+                    (bodyPartConnectorBase.cpp compiled from /root/reference into oracle/_ref);
+                    inputs are regenerated from the stored seeds (openpose_amd.synth is
+                    deterministic) and checked against the stored SHA-256 of the field and peaks.
+nms_*.npz, resize_*.npz, cnn_*.npz
+                 -- outputs of the oracle's CPU restatements (parity unpinned: the reference code
+                    behind them needs OpenCV / Caffe, absent from the image); stored so the GPU box
+                    (no /root/reference) checks the same numbers and regressions are caught.
+"""
+import hashlib
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+
+import oracle  # noqa: E402
+from oracle import body25  # noqa: E402
+from openpose_amd import synth  # noqa: E402
+from tests.fields import noise_field, people_field  # noqa: E402
+
+CONNECTOR_CASES = [  # (name, kind, n_people, seed, h, w, maximize_positives)
+    ("p1", "people", 1, 101, 368, 656, False),
+    ("p5", "people", 5, 102, 368, 656, False),
+    ("p20", "people", 20, 103, 368, 656, False),
+    ("p0", "people", 0, 104, 368, 656, False),
+    ("p5_small", "people", 5, 105, 184, 328, False),
+    ("p5_maxpos", "people", 5, 106, 368, 656, True),
+    ("noise", "noise", 0, 107, 120, 160, False),
+]
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def connector_field(kind, n, seed, h, w):
+    if kind == "people":
+        return people_field(n, h, w, seed)
+    f = noise_field(78, h, w, seed, levels=6, density=0.7)
+    f[26:] = f[26:] * 2 - 1
+    return f
+
+
+def make_connector():
+    assert oracle.ref_lib() is not None, "needs /root/reference (oracle/_ref)"
+    for name, kind, n, seed, h, w, maxpos in CONNECTOR_CASES:
+        f = connector_field(kind, n, seed, h, w)
+        scale = 1.959128
+        off = np.float32(0.5 / scale)
+        pk = oracle.nms(f, 0.05, 128, (off, off))
+        kw = dict(scale=scale, maximize_positives=maxpos)
+        kp, ks = oracle.connect(f, pk, use_reference=True, **kw)
+        np.savez_compressed(os.path.join(HERE, "connector_%s.npz" % name), kind=kind, n_people=n,
+                            seed=seed, h=h, w=w, maximize_positives=maxpos, scale=scale,
+                            field_sha=sha(f), peaks=pk, keypoints=kp, scores=ks)
+
+
+def make_nms():
+    cases = {"people": people_field(5, 92, 164, 201),
+             "noise": noise_field(78, 40, 56, 202, levels=5, density=0.8),
+             "plateau": noise_field(78, 33, 35, 203, levels=3, density=1.0)}
+    for name, f in cases.items():
+        pk = oracle.nms(f, 0.05, 128, (0.25, 0.5))
+        np.savez_compressed(os.path.join(HERE, "nms_%s.npz" % name), field=f, peaks=pk)
+
+
+def make_resize():
+    rng = np.random.default_rng(301)
+    src = rng.normal(0, 0.5, (2, 10, 20)).astype(np.float32)
+    out = oracle.resize_merge([src], 80, 160)
+    srcs = [rng.normal(0, 0.5, (2, h, w)).astype(np.float32) for h, w in [(10, 20), (7, 15), (5, 10)]]
+    merged = oracle.resize_merge(srcs, 80, 160)
+    np.savez_compressed(os.path.join(HERE, "resize.npz"), src=src, out=out,
+                        ms_src0=srcs[0], ms_src1=srcs[1], ms_src2=srcs[2], ms_out=merged)
+
+
+def make_cnn():
+    graph = body25.layers()
+    params = synth.he_weights(graph, seed=401)
+    x = np.random.default_rng(402).uniform(-0.5, 0.5, (1, 3, 64, 96)).astype(np.float32)
+    out = body25.forward(x, params, graph=graph)
+    np.savez_compressed(os.path.join(HERE, "cnn_body25_64x96.npz"), weight_seed=401,
+                        input=x, net_output=out)
+
+
+if __name__ == "__main__":
+    make_connector()
+    make_nms()
+    make_resize()
+    make_cnn()
+    print("fixtures written to", HERE)

@@ -1,0 +1,121 @@
+"""GPU: whole hot path through libopk_hip.so against the committed fixtures and the oracle.
+
+* connector fixtures hold the REFERENCE's own connector outputs (oracle/_ref): the GPU pipeline
+  (GPU NMS -> GPU PAF integrals -> host assembly) must reproduce them bit for bit;
+* NMS / resize fixtures: bit-exact; CNN fixture: relative L2 < 2e-2 (fp16 MFMA vs fp32);
+* end-to-end on 656x368 frames: GPU keypoints vs the fp32 CPU pipeline within 1e-3 px
+  (north_star tolerance), identical people and peak counts.
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from oracle import body25
+from openpose_amd import synth
+from openpose_amd.api import Net, PoseExtractor
+from tests.golden.make_golden import connector_field
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+KEYPOINT_TOL = 1e-3
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a, np.float32)).cuda()
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "connector_*.npz"))),
+                         ids=lambda p: os.path.basename(p))
+def test_gpu_connector_matches_reference_fixture(ctx, path):
+    g = np.load(path, allow_pickle=False)
+    f = connector_field(str(g["kind"]), int(g["n_people"]), int(g["seed"]), int(g["h"]), int(g["w"]))
+    scale = float(g["scale"])
+    off = float(np.float32(0.5 / scale))
+    peaks = torch.zeros((1, 25, 128, 3), device="cuda")
+    heat = _dev(f[None])
+    ctx.nms(peaks, heat, 0.05, (off, off))
+    np.testing.assert_array_equal(peaks.cpu().numpy()[0], g["peaks"])
+    kp, ks = ctx.connect_body_parts(heat, peaks, scale=scale,
+                                    maximize_positives=bool(g["maximize_positives"]))
+    np.testing.assert_array_equal(kp, g["keypoints"])
+    np.testing.assert_array_equal(ks, g["scores"])
+
+
+@pytest.mark.parametrize("name", ["people", "noise", "plateau"])
+def test_gpu_nms_fixture(ctx, name):
+    g = np.load(os.path.join(GOLDEN, "nms_%s.npz" % name), allow_pickle=False)
+    peaks = torch.zeros((1, 25, 128, 3), device="cuda")
+    ctx.nms(peaks, _dev(g["field"][None]), 0.05, (0.25, 0.5))
+    got, ref = peaks.cpu().numpy()[0], g["peaks"]
+    for c in range(25):
+        n = int(ref[c, 0, 0])
+        assert int(got[c, 0, 0]) == n
+        np.testing.assert_array_equal(got[c, 1:n + 1], ref[c, 1:n + 1])
+
+
+def test_gpu_resize_fixture(ctx):
+    g = np.load(os.path.join(GOLDEN, "resize.npz"), allow_pickle=False)
+    out = torch.empty((1, 2, 80, 160), device="cuda")
+    ctx.resize_and_merge(out, [_dev(g["src"][None])])
+    np.testing.assert_array_equal(out.cpu().numpy()[0], g["out"])
+    ctx.resize_and_merge(out, [_dev(g["ms_src%d" % i][None]) for i in range(3)])
+    np.testing.assert_array_equal(out.cpu().numpy()[0], g["ms_out"])
+
+
+def test_gpu_cnn_fixture(ctx):
+    g = np.load(os.path.join(GOLDEN, "cnn_body25_64x96.npz"), allow_pickle=False)
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(synth.he_weights(body25.layers(), seed=int(g["weight_seed"])))
+    net.forward(_dev(g["input"]))
+    got, ref = net.output_numpy(), g["net_output"]
+    assert np.linalg.norm(got - ref) / np.linalg.norm(ref) < 2e-2
+
+
+def test_pose_injection_batch_bitexact(ctx):
+    """poseNetOutput path (poseExtractorCaffe.cpp:249-262) on 3 frames at once."""
+    fields = np.stack([synth.overlay(k + 2, 46, 82, seed=600 + k) +
+                       np.random.default_rng(k).normal(0, 0.01, (78, 46, 82)).astype(np.float32)
+                       for k in range(3)]).astype(np.float32)
+    pose = PoseExtractor(ctx, None)
+    pose.forward_net_output(_dev(fields), (656, 368), (1280, 720))
+    s = pose.scale_net_to_output()
+    assert abs(s - 1.959128) < 1e-5                  # poseExtractorCaffe.cpp:306-310
+    off = float(np.float32(0.5 / np.float64(s)))
+    for k in range(3):
+        heat = oracle.resize_merge([fields[k]], 368, 656)
+        peaks = oracle.nms(heat, 0.05, 128, (off, off))
+        rk, rs = oracle.connect(heat, peaks, scale=s)
+        kp, ks = pose.keypoints(k)
+        assert len(kp) >= 1
+        np.testing.assert_array_equal(kp, rk)
+        np.testing.assert_array_equal(ks, rs)
+
+
+def test_end_to_end_keypoints_within_tolerance(ctx):
+    """CNN (fp16 MFMA) + overlay + resize + NMS + connector vs the fp32 CPU pipeline, 656x368."""
+    graph = body25.layers()
+    params = synth.he_weights(graph, seed=7, out_scale=0.02)
+    x = np.random.default_rng(8).uniform(-0.5, 0.5, (2, 3, 368, 656)).astype(np.float32)
+    ov = np.stack([synth.overlay(5, 46, 82, seed=900 + k) for k in range(2)]).astype(np.float32)
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(params)
+    pose = PoseExtractor(ctx, net)
+    ovd = _dev(ov)
+    pose.set_overlay(ovd)
+    pose.forward(_dev(x), (1280, 720))
+    s = pose.scale_net_to_output()
+    off = float(np.float32(0.5 / np.float64(s)))
+    for k in range(2):
+        out = body25.forward(x[k:k + 1], params, graph=graph)[0] + ov[k]
+        heat = oracle.resize_merge([out], 368, 656)
+        peaks = oracle.nms(heat, 0.05, 128, (off, off))
+        rk, rs = oracle.connect(heat, peaks, scale=s)
+        kp, ks = pose.keypoints(k)
+        assert kp.shape == rk.shape and len(kp) >= 3
+        np.testing.assert_array_equal(kp[..., 2] > 0, rk[..., 2] > 0)   # same parts found
+        assert np.abs(kp[..., :2] - rk[..., :2]).max() <= KEYPOINT_TOL
+        assert np.abs(ks - rs).max() <= KEYPOINT_TOL

@@ -4,7 +4,7 @@ sys.path.insert(0, '.')
 from oracle import body25
 rows = list(csv.DictReader(open(sys.argv[1])))
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 16
-ks = [r for r in rows if 'conv_kernel' in r['Kernel_Name'] or 'maxpool' in r['Kernel_Name']]
+ks = [r for r in rows if 'conv' in r['Kernel_Name'] and 'kernel' in r['Kernel_Name'] or 'maxpool' in r['Kernel_Name']]
 L = [l for l in body25.layers() if l['type'] in ('Convolution', 'Pooling')]
 per = len(L)
 nfw = len(ks) // per
