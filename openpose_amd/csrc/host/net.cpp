@@ -218,10 +218,28 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
                 dst[t * c.cin_pad + ci] = f2h(w[(((size_t)co * cin + ci) * k + ky) * k + kx]);
         }
     }
+    // halo-kernel layout (conv3.hip): [cout/128][cin_pad/32][ky][kx][n 128][ci 32]
+    std::vector<uint16_t> packed3;
+    if (c.ntaps == 9 && !c.from_image) {
+        const int nb = (c.info.cout + kConv3BN - 1) / kConv3BN, cpt = c.cin_pad / 32;
+        packed3.assign((size_t)nb * cpt * 9 * kConv3BN * 32, 0);
+        for (int co = 0; co < c.info.cout; ++co)
+            for (int ci = 0; ci < cin; ++ci)
+                for (int t = 0; t < 9; ++t) {
+                    const size_t unit = ((size_t)(co / kConv3BN) * cpt + ci / 32) * 3 + t / 3;
+                    const size_t idx = ((unit * 3 + t % 3) * kConv3BN + co % kConv3BN) * 32 + ci % 32;
+                    packed3[idx] = f2h(w[(((size_t)co * cin + ci) * 3 + t / 3) * 3 + t % 3]);
+                }
+    }
     std::vector<float> bias(c.info.cout), sl(c.info.cout, 0.f);
     std::copy(b, b + c.info.cout, bias.begin());
     if (slope) std::copy(slope, slope + c.info.cout, sl.begin());
     ctx_->bind();
+    if (!packed3.empty()) {
+        void* dw3 = c.w3.get(packed3.size() * 2);
+        OPK_HIP(hipMemcpyAsync(dw3, packed3.data(), packed3.size() * 2, hipMemcpyHostToDevice,
+                               ctx_->stream));
+    }
     void* dw = c.w.get(packed.size() * 2);
     void* db = c.bias.get(bias.size() * 4);
     void* ds = c.slope.get(sl.size() * 4);
@@ -265,16 +283,23 @@ void NetHip::reshape(int n, int h, int w)
         lw_[l] = (lw_[l - 1] - 2 + 1) / 2 + 1;
     }
     mem_.clear();
-    std::vector<uint16_t*> ptr(bufs_.size());
+    std::vector<uint16_t*>& ptr = base_;
+    ptr.assign(bufs_.size(), nullptr);
     for (size_t i = 0; i < bufs_.size(); ++i) {
+        // zeroed guards: the kernels read up to W+3 positions before the first frame and up to
+        // kConvGuardTail positions after the last one (conv.h)
         const int L = bufs_[i].level;
-        const size_t pos = (size_t)n * (lh_[L] + 2) * (lw_[L] + 2) + (lw_[L] + 2) + 64;
+        const size_t head = (size_t)lw_[L] + 2 + 64;
+        const size_t pos = head + (size_t)n * (lh_[L] + 2) * (lw_[L] + 2) + kConvGuardTail;
         const size_t bytes = pos * bufs_[i].cs * 2;
         OPK_CHECK_ARG(pos * bufs_[i].cs < (size_t)1 << 31, "activation buffer exceeds 2^31 elements");
         mem_.push_back(std::make_unique<DevBuf>());
-        ptr[i] = static_cast<uint16_t*>(mem_.back()->get(bytes));
-        OPK_HIP(hipMemsetAsync(ptr[i], 0, bytes, ctx_->stream));
+        uint16_t* raw = static_cast<uint16_t*>(mem_.back()->get(bytes));
+        OPK_HIP(hipMemsetAsync(raw, 0, bytes, ctx_->stream));
+        ptr[i] = raw + head * bufs_[i].cs;
     }
+    const char* e3 = std::getenv("OPK_CONV3");   // dev A/B switch: OPK_CONV3=0 disables the halo kernel
+    const bool allow3 = !conv_v1_ && !(e3 && e3[0] == '0');
     const size_t out_bytes = (size_t)n * out_c_ * lh_[out_level_] * lw_[out_level_] * 4;
     out32_ = static_cast<float*>(out_mem_.get(out_bytes));
     for (auto& c : convs_) {
@@ -291,7 +316,9 @@ void NetHip::reshape(int n, int h, int w)
         else
             a.tapoff[0] = Wp + 1;
         a.ksteps = c.ksteps;
-        a.w = static_cast<const uint16_t*>(c.w.ptr);
+        c.use3 = allow3 && c.ntaps == 9 && !c.from_image && c.info.cout >= 96 &&
+                 conv3_halo_rows(W) > 0 && c.w3.ptr != nullptr;
+        a.w = static_cast<const uint16_t*>(c.use3 ? c.w3.ptr : c.w.ptr);
         a.bias = static_cast<const float*>(c.bias.ptr);
         a.slope = static_cast<const float*>(c.slope.ptr);
         a.act = c.info.act;
@@ -324,13 +351,13 @@ void NetHip::forward(const float* input, int n, int h, int w)
     OPK_CHECK_ARG(ready(), "weights not loaded for every convolution");
     ctx_->bind();
     if (n != n_ || h != h_ || w != w_) reshape(n, h, w);
-    std::vector<uint16_t*> ptr(bufs_.size());
-    for (size_t i = 0; i < bufs_.size(); ++i) ptr[i] = static_cast<uint16_t*>(mem_[i]->ptr);
+    const std::vector<uint16_t*>& ptr = base_;
     launch_im2col3(ptr[image_buf_], input, n, h, w, ctx_->stream);
     for (const auto& s : steps_) {
         if (s.conv) {
             const ConvPlan& c = convs_[s.idx];
             if (conv_v1_) launch_conv(c.args, c.bn > 128 ? 128 : c.bn, ctx_->stream);
+            else if (c.use3) launch_conv3(c.args, ctx_->stream);
             else launch_conv2(c.args, c.bn, ctx_->stream);
         } else {
             const PoolPlan& p = pools_[s.idx];

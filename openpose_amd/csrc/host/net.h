@@ -45,6 +45,8 @@ private:
         std::vector<Placement> outs;
         int out32_coff = -1;
         DevBuf w, bias, slope;
+        DevBuf w3;            // halo-kernel weight layout (3x3 convs)
+        bool use3 = false;    // launch conv3 (decided per input shape)
         bool loaded = false;
         ConvArgs args{};
     };
@@ -70,6 +72,7 @@ private:
     int n_ = 0, h_ = 0, w_ = 0;
     std::vector<int> lh_, lw_;
     std::vector<std::unique_ptr<DevBuf>> mem_;
+    std::vector<uint16_t*> base_;   // first position of each buffer (past its head guard)
     DevBuf out_mem_;
     float* out32_ = nullptr;
 };

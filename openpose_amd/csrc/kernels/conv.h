@@ -41,6 +41,14 @@ struct ConvArgs {
 void launch_conv(const ConvArgs& a, int bn, hipStream_t stream);
 // v2 (conv2.hip): 512 lanes, 256 x bn tile, LDS-DMA 3-slot ring; bn: 32, 64, 96, 128 or 256
 void launch_conv2(const ConvArgs& a, int bn, hipStream_t stream);
+// v3 (conv3.hip): 3x3 only, 256 padded positions x 128 channels, input halo staged once per
+// 32-channel chunk.  Weights packed [cout/128][cin_pad/32][ky][kx][128][32] (kConv3BN = 128).
+// Reads positions down to -(W+3) and up to (frames*(H+2)*(W+2) + kConvGuardTail): buffers carry
+// zeroed guards on both sides.  conv3_halo_rows(W) == 0 means "row too long, use v2".
+constexpr int kConv3BN = 128;
+constexpr int kConvGuardTail = 1024;   // positions
+int conv3_halo_rows(int W);
+void launch_conv3(const ConvArgs& a, hipStream_t stream);
 
 // NCHW fp32 [frames][3][H][W] -> padded NHWC fp16 [frames][H+2][W+2][32] holding, at each pixel,
 // the 27 values of its 3x3x3 window (channel q = (ky*3+kx)*3 + ci), then zeros: conv1_1 becomes

@@ -57,8 +57,14 @@ __global__ __launch_bounds__(512, 2) void conv2_kernel(const ConvArgs a)
 
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1;
-    const int m0 = blockIdx.x * BM;
-    const int n0 = blockIdx.y * BN;
+    // XCD-aware tile order (cdna_hip_programming.md T1, bijective form): the dispatcher deals
+    // workgroups round-robin over the 8 XCDs, so give each XCD a contiguous range of tiles, N-tiles
+    // of one M-tile adjacent: the 3x3 halo rows and the shared A rows then hit that XCD's L2.
+    const int nblk = gridDim.x, nn = (a.cout + BN - 1) / BN;
+    const int xcd = blockIdx.x & 7, qq = nblk >> 3, rr = nblk & 7;
+    const int tix = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (blockIdx.x >> 3);
+    const int m0 = (tix / nn) * BM;
+    const int n0 = (tix - (tix / nn) * nn) * BN;
     const int Wp = a.W + 2;
     const int per_frame = a.H * Wp;
 
@@ -259,7 +265,7 @@ void launch_conv2(const ConvArgs& a, int bn, hipStream_t stream)
     OPK_CHECK_ARG(a.ntaps == 1 || a.ntaps == 9, "1 or 9 taps");
     OPK_CHECK_ARG(a.ksteps * 64 >= a.ntaps * a.cin_pad, "ksteps too small");
     OPK_CHECK_ARG(a.M > 0 && a.cout > 0 && a.ndst >= 0 && a.ndst <= kConvMaxDst, "bad sizes");
-    dim3 grid((a.M + BM2 - 1) / BM2, (a.cout + bn - 1) / bn);
+    dim3 grid(((a.M + BM2 - 1) / BM2) * ((a.cout + bn - 1) / bn));   // 1-D, remapped in-kernel
     switch (bn) {
         case 32: hipLaunchKernelGGL((conv2_kernel<32, 3>), grid, dim3(512), 0, stream, a); break;
         case 64: hipLaunchKernelGGL((conv2_kernel<64, 3>), grid, dim3(512), 0, stream, a); break;
