@@ -218,20 +218,23 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
                 dst[t * c.cin_pad + ci] = f2h(w[(((size_t)co * cin + ci) * k + ky) * k + kx]);
         }
     }
-    // halo-kernel layout (conv3.hip): [cout/128][cin_pad/32][ky][kx][n 128][ci 32]
+    // halo-kernel layout (conv3.hip): [cout_pad/BN][cin_pad/32][ky][kx][n BN][ci 32]
     std::vector<uint16_t> packed3;
     if (c.ntaps == 9 && !c.from_image) {
-        const int nb = (c.info.cout + kConv3BN - 1) / kConv3BN, cpt = c.cin_pad / 32;
-        packed3.assign((size_t)nb * cpt * 9 * kConv3BN * 32, 0);
+        const int BN = conv3_shape(1, c.info.cout).bn;   // BN depends on cout only
+        const int nb = (c.info.cout + BN - 1) / BN, cpt = c.cin_pad / 32;
+        packed3.assign((size_t)nb * cpt * 9 * BN * 32, 0);
         for (int co = 0; co < c.info.cout; ++co)
             for (int ci = 0; ci < cin; ++ci)
                 for (int t = 0; t < 9; ++t) {
-                    const size_t unit = ((size_t)(co / kConv3BN) * cpt + ci / 32) * 3 + t / 3;
-                    const size_t idx = ((unit * 3 + t % 3) * kConv3BN + co % kConv3BN) * 32 + ci % 32;
+                    const size_t unit = ((size_t)(co / BN) * cpt + ci / 32) * 3 + t / 3;
+                    const size_t idx = ((unit * 3 + t % 3) * BN + co % BN) * 32 + ci % 32;
                     packed3[idx] = f2h(w[(((size_t)co * cin + ci) * 3 + t / 3) * 3 + t % 3]);
                 }
     }
-    std::vector<float> bias(c.info.cout), sl(c.info.cout, 0.f);
+    // bias/slope zero-padded to a multiple of 128 channels (conv3 reads whole 4-channel groups)
+    const size_t cpad = (size_t)(c.info.cout + 127) / 128 * 128;
+    std::vector<float> bias(cpad, 0.f), sl(cpad, 0.f);
     std::copy(b, b + c.info.cout, bias.begin());
     if (slope) std::copy(slope, slope + c.info.cout, sl.begin());
     ctx_->bind();
@@ -316,8 +319,12 @@ void NetHip::reshape(int n, int h, int w)
         else
             a.tapoff[0] = Wp + 1;
         a.ksteps = c.ksteps;
-        c.use3 = allow3 && c.ntaps == 9 && !c.from_image && c.info.cout >= 96 &&
-                 conv3_halo_rows(W) > 0 && c.w3.ptr != nullptr;
+        c.use3 = allow3 && c.ntaps == 9 && !c.from_image && c.w3.ptr != nullptr && c.out32_coff < 0;
+        if (c.use3) {
+            const Conv3Shape s3 = conv3_shape(W, c.info.cout);
+            a.sw = s3.sw;
+            a.nstrips = s3.nstrips;
+        }
         a.w = static_cast<const uint16_t*>(c.use3 ? c.w3.ptr : c.w.ptr);
         a.bias = static_cast<const float*>(c.bias.ptr);
         a.slope = static_cast<const float*>(c.slope.ptr);

@@ -35,19 +35,23 @@ struct ConvArgs {
     int dst_cs[kConvMaxDst], dst_coff[kConvMaxDst];
     float* out32;         // optional NCHW fp32 [frames][out32_c][H][W]
     int out32_c, out32_coff;
+    int sw, nstrips;      // conv3 only: strip width and count (conv3_shape)
 };
 
 // v1 (conv.hip): 256 lanes, 128 x bn tile, register-staged; bn: 32, 64, 96 or 128
 void launch_conv(const ConvArgs& a, int bn, hipStream_t stream);
 // v2 (conv2.hip): 512 lanes, 256 x bn tile, LDS-DMA 3-slot ring; bn: 32, 64, 96, 128 or 256
 void launch_conv2(const ConvArgs& a, int bn, hipStream_t stream);
-// v3 (conv3.hip): 3x3 only, 256 padded positions x 128 channels, input halo staged once per
-// 32-channel chunk.  Weights packed [cout/128][cin_pad/32][ky][kx][128][32] (kConv3BN = 128).
-// Reads positions down to -(W+3) and up to (frames*(H+2)*(W+2) + kConvGuardTail): buffers carry
-// zeroed guards on both sides.  conv3_halo_rows(W) == 0 means "row too long, use v2".
-constexpr int kConv3BN = 128;
+// v3 (conv3.hip): 3x3 only, input halo staged once per 32-channel chunk over a "virtual image" of
+// column strips (sw interior columns each).  Tile BM x BN = 256 x 128, or 512 x 64 for cout <= 64.
+// Weights packed [cout_pad/BN][cin_pad/32][ky][kx][BN][32].  Reads padded positions down to -1
+// and the whole row past the last one: buffers carry zeroed guards (kConvGuardTail positions).
 constexpr int kConvGuardTail = 1024;   // positions
-int conv3_halo_rows(int W);
+constexpr int kConv3MaxStrip = 125;    // interior columns per strip (halo rows = BM + 256)
+struct Conv3Shape {
+    int bm, bn, sw, nstrips;
+};
+Conv3Shape conv3_shape(int W, int cout);
 void launch_conv3(const ConvArgs& a, hipStream_t stream);
 
 // NCHW fp32 [frames][3][H][W] -> padded NHWC fp16 [frames][H+2][W+2][32] holding, at each pixel,

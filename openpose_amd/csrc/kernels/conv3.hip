@@ -1,21 +1,31 @@
 // conv3.hip -- 3x3 convolutions on gfx950 MFMA with the input halo staged ONCE per channel chunk.
 //
-// Same role as conv2.hip (Caffe ConvolutionLayer + fused PReLU/ReLU + concat-by-slice,
-// netCaffe.cpp:248) for the 3x3 layers whose image rows are short enough (W <= 164: the 46x82
-// stage layers and conv3_x/conv4_x), where the implicit GEMM of conv2 re-reads every input row
-// nine times (once per tap) and is bound by the per-CU LDS fill rate (profiles/round1).
+// Role: Caffe ConvolutionLayer + fused PReLU/ReLU + concat-by-slice (netCaffe.cpp:248) for every
+// 3x3 layer of the net except conv1_1 (which reads the 3-channel image).  The implicit GEMM of
+// conv2.hip re-reads each input row nine times (once per tap) and is bound by the per-CU LDS fill
+// rate (profiles/round1); here each input row is staged once per 32-channel chunk.
 //
-// Here the GEMM row space M is the padded image itself ([frames][H+2][W+2] positions; border
-// rows/columns are computed and discarded), so a tile of 256 consecutive positions needs, for a
-// 32-channel chunk, the contiguous position range [p0 - Wp - 1, p0 + 256 + Wp + 1): one "halo"
-// of HR rows x 64 B.  The K loop runs chunk-major, tap-minor in units (chunk, ky):
+// Row space ("virtual image").  The padded NHWC image [frames][H+2][W+2] is cut into vertical
+// strips of sw interior columns (nstrips = ceil(W / sw); sw = W for narrow images).  Each strip is
+// a padded image of width VW = sw + 2 that shares its two border columns with its neighbours; the
+// virtual image is [frames][nstrips][H+2][VW] in row-major order.  The GEMM row space M is that
+// virtual image (border rows/columns are computed and discarded), so every 3x3 tap is a constant
+// shift ky*VW + kx of the whole tile, and a tile of BM consecutive virtual positions needs, for a
+// 32-channel chunk, the virtual range [p0 - VW - 1, p0 + BM + VW + 1): one "halo" of HR rows x
+// 64 B.  Strips keep the halo short (HR = BM + 256) for any image width.
+//
+// The K loop runs chunk-major, tap-minor in units (chunk c, ky):
 //   * unit (c, 0) stages the halo of chunk c (A slot c & 1) and the 3 kx-taps' weights;
-//   * units (c, 1), (c, 2) stage only their 3 taps' weights (B slot u % 3, 24 KB each);
-//   * every tap reads its A fragments from the SAME halo at row offset ky*Wp + kx.
-// A traffic drops ~5x, B is unchanged (weights are L2-resident and shared by every tile).
+//   * units (c, 1), (c, 2) stage only their 3 taps' weights (B slot u % 3);
+//   * every tap reads its A fragments from the SAME halo at row offset ky*VW + kx.
 // Staging is global_load_lds_dwordx4 (lane-linear LDS) with the swizzle applied on the source
 // address; 64-byte rows use piece ^ (((row >> 2) & 1) << 1), conflict-free for the unaligned row
 // windows the taps read (brute-forced over all ds_read_b128 lane groups and window offsets).
+//
+// Tiles: BM x BN = 256 x 128 (8 waves as 4 x 2) or 512 x 64 (8 x 1); every wave owns 64 x 64.
+// The MFMAs compute C^T (weights are the A operand) so each lane ends with 4 consecutive output
+// channels of one position: the epilogue packs them to 8 fp16 bytes and stores straight from
+// registers (no LDS pass).
 #include "conv.h"
 
 #include "../common.h"
@@ -27,9 +37,6 @@ namespace {
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
 
-constexpr int BM3 = 256;
-constexpr int BN3 = 128;
-
 __device__ __forceinline__ int swz64(int row, int piece) { return row * 4 + (piece ^ (((row >> 2) & 1) << 1)); }
 
 __device__ __forceinline__ uint16_t f2h_bits3(float v)
@@ -38,34 +45,97 @@ __device__ __forceinline__ uint16_t f2h_bits3(float v)
     return __builtin_bit_cast(uint16_t, h);
 }
 
+#ifdef OPK3_STAMPS   // dev probe (tools/conv3_probe.hip): per-block phase timestamps
+__device__ unsigned long long* opk3_stamps;
+#define OPK3_STAMP(k_)                                                                        \
+    do {                                                                                      \
+        if (threadIdx.x == 0) {                                                               \
+            opk3_stamps[blockIdx.x * 8 + (k_)] = __builtin_amdgcn_s_memtime();                \
+            if ((k_) == 0) opk3_stamps[blockIdx.x * 8 + 6] = __builtin_amdgcn_s_memrealtime(); \
+            if ((k_) == 5) opk3_stamps[blockIdx.x * 8 + 7] = __builtin_amdgcn_s_memrealtime(); \
+        }                                                                                     \
+    } while (0)
+#else
+#define OPK3_STAMP(k_) do {} while (0)
+#endif
+
 template <int N>
 __device__ __forceinline__ void vm_wait()
 {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int HR>
-__global__ __launch_bounds__(512, 2) void conv3_kernel(const ConvArgs a)
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0..15)
+__device__ __forceinline__ void vm_wait_rt(int n)
 {
-    constexpr int BM = BM3, BN = BN3;
-    constexpr int WN = BN / 2, NF = WN / 16, MF = 4;
+    switch (n) {
+    case 0: vm_wait<0>(); break;
+    case 1: vm_wait<1>(); break;
+    case 2: vm_wait<2>(); break;
+    case 3: vm_wait<3>(); break;
+    case 4: vm_wait<4>(); break;
+    case 5: vm_wait<5>(); break;
+    case 6: vm_wait<6>(); break;
+    case 7: vm_wait<7>(); break;
+    case 8: vm_wait<8>(); break;
+    case 9: vm_wait<9>(); break;
+    case 10: vm_wait<10>(); break;
+    case 11: vm_wait<11>(); break;
+    case 12: vm_wait<12>(); break;
+    case 13: vm_wait<13>(); break;
+    case 14: vm_wait<14>(); break;
+    case 15: vm_wait<15>(); break;
+    default: vm_wait<0>(); break;
+    }
+}
+
+// virtual-image geometry (see the header comment)
+struct Strips {
+    int H, Wp, sw, VW, nstrips, fposV, total;
+    __device__ Strips(const ConvArgs& a)
+        : H(a.H), Wp(a.W + 2), sw(a.sw), VW(a.sw + 2), nstrips(a.nstrips),
+          fposV((a.H + 2) * (a.sw + 2)), total(a.frames * a.nstrips * (a.H + 2) * (a.sw + 2))
+    {
+    }
+    // padded-image position of virtual position v (any v; outside the image -> -1, a zeroed guard)
+    __device__ long map(int v, int& yy, int& xx, int& s) const
+    {
+        if (v < 0 || v >= total) {
+            yy = -1;
+            xx = -1;
+            s = 0;
+            return -1;
+        }
+        const int vf = v / fposV;
+        const int rem = v - vf * fposV;
+        yy = rem / VW;
+        xx = rem - yy * VW;
+        const int f = vf / nstrips;
+        s = vf - f * nstrips;
+        return (long)(f * (H + 2) + yy) * Wp + s * sw + xx;
+    }
+};
+
+template <int BM, int BN, int HR>
+__global__ __launch_bounds__(512, 1) void conv3_kernel(const ConvArgs a)
+{
+    constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
+    static_assert(WAVES_M * 64 == BM && WAVES_N * 64 == BN, "64 x 64 wave tiles");
+    constexpr int MF = 4, NF = 4;
     constexpr int AI = HR / 128;                  // halo DMA instructions per wave (16 rows each)
     constexpr int BROWS = 3 * BN;                 // B rows per unit: kx-major, then channel n
-    constexpr int BI = BROWS / 128;               // B DMA instructions per wave per unit (3)
+    constexpr int BPI = BROWS / 16;               // B DMA instructions per block per unit
     constexpr int ASLOT = HR * 4;                 // 16-byte pieces per halo slot
     constexpr int BSLOT = BROWS * 4;
     constexpr int LDS_PIECES = 2 * ASLOT + 3 * BSLOT;
-    constexpr int TSTRIDE = BN + 8;
     static_assert(LDS_PIECES * 16 <= 160 * 1024, "LDS budget");
-    static_assert(BM * TSTRIDE * 2 <= LDS_PIECES * 16, "epilogue tile fits");
     __shared__ uint4 lds[LDS_PIECES];
 
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int wm = wave >> 1, wn = wave & 1;
-    const int Wp = a.W + 2;
-    const int fpos = (a.H + 2) * Wp;              // positions per padded frame
-    const int total = a.frames * fpos;
-    const int ntile_m = (total + BM - 1) / BM;
+    OPK3_STAMP(0);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WAVES_N, wn = wave - (wave / WAVES_N) * WAVES_N;
+    const Strips g(a);
     const int nn = (a.cout + BN - 1) / BN;
     // XCD-aware bijective tile order (see conv2.hip)
     const int nblk = gridDim.x;
@@ -74,15 +144,24 @@ __global__ __launch_bounds__(512, 2) void conv3_kernel(const ConvArgs a)
     const int p0 = (tix / nn) * BM;
     const int nb = tix - (tix / nn) * nn;
     const int n0 = nb * BN;
-    (void)ntile_m;
 
     // ---- DMA lane geometry: 16 rows x 4 pieces per wave instruction --------------------------
     const int lrow = lane >> 2, phys = lane & 3;
     const int cpt = a.cin_pad >> 5;               // 32-channel chunks
     const int U = 3 * cpt;                        // units (chunk, ky)
-    // halo row hr = (i*8 + wave)*16 + lrow, position p0 - Wp - 1 + hr
-    const uint16_t* ain = a.in + a.in_coff;
-    // packed weights: [nb][c][ky][kx][n 128][32 ch]; a unit is 3*128 rows of 64 B
+    // halo row hr = (i*8 + wave)*16 + lrow holds virtual position p0 - VW - 1 + hr; its image
+    // address (chunk 0, swizzled piece) is fixed for the whole tile
+    const uint16_t* arow[AI];
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+        const int hr = (i * 8 + wave) * 16 + lrow;
+        const int lp = phys ^ (((hr >> 2) & 1) << 1);
+        int yy, xx, s;
+        const long pos = g.map(p0 - g.VW - 1 + hr, yy, xx, s);
+        arow[i] = a.in + a.in_coff + pos * a.in_cs + lp * 8;
+    }
+    // B: this wave issues instructions j*8 + wave < BPI of every unit
+    const int bi = (BPI - wave + 7) / 8;
     const uint16_t* wbase = a.w + (size_t)nb * cpt * 3 * BROWS * 32;
 
 #define OPK3_ISSUE(u_)                                                                        \
@@ -90,25 +169,23 @@ __global__ __launch_bounds__(512, 2) void conv3_kernel(const ConvArgs a)
         const int c_ = (u_) / 3, ky_ = (u_) - 3 * ((u_) / 3);                                 \
         if (ky_ == 0) {                                                                       \
             const int as_ = (c_ & 1) * ASLOT;                                                 \
-            _Pragma("unroll") for (int i_ = 0; i_ < AI; ++i_) {                               \
-                const int hr_ = (i_ * 8 + wave) * 16 + lrow;                                  \
-                const int lp_ = phys ^ (((hr_ >> 2) & 1) << 1);                               \
-                const long pos_ = (long)p0 - Wp - 1 + hr_;                                    \
+            _Pragma("unroll") for (int i_ = 0; i_ < AI; ++i_)                                 \
                 __builtin_amdgcn_global_load_lds(                                             \
-                    (const void*)(ain + pos_ * a.in_cs + c_ * 32 + lp_ * 8),                 \
+                    (const void*)(arow[i_] + c_ * 32),                                        \
                     (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * 8 + wave) * 64]), \
                     16, 0, 0);                                                                \
-            }                                                                                 \
         }                                                                                     \
         const int bs_ = 2 * ASLOT + ((u_) % 3) * BSLOT;                                       \
         const uint16_t* ub_ = wbase + (size_t)(u_) * BROWS * 32;                              \
-        _Pragma("unroll") for (int j_ = 0; j_ < BI; ++j_) {                                   \
-            const int rb_ = (j_ * 8 + wave) * 16 + lrow;                                      \
-            const int lp_ = phys ^ (((rb_ >> 2) & 1) << 1);                                   \
-            __builtin_amdgcn_global_load_lds(                                                 \
-                (const void*)(ub_ + rb_ * 32 + lp_ * 8),                                      \
-                (__attribute__((address_space(3))) void*)(&lds[bs_ + (j_ * 8 + wave) * 64]),  \
-                16, 0, 0);                                                                    \
+        _Pragma("unroll") for (int j_ = 0; j_ < (BPI + 7) / 8; ++j_) {                        \
+            if (BPI % 8 == 0 || j_ * 8 + wave < BPI) {                                        \
+                const int rb_ = (j_ * 8 + wave) * 16 + lrow;                                  \
+                const int lp_ = phys ^ (((rb_ >> 2) & 1) << 1);                               \
+                __builtin_amdgcn_global_load_lds(                                             \
+                    (const void*)(ub_ + rb_ * 32 + lp_ * 8),                                  \
+                    (__attribute__((address_space(3))) void*)(&lds[bs_ + (j_ * 8 + wave) * 64]), \
+                    16, 0, 0);                                                                \
+            }                                                                                 \
         }                                                                                     \
     } while (0)
 
@@ -119,121 +196,115 @@ __global__ __launch_bounds__(512, 2) void conv3_kernel(const ConvArgs a)
         for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
     const int r16 = lane & 15, q = lane >> 4;
+    // bias and negative-side multiplier (1: identity, 0: ReLU, slope: PReLU) of this lane's
+    // output channels, fetched before the K loop
+    float4_t bv[NF], mv[NF];
+    const float neg = a.act == 1 ? 0.f : 1.f;
+#pragma unroll
+    for (int j = 0; j < NF; ++j) {   // bias/slope arrays are zero-padded to a multiple of 128
+        const int ch = n0 + wn * 64 + j * 16 + 4 * q;
+        bv[j] = *reinterpret_cast<const float4_t*>(a.bias + ch);
+        const float4_t sl = *reinterpret_cast<const float4_t*>(a.slope + ch);
+        mv[j] = a.act == 2 ? sl : float4_t{neg, neg, neg, neg};
+    }
+
     OPK3_ISSUE(0);
     if (U > 1) OPK3_ISSUE(1);
     for (int u = 0; u < U; ++u) {
         const int ky = u - 3 * (u / 3);
-        // wait for this wave's loads of unit u: units 0..u+1 have been issued, so only unit u+1's
-        // loads (B, plus the next halo when u+1 starts a chunk) may stay in flight
-        if (ky != 2) {
-            vm_wait<BI>();
-        } else {
-            if (u + 1 < U) vm_wait<AI + BI>(); else vm_wait<0>();
-        }
+        // this wave's loads of unit u have landed once only unit u+1's may still be in flight
+        vm_wait_rt(u + 1 < U ? bi + (ky == 2 ? AI : 0) : 0);
         __builtin_amdgcn_s_barrier();
+        if (u == 0) OPK3_STAMP(1);
         if (u + 2 < U) OPK3_ISSUE(u + 2);
         const uint4* As = lds + ((u / 3) & 1) * ASLOT;
         const uint4* Bs = lds + 2 * ASLOT + (u % 3) * BSLOT;
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) {
-            half8_t af[MF], bf[NF];
-            const int hoff = ky * Wp + kx;
+            half8_t fa[MF], fb[NF];
+            const int hoff = ky * g.VW + kx;
 #pragma unroll
-            for (int i = 0; i < MF; ++i) {
-                const int hr = wm * 64 + i * 16 + r16 + hoff;
-                af[i] = __builtin_bit_cast(half8_t, As[swz64(hr, q)]);
-            }
+            for (int i = 0; i < MF; ++i)
+                fa[i] = __builtin_bit_cast(half8_t, As[swz64(wm * 64 + i * 16 + r16 + hoff, q)]);
 #pragma unroll
-            for (int j = 0; j < NF; ++j) {
-                const int rb = kx * BN + wn * WN + j * 16 + r16;
-                bf[j] = __builtin_bit_cast(half8_t, Bs[swz64(rb, q)]);
-            }
+            for (int j = 0; j < NF; ++j)
+                fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(kx * BN + wn * 64 + j * 16 + r16, q)]);
 #pragma unroll
             for (int i = 0; i < MF; ++i)
 #pragma unroll
                 for (int j = 0; j < NF; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bf[j], acc[i][j], 0,
-                                                                       0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
         }
     }
 #undef OPK3_ISSUE
-    vm_wait<0>();
-    __syncthreads();
+    OPK3_STAMP(2);
 
-    // ---- epilogue (padded-position rows; border positions are discarded) -----------------------
-    uint16_t* tile = reinterpret_cast<uint16_t*>(lds);
-    float bias[NF], slope[NF];
-    int co[NF];
+    // ---- epilogue straight from registers ------------------------------------------------------
+    // lane (q, r16) of fragment (i, j) holds output channels ch..ch+3 (ch = n0 + wn*64 + j*16 + 4q)
+    // of virtual position p0 + wm*64 + i*16 + r16; border and out-of-image positions are dropped.
+    long prow[MF];
+    bool pok[MF];
 #pragma unroll
-    for (int j = 0; j < NF; ++j) {
-        co[j] = n0 + wn * WN + j * 16 + r16;
-        const bool ok = co[j] < a.cout;
-        bias[j] = ok ? a.bias[co[j]] : 0.f;
-        slope[j] = (ok && a.act == 2) ? a.slope[co[j]] : 0.f;
+    for (int i = 0; i < MF; ++i) {
+        int yy, xx, s;
+        prow[i] = g.map(p0 + wm * 64 + i * 16 + r16, yy, xx, s);
+        pok[i] = yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
     }
+    uint32_t pk[MF][NF][2];
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int ml = wm * 64 + i * 16 + q * 4 + r;
-            int f = 0, y = 0, x = 0;
-            bool valid = false;
-            if (a.out32) {
-                const int pos = p0 + ml;
-                f = pos / fpos;
-                const int rem = pos - f * fpos;
-                y = rem / Wp - 1;
-                x = rem - (y + 1) * Wp - 1;
-                valid = pos < total && y >= 0 && y < a.H && x >= 0 && x < a.W;
-            }
+        for (int j = 0; j < NF; ++j) {
+            float v[4];
 #pragma unroll
-            for (int j = 0; j < NF; ++j) {
-                float v = acc[i][j][r] + bias[j];
-                if (a.act == 1) v = v > 0.f ? v : 0.f;
-                else if (a.act == 2) v = v > 0.f ? v : v * slope[j];
-                tile[ml * TSTRIDE + wn * WN + j * 16 + r16] = f2h_bits3(v);
-                if (valid && co[j] < a.cout)
-                    a.out32[(((size_t)f * a.out32_c + a.out32_coff + co[j]) * a.H + y) * a.W + x] = v;
+            for (int r = 0; r < 4; ++r) {
+                const float t = acc[i][j][r] + bv[j][r];
+                v[r] = t > 0.f ? t : t * mv[j][r];
             }
+            pk[i][j][0] = (uint32_t)f2h_bits3(v[0]) | ((uint32_t)f2h_bits3(v[1]) << 16);
+            pk[i][j][1] = (uint32_t)f2h_bits3(v[2]) | ((uint32_t)f2h_bits3(v[3]) << 16);
         }
-    __syncthreads();
-    if (a.ndst == 0) return;
-    constexpr int CPR = BN / 8;
-    for (int c = tid; c < BM * CPR; c += 512) {
-        const int row = c / CPR, col = (c - row * CPR) * 8;
-        const int pos = p0 + row;
-        if (pos >= total) continue;
-        const int f = pos / fpos;
-        const int rem = pos - f * fpos;
-        const int y = rem / Wp;
-        const int x = rem - y * Wp;
-        if (y < 1 || y > a.H || x < 1 || x > a.W) continue;
-        const int n = n0 + col;
-        if (n >= a.cout) continue;
-        const uint4 v = *reinterpret_cast<const uint4*>(tile + row * TSTRIDE + col);
-        const bool full = n + 8 <= a.cout;
-        for (int d = 0; d < a.ndst; ++d) {
-            uint16_t* dst = a.dst[d] + (size_t)pos * a.dst_cs[d] + a.dst_coff[d] + n;
-            if (full && ((a.dst_coff[d] | a.dst_cs[d]) & 7) == 0) {
-                *reinterpret_cast<uint4*>(dst) = v;
-            } else {
-                const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+    const int chl = n0 + wn * 64 + 4 * q;   // this lane's first channel (fragment j adds 16 j)
+    for (int d = 0; d < a.ndst; ++d) {
+        const int cs = a.dst_cs[d];
+        uint16_t* base = a.dst[d] + a.dst_coff[d] + chl;
+        if (((a.dst_coff[d] | cs | a.cout) & 3) == 0) {
 #pragma unroll
-                for (int e = 0; e < 8; ++e)
-                    if (n + e < a.cout) dst[e] = (uint16_t)(wv[e >> 1] >> (16 * (e & 1)));
+            for (int i = 0; i < MF; ++i) {
+                if (!pok[i]) continue;
+                uint16_t* p = base + prow[i] * cs;
+#pragma unroll
+                for (int j = 0; j < NF; ++j)
+                    if (chl + j * 16 < a.cout)
+                        *reinterpret_cast<uint2*>(p + j * 16) = make_uint2(pk[i][j][0], pk[i][j][1]);
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < MF; ++i) {
+                if (!pok[i]) continue;
+                uint16_t* p = base + prow[i] * cs;
+#pragma unroll
+                for (int j = 0; j < NF; ++j)
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (chl + j * 16 + e < a.cout)
+                            p[j * 16 + e] = (uint16_t)(pk[i][j][e >> 1] >> (16 * (e & 1)));
             }
         }
     }
+    OPK3_STAMP(5);
 }
 
 }  // namespace
 
-int conv3_halo_rows(int W)
+Conv3Shape conv3_shape(int W, int cout)
 {
-    const int need = BM3 + 2 * (W + 2) + 2;
-    if (need <= 512) return 512;
-    if (need <= 640) return 640;
-    return 0;
+    Conv3Shape s;
+    s.bn = cout <= 64 ? 64 : 128;
+    s.bm = s.bn == 64 ? 512 : 256;
+    s.nstrips = (W + kConv3MaxStrip - 1) / kConv3MaxStrip;
+    s.sw = (W + s.nstrips - 1) / s.nstrips;
+    return s;
 }
 
 void launch_conv3(const ConvArgs& a, hipStream_t stream)
@@ -242,12 +313,16 @@ void launch_conv3(const ConvArgs& a, hipStream_t stream)
     OPK_CHECK_ARG(a.in_cs % 8 == 0 && a.in_coff % 8 == 0, "input slice must be 16-byte aligned");
     OPK_CHECK_ARG(a.in_coff + a.cin_pad <= a.in_cs, "input slice exceeds the buffer");
     OPK_CHECK_ARG(a.M > 0 && a.cout > 0 && a.ndst <= kConvMaxDst, "bad sizes");
-    const int hr = conv3_halo_rows(a.W);
-    OPK_CHECK_ARG(hr > 0, "row too long for the halo kernel");
-    const int total = a.frames * (a.H + 2) * (a.W + 2);
-    dim3 grid(((total + BM3 - 1) / BM3) * ((a.cout + BN3 - 1) / BN3));
-    if (hr == 512) hipLaunchKernelGGL(conv3_kernel<512>, grid, dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL(conv3_kernel<640>, grid, dim3(512), 0, stream, a);
+    OPK_CHECK_ARG(a.out32 == nullptr, "the halo kernel has no fp32 NCHW output");
+    const Conv3Shape s = conv3_shape(a.W, a.cout);
+    OPK_CHECK_ARG(a.sw == s.sw && a.nstrips == s.nstrips, "strip geometry differs from conv3_shape");
+    OPK_CHECK_ARG(2 * (s.sw + 2) + 2 <= 256, "strip too wide for the halo (HR = BM + 256)");
+    const long total = (long)a.frames * s.nstrips * (a.H + 2) * (s.sw + 2);
+    OPK_CHECK_ARG(total < (1L << 30), "too many positions");
+    const int nn = (a.cout + s.bn - 1) / s.bn;
+    dim3 grid((unsigned)(((total + s.bm - 1) / s.bm) * nn));
+    if (s.bn == 128) hipLaunchKernelGGL((conv3_kernel<256, 128, 512>), grid, dim3(512), 0, stream, a);
+    else hipLaunchKernelGGL((conv3_kernel<512, 64, 768>), grid, dim3(512), 0, stream, a);
     OPK_LAUNCH_CHECK();
 }
 
