@@ -66,8 +66,9 @@ int opk_resize_and_merge(opk_ctx* ctx, float* target_dev, const float* const* so
 /* ---- NMS: replaces op::nmsGpu<float> (include/openpose/net/nmsBase.hpp:14-16) with nmsCpu
  *      numerics (src/openpose/net/nmsBase.cpp:7-170).  target_size = {N, parts, maxPeaks+1, 3},
  *      source_size = {N, C, H, W}; only the first `parts` planes of each frame are scanned.
- *      kernel_scratch (the reference's int peak map) may be NULL: this implementation compacts
- *      peaks in-kernel and never materialises it. */
+ *      kernel_scratch (the reference's int peak map) may be NULL: this implementation never
+ *      materialises it (peaks are appended to small per-plane candidate lists owned by the
+ *      context, then sorted into raster order per plane). */
 int opk_nms(opk_ctx* ctx, float* target_dev, int* kernel_scratch_dev, const float* source_dev,
             float threshold, const int target_size[4], const int source_size[4],
             float offset_x, float offset_y);
@@ -152,7 +153,11 @@ int opk_pose_set_overlay(opk_pose* pose, const float* overlay_dev);
 int opk_pose_num_people(opk_pose* pose, int frame);
 int opk_pose_keypoints(opk_pose* pose, int frame, float* keypoints_host, float* scores_host,
                        int max_people);
-/* device pointers of the last forward's heatmaps [n][78][H][W] and peaks [n][25][128][3] */
+/* device pointers of the last forward's heatmaps [n][78][H][W] and peaks [n][25][128][3].
+ * The pipeline evaluates heat-map values lazily from the net output (NMS and PAF scoring compute
+ * the resized values they touch, bit-identical to resizeAndMerge); opk_pose_heatmaps writes the
+ * full stack on first request after a forward.  With opk_pose_forward_net_output the net output
+ * buffer must stay unchanged until then. */
 int opk_pose_heatmaps(opk_pose* pose, float** heat_dev, int shape[4]);
 int opk_pose_peaks(opk_pose* pose, float** peaks_dev, int shape[4]);
 float opk_pose_scale_net_to_output(opk_pose* pose);

@@ -185,8 +185,9 @@ int opk_nms(opk_ctx* ctx, float* target, int* kernel_scratch, const float* sourc
         OPK_CHECK_ARG(ts[3] == 3, "target peak vector must be 3 (x, y, score)");
         OPK_CHECK_ARG(ts[1] <= ss[1], "more target parts than source channels");
         ctx->bind();
-        opk::launch_nms(target, source, ts[0], ss[1], ts[1], ss[2], ss[3], ts[2], th, offx, offy,
-                        ctx->stream);
+        opk::launch_nms(target, ctx->nms_candidates(ts[0], ts[1]),
+                        opk::heat_materialised(source, ss[1], ss[2], ss[3]), ts[0], ts[1], ts[2],
+                        th, offx, offy, ctx->stream);
     });
 }
 
@@ -202,8 +203,10 @@ int opk_paf_scores(opk_ctx* ctx, float* pair_scores, const float* heat, const fl
         const auto& t = ctx->pose_table(pose_model);
         const double near = std::sqrt((double)(heat_w * heat_h)) / 150;
         const float reject = float(default_nms_th + 1e-6);
-        opk::launch_paf_scores(pair_scores, heat, peaks, frames, heat_channels, heat_h, heat_w,
-                               max_peaks, t, inter_th, inter_min_above, reject, near, ctx->stream);
+        opk::launch_paf_scores(pair_scores,
+                               opk::heat_materialised(heat, heat_channels, heat_h, heat_w), peaks,
+                               frames, max_peaks, t, inter_th, inter_min_above, reject, near,
+                               ctx->stream);
     });
 }
 
@@ -243,9 +246,9 @@ int opk_connect_body_parts(opk_ctx* ctx, float* kp_out, float* ks_out, int max_p
         auto* dscores = static_cast<float*>(ctx->scratch_scores.get(score_floats * sizeof(float)));
         const auto& t = ctx->pose_table(pose_model);
         const double near = std::sqrt((double)(heat_w * heat_h)) / 150;
-        opk::launch_paf_scores(dscores, heat, peaks_dev, 1, heat_channels, heat_h, heat_w,
-                               max_peaks, t, inter_th, inter_min_above, float(nms_th + 1e-6),
-                               near, ctx->stream);
+        opk::launch_paf_scores(dscores, opk::heat_materialised(heat, heat_channels, heat_h, heat_w),
+                               peaks_dev, 1, max_peaks, t, inter_th, inter_min_above,
+                               float(nms_th + 1e-6), near, ctx->stream);
         auto* hpk = static_cast<float*>(ctx->host_peaks.get(peak_floats * sizeof(float)));
         auto* hsc = static_cast<float*>(ctx->host_scores.get(score_floats * sizeof(float)));
         OPK_HIP(hipMemcpyAsync(hpk, peaks_dev, peak_floats * sizeof(float), hipMemcpyDeviceToHost,

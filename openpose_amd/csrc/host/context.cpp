@@ -77,4 +77,14 @@ const PafPairTable& Context::pose_table(int model)
     return ref;
 }
 
+int* Context::nms_candidates(int frames, int parts)
+{
+    const size_t need = nms_scratch_ints(frames, parts) * sizeof(int);
+    if (need > nms_scratch.bytes) {
+        nms_scratch.get(need);
+        OPK_HIP(hipMemsetAsync(nms_scratch.ptr, 0, need, stream));
+    }
+    return static_cast<int*>(nms_scratch.ptr);
+}
+
 }  // namespace opk

@@ -32,6 +32,9 @@ struct Context {
     const PafPairTable& pose_table(int model);
 
     DevBuf scratch_scores;   // dense pair scores for opk_connect_body_parts
+    // NMS candidate lists (nms.hip), zeroed when (re)allocated; the kernels keep them zeroed
+    DevBuf nms_scratch;
+    int* nms_candidates(int frames, int parts);
     HostBuf host_peaks, host_scores;
 
     // device < 0: host-only context (graph planning / host assembly; no device calls)

@@ -289,6 +289,8 @@ void NetHip::reshape(int n, int h, int w)
     std::vector<uint16_t*>& ptr = base_;
     ptr.assign(bufs_.size(), nullptr);
     for (size_t i = 0; i < bufs_.size(); ++i) {
+        mem_.push_back(std::make_unique<DevBuf>());
+        if ((int)i == image_buf_ && !conv_v1_) continue;   // conv_image reads the NCHW input itself
         // zeroed guards: the kernels read up to W+3 positions before the first frame and up to
         // kConvGuardTail positions after the last one (conv.h)
         const int L = bufs_[i].level;
@@ -296,7 +298,6 @@ void NetHip::reshape(int n, int h, int w)
         const size_t pos = head + (size_t)n * (lh_[L] + 2) * (lw_[L] + 2) + kConvGuardTail;
         const size_t bytes = pos * bufs_[i].cs * 2;
         OPK_CHECK_ARG(pos * bufs_[i].cs < (size_t)1 << 31, "activation buffer exceeds 2^31 elements");
-        mem_.push_back(std::make_unique<DevBuf>());
         uint16_t* raw = static_cast<uint16_t*>(mem_.back()->get(bytes));
         OPK_HIP(hipMemsetAsync(raw, 0, bytes, ctx_->stream));
         ptr[i] = raw + head * bufs_[i].cs;
@@ -359,11 +360,12 @@ void NetHip::forward(const float* input, int n, int h, int w)
     ctx_->bind();
     if (n != n_ || h != h_ || w != w_) reshape(n, h, w);
     const std::vector<uint16_t*>& ptr = base_;
-    launch_im2col3(ptr[image_buf_], input, n, h, w, ctx_->stream);
+    if (conv_v1_) launch_im2col3(ptr[image_buf_], input, n, h, w, ctx_->stream);
     for (const auto& s : steps_) {
         if (s.conv) {
             const ConvPlan& c = convs_[s.idx];
             if (conv_v1_) launch_conv(c.args, c.bn > 128 ? 128 : c.bn, ctx_->stream);
+            else if (c.from_image) launch_conv_image(c.args, input, ctx_->stream);
             else if (c.use3) launch_conv3(c.args, ctx_->stream);
             else launch_conv2(c.args, c.bn, ctx_->stream);
         } else {

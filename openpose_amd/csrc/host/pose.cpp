@@ -42,9 +42,16 @@ void PoseHip::set_property(int prop, double v)
     props_[prop] = v;
 }
 
-float* PoseHip::heatmaps(int shape[4]) const
+float* PoseHip::heatmaps(int shape[4])
 {
     shape[0] = n_; shape[1] = pose_model(0).heat_channels(); shape[2] = hh_; shape[3] = hw_;
+    if (n_ > 0 && !heat_valid_) {
+        ctx_->bind();
+        float* heat = static_cast<float*>(heat_.get((size_t)n_ * lazy_.channels * hh_ * hw_ * 4));
+        launch_resize_merge(heat, lazy_.src, lazy_.nsrc, n_ * lazy_.channels, hh_, hw_, ctx_->stream);
+        OPK_HIP(hipStreamSynchronize(ctx_->stream));
+        heat_valid_ = true;
+    }
     return static_cast<float*>(heat_.ptr);
 }
 
@@ -73,15 +80,23 @@ void PoseHip::forward_net_output(const float* net_out, int n, int oh, int ow, in
     const size_t out_elems = (size_t)n * C * oh * ow;
     if (overlay_) launch_add_inplace(const_cast<float*>(net_out), overlay_, out_elems, s);
 
-    // 1. resize x8 (ResizeAndMergeCaffe::Reshape: (h*8 - 1)*1 + 1)
+    // 1. resize x8 (ResizeAndMergeCaffe::Reshape: (h*8 - 1)*1 + 1), evaluated lazily: NMS and
+    //    the PAF scorer compute the resized values they touch with resize.hip's arithmetic
+    //    (bit-identical), so the 75 MB/frame heat-map stack is only written if requested
     const int H = oh * 8, W = ow * 8;
     hh_ = H;
     hw_ = W;
     n_ = n;
-    float* heat = static_cast<float*>(heat_.get((size_t)n * C * H * W * 4));
     const auto& t = ctx_->tables(oh, ow, H, W);
-    ResizeSource rs{net_out, oh, ow, t.yofs, t.ycoef, t.xofs, t.xcoef};
-    launch_resize_merge(heat, &rs, 1, n * C, H, W, s);
+    HeatMap heat{};
+    heat.channels = C;
+    heat.h = H;
+    heat.w = W;
+    heat.nsrc = 1;
+    heat.inv_n = 1.f;
+    heat.src[0] = ResizeSource{net_out, oh, ow, t.yofs, t.ycoef, t.xofs, t.xcoef};
+    lazy_ = heat;
+    heat_valid_ = false;
 
     // 2. scale net -> output (poseExtractorCaffe.cpp:281-310), net output size == net input size
     const double sp = resize_scale_factor(prod_w, prod_h, net_w, net_h);
@@ -95,7 +110,7 @@ void PoseHip::forward_net_output(const float* net_out, int n, int oh, int ow, in
     const int P1 = kMaxPeaks + 1;
     const size_t peak_floats = (size_t)m.parts * P1 * 3;
     float* peaks = static_cast<float*>(peaks_.get((size_t)n * peak_floats * 4));
-    launch_nms(peaks, heat, n, C, m.parts, H, W, P1, nms_th, off, off, s);
+    launch_nms(peaks, ctx_->nms_candidates(n, m.parts), heat, n, m.parts, P1, nms_th, off, off, s);
 
     // 4. connector: PAF integrals on the GPU (compact), assembly on the host
     const float inter_th = (float)props_[OPK_PROP_INTER_THRESHOLD];
@@ -104,7 +119,7 @@ void PoseHip::forward_net_output(const float* net_out, int n, int oh, int ow, in
     const float reject = float(nms_th + 1e-6);   // defaultNmsThreshold = NMSThreshold (:325)
     const auto& pt = ctx_->pose_table(0);
     float* rec = static_cast<float*>(records_.get((size_t)n * kRecordFloats * 4));
-    launch_paf_scores_compact(rec, kRecordFloats, heat, peaks, n, C, H, W, kMaxPeaks, pt, inter_th,
+    launch_paf_scores_compact(rec, kRecordFloats, heat, peaks, n, kMaxPeaks, pt, inter_th,
                               inter_min, reject, near, s);
     float* hp = static_cast<float*>(hpeaks_.get((size_t)n * peak_floats * 4));
     float* hr = static_cast<float*>(hrecords_.get((size_t)n * kRecordFloats * 4));
@@ -130,8 +145,10 @@ void PoseHip::forward_net_output(const float* net_out, int n, int oh, int ow, in
         } else {   // more candidates than a compact record holds: dense scores for this frame
             const size_t dense = (size_t)m.npairs() * kMaxPeaks * kMaxPeaks;
             float* d = static_cast<float*>(dense_.get(dense * 4));
-            launch_paf_scores(d, heat + (size_t)f * C * H * W, peaks + (size_t)f * peak_floats, 1,
-                              C, H, W, kMaxPeaks, pt, inter_th, inter_min, reject, near, s);
+            HeatMap hf = heat;   // frame f alone
+            hf.src[0].src = net_out + (size_t)f * C * oh * ow;
+            launch_paf_scores(d, hf, peaks + (size_t)f * peak_floats, 1, kMaxPeaks, pt, inter_th,
+                              inter_min, reject, near, s);
             float* hd = static_cast<float*>(hdense_.get(dense * 4));
             OPK_HIP(hipMemcpyAsync(hd, d, dense * 4, hipMemcpyDeviceToHost, s));
             OPK_HIP(hipStreamSynchronize(s));

@@ -24,7 +24,9 @@ public:
     int num_people(int f) const { return people_.at(f); }
     const std::vector<float>& keypoints(int f) const { return kp_.at(f); }
     const std::vector<float>& scores(int f) const { return ks_.at(f); }
-    float* heatmaps(int shape[4]) const;
+    // full-resolution heat maps of the last forward, materialised on first request (the pipeline
+    // itself evaluates them lazily from the net output: HeatMap in kernels.h)
+    float* heatmaps(int shape[4]);
     float* peaks(int shape[4]) const;
     float scale_net_to_output() const { return scale_net_to_output_; }
 
@@ -37,6 +39,8 @@ private:
     float scale_net_to_output_ = 1.f;
 
     int n_ = 0, hh_ = 0, hw_ = 0;
+    HeatMap lazy_{};            // last forward's heat maps as resize of the net output
+    bool heat_valid_ = false;   // heat_ holds them
     DevBuf heat_, peaks_, records_, dense_;
     HostBuf hpeaks_, hrecords_, hdense_;
     static constexpr int kMaxPeaks = kPoseMaxPeople;   // peaks blob [25][128][3]

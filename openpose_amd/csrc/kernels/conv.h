@@ -59,6 +59,10 @@ void launch_conv3(const ConvArgs& a, hipStream_t stream);
 // a 1-tap GEMM with K = 32.
 void launch_im2col3(uint16_t* out, const float* in, int frames, int H, int W, hipStream_t stream);
 
+// First conv (3 input channels, 3x3, cout <= 64) straight from the fp32 NCHW input [frames][3][H][W]
+// (conv_image.hip); weights as packed for v1/v2 ([cout_pad][64], K order (ky*3 + kx)*3 + ci).
+void launch_conv_image(const ConvArgs& a, const float* image, hipStream_t stream);
+
 // 2x2 stride-2 max pool with Caffe ceil sizing, padded NHWC fp16 -> padded NHWC fp16.
 void launch_maxpool2(uint16_t* out, const uint16_t* in, int frames, int H, int W, int C, int OH,
                      int OW, hipStream_t stream);

@@ -1,0 +1,133 @@
+// conv_image.hip -- the first 3x3 convolution (3 -> <=64 channels) read straight from the fp32
+// NCHW network input (the blob op::Net::forwardPass receives, netCaffe.cpp:248 / the Caffe
+// "image" input), fused with bias + activation, written as padded NHWC fp16.
+//
+// K = 27 (3 taps x 3 taps x 3 channels) fits one 16x16x32 MFMA step, so the layer is pure data
+// movement: read 12 B and write 128 B per pixel.  A block stages a (4+2) x (64+2) x 3 fp32 input
+// tile in LDS; each lane gathers the 8 K-values of its MFMA operand from it (K order
+// (ky*3 + kx)*3 + ci, zero past 27), the weights of all 64 output channels stay in registers,
+// and the MFMAs compute C^T so each lane stores 4 consecutive output channels (8 bytes) of one
+// pixel.  Replaces the im2col image + 1-step GEMM of conv.hip (two passes over HBM).
+#include "conv.h"
+
+#include "../common.h"
+
+namespace opk {
+
+namespace {
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
+
+constexpr int TH = 4;            // output rows per block (one per wave)
+constexpr int TW = 64;           // output columns per block
+constexpr int LW = TW + 2;       // staged columns
+constexpr int NG = 4;            // 16-channel groups (cout <= 64)
+
+__device__ __forceinline__ uint16_t f2h_bits_i(float v)
+{
+    const _Float16 h = (_Float16)v;
+    return __builtin_bit_cast(uint16_t, h);
+}
+
+__global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const float* __restrict__ img)
+{
+    __shared__ float tile[3 * (TH + 2) * LW];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int H = a.H, W = a.W;
+    const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
+    int b = blockIdx.x;
+    const int tx = b % tiles_x;
+    b /= tiles_x;
+    const int ty = b % tiles_y;
+    const int f = b / tiles_y;
+    const int x0 = tx * TW, y0 = ty * TH;
+
+    // stage the input tile (zero outside the image = the conv's zero padding)
+    const size_t plane = (size_t)H * W;
+    const float* src = img + (size_t)f * 3 * plane;
+    for (int i = tid; i < 3 * (TH + 2) * LW; i += 256) {
+        const int ci = i / ((TH + 2) * LW);
+        const int rem = i - ci * (TH + 2) * LW;
+        const int r = rem / LW, c = rem - (rem / LW) * LW;
+        const int y = y0 + r - 1, x = x0 + c - 1;
+        tile[i] = (y >= 0 && y < H && x >= 0 && x < W) ? src[ci * plane + (size_t)y * W + x] : 0.f;
+    }
+
+    const int r16 = lane & 15, q = lane >> 4;
+    // weights (A operand of C^T): rows = output channels g*16 + r16, K = 8q .. 8q+7; row stride 64
+    half8_t wf[NG];
+    float4_t bv[NG], mv[NG];
+    const float neg = a.act == 1 ? 0.f : 1.f;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const int co = g * 16 + r16;
+        wf[g] = co < a.cout ? *reinterpret_cast<const half8_t*>(a.w + (size_t)co * 64 + 8 * q)
+                            : half8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        const int ch = g * 16 + 4 * q;   // bias/slope arrays are zero-padded to 128 channels
+        bv[g] = *reinterpret_cast<const float4_t*>(a.bias + ch);
+        const float4_t sl = *reinterpret_cast<const float4_t*>(a.slope + ch);
+        mv[g] = a.act == 2 ? sl : float4_t{neg, neg, neg, neg};
+    }
+    // this lane's 8 K values: LDS offset of (ci, ky, kx) for k = 8q + e, or -1 past k = 26
+    int off[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int k = 8 * q + e;
+        const int t = k / 3, ci = k - 3 * (k / 3);
+        off[e] = k < 27 ? (ci * (TH + 2) + t / 3) * LW + (t - 3 * (t / 3)) : -1;
+    }
+    __syncthreads();
+
+    const int y = y0 + wave;
+    if (y >= H) return;
+    uint16_t* dbase[kConvMaxDst];
+    for (int d = 0; d < a.ndst; ++d)
+        dbase[d] = a.dst[d] + ((size_t)f * (H + 2) + y + 1) * (W + 2) * a.dst_cs[d] + a.dst_coff[d];
+#pragma unroll
+    for (int grp = 0; grp < TW / 16; ++grp) {
+        const int xl = grp * 16 + r16;
+        half8_t xf;
+#pragma unroll
+        for (int e = 0; e < 8; ++e)
+            xf[e] = off[e] >= 0 ? (_Float16)tile[off[e] + wave * LW + xl] : (_Float16)0.f;
+        float4_t acc[NG];
+#pragma unroll
+        for (int g = 0; g < NG; ++g)
+            acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[g], xf, float4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const int x = x0 + xl;
+        if (x >= W) continue;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            const int ch = g * 16 + 4 * q;
+            if (ch >= a.cout) continue;
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const float t = acc[g][r] + bv[g][r];
+                v[r] = t > 0.f ? t : t * mv[g][r];
+            }
+            const uint32_t lo = (uint32_t)f2h_bits_i(v[0]) | ((uint32_t)f2h_bits_i(v[1]) << 16);
+            const uint32_t hi = (uint32_t)f2h_bits_i(v[2]) | ((uint32_t)f2h_bits_i(v[3]) << 16);
+            for (int d = 0; d < a.ndst; ++d)
+                *reinterpret_cast<uint2*>(dbase[d] + (size_t)(x + 1) * a.dst_cs[d] + ch) = make_uint2(lo, hi);
+        }
+    }
+}
+
+}  // namespace
+
+void launch_conv_image(const ConvArgs& a, const float* image, hipStream_t stream)
+{
+    OPK_CHECK_ARG(image != nullptr && a.w != nullptr, "image and weights required");
+    OPK_CHECK_ARG(a.cout > 0 && a.cout <= 16 * NG && a.cout % 4 == 0, "conv_image: cout <= 64, % 4");
+    OPK_CHECK_ARG(a.ndst >= 1 && a.ndst <= kConvMaxDst && a.out32 == nullptr, "conv_image: outputs");
+    for (int d = 0; d < a.ndst; ++d)
+        OPK_CHECK_ARG(((a.dst_cs[d] | a.dst_coff[d]) & 3) == 0, "conv_image: 8-byte aligned slices");
+    const long blocks = (long)a.frames * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
+    OPK_CHECK_ARG(blocks > 0 && blocks < (1L << 31), "conv_image: bad sizes");
+    hipLaunchKernelGGL(conv_image_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a, image);
+    OPK_LAUNCH_CHECK();
+}
+
+}  // namespace opk

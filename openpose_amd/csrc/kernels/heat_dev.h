@@ -1,0 +1,49 @@
+// heat_dev.h -- device side of HeatMap (kernels.h): one full-resolution heat-map value, read from
+// HBM or evaluated on the fly with the resize/merge arithmetic of resize.hip.
+//
+// cv::resize INTER_CUBIC numerics (resizeAndMergeBase.cpp:9-113 -> OpenCV): horizontal pass of the
+// four source rows around the target row ((t0 + t1) + t2) + t3 with the column's coefficients,
+// then the vertical combination in the same order; sources merged in order as v + acc, and the
+// sum times (float)(1/N) for N > 1.  Compiled with -ffp-contract=off everywhere it is used, so
+// resize_merge_kernel, the NMS and the PAF scorer all produce the same bits for a pixel.
+#pragma once
+#include "kernels.h"
+
+namespace opk {
+
+__device__ __forceinline__ int heat_clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+// horizontal pass of one source row at the output column whose first tap is x0
+__device__ __forceinline__ float cubic_hpass(const float* row, int sw, int x0, const float* a)
+{
+    const float v0 = row[heat_clampi(x0 - 1, 0, sw - 1)];
+    const float v1 = row[heat_clampi(x0, 0, sw - 1)];
+    const float v2 = row[heat_clampi(x0 + 1, 0, sw - 1)];
+    const float v3 = row[heat_clampi(x0 + 2, 0, sw - 1)];
+    return v0 * a[0] + v1 * a[1] + v2 * a[2] + v3 * a[3];
+}
+
+// value of plane `plane` (= frame * channels + channel) at full-resolution pixel (x, y)
+__device__ __forceinline__ float heat_at(const HeatMap& M, int plane, int x, int y)
+{
+    if (M.heat) return M.heat[((size_t)plane * M.h + y) * M.w + x];
+    float acc = 0.f;
+    for (int n = 0; n < M.nsrc; ++n) {
+        const ResizeSource& S = M.src[n];
+        const float* src = S.src + (size_t)plane * S.sh * S.sw;
+        const int x0 = S.xofs[x];
+        const float4 c = *reinterpret_cast<const float4*>(S.xcoef + 4 * x);
+        const float a[4] = {c.x, c.y, c.z, c.w};
+        const float4 b = *reinterpret_cast<const float4*>(S.ycoef + 4 * y);
+        const int yb = S.yofs[y] - 1;
+        float h[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            h[k] = cubic_hpass(src + (size_t)heat_clampi(yb + k, 0, S.sh - 1) * S.sw, S.sw, x0, a);
+        const float v = h[0] * b.x + h[1] * b.y + h[2] * b.z + h[3] * b.w;
+        acc = (n == 0) ? v : v + acc;
+    }
+    return M.nsrc > 1 ? acc * M.inv_n : acc;
+}
+
+}  // namespace opk

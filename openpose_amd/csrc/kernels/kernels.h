@@ -21,9 +21,33 @@ constexpr int kMaxResizeSources = 8;
 void launch_resize_merge(float* dst, const ResizeSource* srcs, int nsrc, int planes, int dh,
                          int dw, hipStream_t stream);
 
+// A full-resolution heat-map stack [frames][channels][h][w], either materialised in HBM
+// (heat != nullptr) or evaluated on the fly, pixel by pixel, as the resize/merge of `nsrc` net
+// outputs with exactly the arithmetic of resize.hip (heat_dev.h) -- bit-identical values without
+// writing the 75 MB/frame stack.  Consumers: NMS (nms.hip) and PAF scores (paf.hip).
+struct HeatMap {
+    const float* heat;
+    int channels, h, w;
+    int nsrc;
+    float inv_n;
+    ResizeSource src[kMaxResizeSources];
+};
+inline HeatMap heat_materialised(const float* heat, int channels, int h, int w)
+{
+    HeatMap m{};
+    m.heat = heat;
+    m.channels = channels;
+    m.h = h;
+    m.w = w;
+    return m;
+}
+
 // ---- NMS (nms.hip) ----------------------------------------------------------------------------
-// peaks [frames][parts][maxPeaks1][3]; heat [frames][channels][h][w]
-void launch_nms(float* peaks, const float* heat, int frames, int channels, int parts, int h, int w,
+// peaks [frames][parts][maxPeaks1][3]; heat [frames][channels][h][w].  scratch: nms_scratch_ints()
+// ints, zeroed once before the first call (every call leaves it zeroed again).
+constexpr int kNmsCandidates = 1024;   // per plane; more peaks fall back to an ordered re-scan
+size_t nms_scratch_ints(int frames, int parts);
+void launch_nms(float* peaks, int* scratch, const HeatMap& heat, int frames, int parts,
                 int max_peaks1, float threshold, float offx, float offy, hipStream_t stream);
 
 // ---- PAF scores (paf.hip) --------------------------------------------------------------------
@@ -35,17 +59,16 @@ struct PafPairTable {
     const int* mapy;     // device [npairs]
 };
 // dense: scores [frames][npairs][maxPeaks][maxPeaks]
-void launch_paf_scores(float* scores, const float* heat, const float* peaks, int frames,
-                       int heat_channels, int h, int w, int max_peaks, const PafPairTable& t,
-                       float inter_th, float inter_min_above, float reject_score,
-                       double near_dist, hipStream_t stream);
+void launch_paf_scores(float* scores, const HeatMap& heat, const float* peaks, int frames,
+                       int max_peaks, const PafPairTable& t, float inter_th,
+                       float inter_min_above, float reject_score, double near_dist,
+                       hipStream_t stream);
 // compact: per frame a record of `rec_floats` floats: [0] = number of scores (or -1 when it did
 // not fit), then the nA*nB scores of pair 0, pair 1, ... (row-major i, j).
-void launch_paf_scores_compact(float* records, int rec_floats, const float* heat,
-                               const float* peaks, int frames, int heat_channels, int h, int w,
-                               int max_peaks, const PafPairTable& t, float inter_th,
-                               float inter_min_above, float reject_score, double near_dist,
-                               hipStream_t stream);
+void launch_paf_scores_compact(float* records, int rec_floats, const HeatMap& heat,
+                               const float* peaks, int frames, int max_peaks,
+                               const PafPairTable& t, float inter_th, float inter_min_above,
+                               float reject_score, double near_dist, hipStream_t stream);
 
 // ---- elementwise helpers (misc.hip) -----------------------------------------------------------
 void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stream);

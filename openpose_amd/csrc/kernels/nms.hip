@@ -1,39 +1,45 @@
 // nms.hip -- body-part peak extraction for gfx950 with nmsCpu numerics.
 //
 // Replaces op::nmsGpu (src/openpose/net/nmsBase.cu:251-351: register kernel + thrust scan over all
-// channels + write kernel) with ONE launch computing what op::nmsCpu computes
-// (src/openpose/net/nmsBase.cpp:7-170):
+// channels + write kernel) computing what op::nmsCpu computes (src/openpose/net/nmsBase.cpp:7-170):
 //   * interior pixels (1 < x < w-2, 1 < y < h-2): v > th and v > all 8 neighbours;
 //   * pixels on row/column 1 or w-2 / h-2 (outer-border pixels of those rows/columns included):
 //     v > th and v >= all 8 neighbours, neighbours outside the map read as th;
 //   * any other pixel: never a peak;
 //   * peaks kept in raster order, the first maxPeaks-1 only; position refined by the 7x7
 //     score-weighted centroid in float (dy outer, dx inner), + offset; score = v.
-// One workgroup of 1024 lanes per (part, frame) walks the plane in raster order, 4 pixels per
-// lane per step; a block-wide OR skips peak-free steps (almost all of them), otherwise a wave
-// shuffle scan + LDS wave totals give each peak its raster rank -- no global scan, no int peak
-// map (the reference's 6 M-int thrust scan, nmsBase.cu:327-329).  HBM-bound: 24.1 MB read per
-// frame (config 2).  -ffp-contract=off keeps the centroid sums bit-identical to the CPU.
+//
+// Two launches:
+//   1. detect: every pixel of every (part, frame) plane in parallel, 4 per lane (HBM-bound pass);
+//      a peak appends its raster index to its plane's candidate list (one atomic per peak --
+//      peaks are rare) -- no int peak map and no global scan (the reference's 6 M-int thrust
+//      scan, nmsBase.cu:327-329);
+//   2. finalize: one workgroup per plane sorts its candidates (bitonic, LDS), keeps the first
+//      maxPeaks-1 in raster order, refines them, and resets the plane's counter for the next
+//      call.  A plane with more than kNmsCandidates peaks (noise, not poses) is re-scanned in
+//      raster order by its workgroup, so the result never depends on the candidate capacity.
+// -ffp-contract=off keeps the centroid sums bit-identical to the CPU.
 #include "kernels.h"
+#include "heat_dev.h"
 #include "../common.h"
 
 namespace opk {
 
 namespace {
 
-constexpr int NT = 1024;
-constexpr int NWAVES = NT / 64;
+constexpr int DT = 256;   // detect lanes per block
+constexpr int FT = 256;   // finalize lanes per block
+constexpr int CAP = kNmsCandidates;
 
-__device__ __forceinline__ bool peak_at(const float* __restrict__ s, int w, int h, float th, int x,
-                                        int y, float v)
+// peak rules of nmsCpu for pixel (x, y) of value v; get(x, y) reads an in-map neighbour
+template <typename Get>
+__device__ __forceinline__ bool peak_at(Get get, int w, int h, float th, int x, int y, float v)
 {
     if (!(v > th)) return false;
     if (x > 1 && x < w - 2 && y > 1 && y < h - 2) {
-        const float* r0 = s + (size_t)(y - 1) * w + x;
-        const float* r1 = r0 + w;
-        const float* r2 = r1 + w;
-        return v > r0[-1] && v > r0[0] && v > r0[1] && v > r1[-1] && v > r1[1] && v > r2[-1] &&
-               v > r2[0] && v > r2[1];
+        return v > get(x - 1, y - 1) && v > get(x, y - 1) && v > get(x + 1, y - 1) &&
+               v > get(x - 1, y) && v > get(x + 1, y) && v > get(x - 1, y + 1) &&
+               v > get(x, y + 1) && v > get(x + 1, y + 1);
     }
     if (x == 1 || x == w - 2 || y == 1 || y == h - 2) {
         bool ok = true;
@@ -43,8 +49,7 @@ __device__ __forceinline__ bool peak_at(const float* __restrict__ s, int w, int 
             for (int dx = -1; dx <= 1; ++dx) {
                 if (dx == 0 && dy == 0) continue;
                 const int xx = x + dx, yy = y + dy;
-                const float nb =
-                    (xx >= 0 && xx < w && yy >= 0 && yy < h) ? s[(size_t)yy * w + xx] : th;
+                const float nb = (xx >= 0 && xx < w && yy >= 0 && yy < h) ? get(xx, yy) : th;
                 ok = ok && (v >= nb);
             }
         return ok;
@@ -52,104 +57,296 @@ __device__ __forceinline__ bool peak_at(const float* __restrict__ s, int w, int 
     return false;
 }
 
-__global__ __launch_bounds__(NT) void nms_kernel(float* __restrict__ peaks,
-                                                 const float* __restrict__ heat, int channels,
-                                                 int parts, int h, int w, int max_peaks1,
-                                                 float th, float offx, float offy)
+__device__ __forceinline__ void push_candidate(int* plane, int idx)
 {
-    __shared__ int wave_tot[NWAVES];
-    const int c = blockIdx.x, b = blockIdx.y;
-    const float* s = heat + ((size_t)b * channels + c) * h * w;
-    float* out = peaks + ((size_t)b * parts + c) * max_peaks1 * 3;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int quads = (w + 3) >> 2;
-    const int items = h * quads;
-    const int cap = max_peaks1 - 1;
-    int count = 0;   // block-uniform
+    const int slot = atomicAdd(plane, 1);
+    if (slot < CAP) plane[1 + slot] = idx;
+}
 
-    for (int base = 0; base < items && count < cap; base += NT) {
-        const int item = base + tid;
-        unsigned mask = 0;
-        int y = 0, x0 = 0;
-        if (item < items) {
-            y = item / quads;
-            x0 = (item - y * quads) << 2;
-            const float* row = s + (size_t)y * w;
+// scratch per plane: [0] candidate count, [1 .. CAP] raster indices
+__global__ __launch_bounds__(DT) void nms_detect_kernel(int* __restrict__ scratch,
+                                                        const float* __restrict__ heat,
+                                                        int channels, int parts, int h, int w,
+                                                        float th)
+{
+    const int c = blockIdx.y, b = blockIdx.z;
+    const float* s = heat + ((size_t)b * channels + c) * h * w;
+    const int quads = (w + 3) >> 2;
+    const int item = blockIdx.x * DT + threadIdx.x;
+    if (item >= h * quads) return;
+    const int y = item / quads;
+    const int x0 = (item - y * quads) << 2;
+    const float* row = s + (size_t)y * w;
+    int* plane = scratch + ((size_t)b * parts + c) * (CAP + 1);
+    auto get = [s, w](int xx, int yy) { return s[(size_t)yy * w + xx]; };
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int x = x0 + k;
-                if (x < w && peak_at(s, w, h, th, x, y, row[x])) mask |= 1u << k;
+    for (int k = 0; k < 4; ++k) {
+        const int x = x0 + k;
+        if (x < w && peak_at(get, w, h, th, x, y, row[x])) push_candidate(plane, y * w + x);
+    }
+}
+
+// Lazy heat map: a workgroup of LT lanes owns LT consecutive columns (x0-1 .. x0+LT-2) of a
+// (LOY+2)-row window of the resized plane (tile + 1-pixel halo; pixels outside the map = th).
+// Each lane runs resize.hip's two passes down its own column -- horizontal pass of the window's
+// source rows into its LDS column, vertical combinations with the row's (block-uniform, scalar)
+// coefficients -- then the LT-2 x LOY tile pixels are tested from LDS.  The full-resolution stack
+// is never written.
+constexpr int LT = 256;           // lanes = window columns
+constexpr int LOX = LT - 2;       // tile columns
+constexpr int LOY = 16;           // tile rows
+constexpr int LWR = LOY + 2;      // window rows
+constexpr int LMAXR = 16;         // source rows per window kept in LDS (x8 upsampling needs 7)
+
+__global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ scratch,
+                                                             const HeatMap M, int parts, float th)
+{
+    // hb (horizontal-pass rows) and win (window values) share LDS: a lane only ever touches its
+    // own column of either before the barrier, and win is written after the last hb read
+    static_assert(LMAXR <= LWR, "hb fits in win");
+    __shared__ float win[LWR * LT];
+    float* hb = win;
+    const int tid = threadIdx.x;
+    const int c = blockIdx.z % parts, b = blockIdx.z / parts;
+    const int plane = b * M.channels + c;
+    const int H = M.h, W = M.w;
+    const int xw0 = blockIdx.x * LOX - 1;          // window column of lane 0
+    const int x = xw0 + tid;
+    const int y0 = blockIdx.y * LOY - 1;           // window row 0
+    const bool xin = x >= 0 && x < W;
+    const int ry_lo = max(y0, 0), ry_hi = min(y0 + LWR - 1, H - 1);
+    __shared__ float4 rcoef[LWR];          // vertical coefficients of the window rows
+    __shared__ int4 rofs[LWR];             // their 4 source rows as offsets into hb
+    float acc[LWR];
+#pragma unroll
+    for (int rr = 0; rr < LWR; ++rr) acc[rr] = 0.f;
+    for (int n = 0; n < M.nsrc; ++n) {
+        const ResizeSource& S = M.src[n];
+        const float* src = S.src + (size_t)plane * S.sh * S.sw;
+        const int r_lo = heat_clampi(S.yofs[ry_lo] - 1, 0, S.sh - 1);
+        const int r_hi = heat_clampi(S.yofs[ry_hi] + 2, 0, S.sh - 1);
+        const int nrows = r_hi - r_lo + 1;
+        const bool tiled = nrows <= LMAXR;   // block-uniform
+        if (n > 0) __syncthreads();          // previous source's row tables fully read
+        if (tid < LWR) {
+            const int y = heat_clampi(y0 + tid, 0, H - 1);
+            rcoef[tid] = *reinterpret_cast<const float4*>(S.ycoef + 4 * y);
+            const int yb = S.yofs[y] - 1;
+            int4 o;
+            o.x = heat_clampi(yb, 0, S.sh - 1);
+            o.y = heat_clampi(yb + 1, 0, S.sh - 1);
+            o.z = heat_clampi(yb + 2, 0, S.sh - 1);
+            o.w = heat_clampi(yb + 3, 0, S.sh - 1);
+            if (tiled) {
+                o.x = (o.x - r_lo) * LT;
+                o.y = (o.y - r_lo) * LT;
+                o.z = (o.z - r_lo) * LT;
+                o.w = (o.w - r_lo) * LT;
+            }
+            rofs[tid] = o;
+        }
+        int xo = 0;
+        float a[4] = {0.f, 0.f, 0.f, 0.f};
+        if (xin) {
+            xo = S.xofs[x];
+            const float4 cf = *reinterpret_cast<const float4*>(S.xcoef + 4 * x);
+            a[0] = cf.x; a[1] = cf.y; a[2] = cf.z; a[3] = cf.w;
+        }
+        if (tiled && xin)
+            for (int r = 0; r < nrows; ++r)
+                hb[r * LT + tid] = cubic_hpass(src + (size_t)(r_lo + r) * S.sw, S.sw, xo, a);
+        __syncthreads();                     // row tables visible (hb columns are lane-private)
+#pragma unroll
+        for (int rr = 0; rr < LWR; ++rr) {
+            const int y = y0 + rr;
+            float v = 0.f;
+            if (y >= 0 && y < H && xin) {
+                const float4 bq = rcoef[rr];
+                const int4 o = rofs[rr];
+                float hv[4];
+                if (tiled) {
+                    hv[0] = hb[o.x + tid];
+                    hv[1] = hb[o.y + tid];
+                    hv[2] = hb[o.z + tid];
+                    hv[3] = hb[o.w + tid];
+                } else {
+                    hv[0] = cubic_hpass(src + (size_t)o.x * S.sw, S.sw, xo, a);
+                    hv[1] = cubic_hpass(src + (size_t)o.y * S.sw, S.sw, xo, a);
+                    hv[2] = cubic_hpass(src + (size_t)o.z * S.sw, S.sw, xo, a);
+                    hv[3] = cubic_hpass(src + (size_t)o.w * S.sw, S.sw, xo, a);
+                }
+                v = hv[0] * bq.x + hv[1] * bq.y + hv[2] * bq.z + hv[3] * bq.w;
+            }
+            acc[rr] = (n == 0) ? v : v + acc[rr];
+        }
+    }
+#pragma unroll
+    for (int rr = 0; rr < LWR; ++rr) {
+        const int y = y0 + rr;
+        win[rr * LT + tid] = (y >= 0 && y < H && xin) ? (M.nsrc > 1 ? acc[rr] * M.inv_n : acc[rr]) : th;
+    }
+    __syncthreads();
+    if (tid == 0 || tid == LT - 1 || !xin) return;
+    int* pl = scratch + ((size_t)b * parts + c) * (CAP + 1);
+    auto get = [xw0, y0](int xx, int yy) { return win[(yy - y0) * LT + (xx - xw0)]; };
+    for (int ty = 0; ty < LOY; ++ty) {
+        const int y = y0 + 1 + ty;
+        if (y >= H) break;
+        if (peak_at(get, W, H, th, x, y, win[(ty + 1) * LT + tid])) push_candidate(pl, y * W + x);
+    }
+}
+
+__device__ void refine_write(float* __restrict__ out, const HeatMap& M, int plane, int idx,
+                             int rank, float offx, float offy)
+{
+    const int w = M.w, h = M.h;
+    const int py = idx / w, px = idx - py * w;
+    float xa = 0.f, ya = 0.f, sa = 0.f;
+    for (int dy = -3; dy <= 3; ++dy) {
+        const int yy = py + dy;
+        if (yy < 0 || yy >= h) continue;
+        for (int dx = -3; dx <= 3; ++dx) {
+            const int xx = px + dx;
+            if (xx < 0 || xx >= w) continue;
+            const float sc = heat_at(M, plane, xx, yy);
+            if (sc > 0) {
+                xa += (float)xx * sc;
+                ya += (float)yy * sc;
+                sa += sc;
             }
         }
-        const int n = __popc(mask);
-        if (!__syncthreads_or(n)) continue;
-        // inclusive scan of n over the wave
-        int incl = n;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const int t = __shfl_up(incl, off, 64);
-            if (lane >= off) incl += t;
-        }
-        if (lane == 63) wave_tot[wave] = incl;
+    }
+    float* o = out + (size_t)(rank + 1) * 3;
+    o[0] = xa / sa + offx;
+    o[1] = ya / sa + offy;
+    o[2] = heat_at(M, plane, px, py);
+}
+
+__global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ peaks,
+                                                          int* __restrict__ scratch,
+                                                          const HeatMap M, int parts,
+                                                          int max_peaks1, float th, float offx,
+                                                          float offy)
+{
+    __shared__ int key[CAP];
+    __shared__ int wave_tot[FT / 64];
+    const int c = blockIdx.x, b = blockIdx.y;
+    const int pln = b * M.channels + c;
+    const int h = M.h, w = M.w;
+    auto get = [&M, pln](int xx, int yy) { return heat_at(M, pln, xx, yy); };
+    float* out = peaks + ((size_t)b * parts + c) * max_peaks1 * 3;
+    int* plane = scratch + ((size_t)b * parts + c) * (CAP + 1);
+    const int tid = threadIdx.x;
+    const int cap = max_peaks1 - 1;
+    const int n = plane[0];
+    int found;
+    if (n <= CAP) {
+        for (int i = tid; i < CAP; i += FT) key[i] = i < n ? plane[1 + i] : 0x7fffffff;
         __syncthreads();
-        int before = 0, total = 0;
-        for (int i = 0; i < NWAVES; ++i) {
-            const int t = wave_tot[i];
-            before += (i < wave) ? t : 0;
-            total += t;
-        }
-        int rank = count + before + incl - n;
-        for (int k = 0; k < 4; ++k) {
-            if (!(mask & (1u << k))) continue;
-            if (rank < cap) {
-                const int px = x0 + k, py = y;
-                float xa = 0.f, ya = 0.f, sa = 0.f;
-                for (int dy = -3; dy <= 3; ++dy) {
-                    const int yy = py + dy;
-                    if (yy < 0 || yy >= h) continue;
-                    for (int dx = -3; dx <= 3; ++dx) {
-                        const int xx = px + dx;
-                        if (xx < 0 || xx >= w) continue;
-                        const float sc = s[(size_t)yy * w + xx];
-                        if (sc > 0) {
-                            xa += (float)xx * sc;
-                            ya += (float)yy * sc;
-                            sa += sc;
+        int len = 1;   // smallest power of two >= n (>= 2)
+        while (len < n) len <<= 1;
+        if (len < 2) len = 2;
+        for (int k = 2; k <= len; k <<= 1)
+            for (int j = k >> 1; j > 0; j >>= 1) {
+                for (int i = tid; i < len; i += FT) {
+                    const int p = i ^ j;
+                    if (p > i) {
+                        const int a = key[i], bb = key[p];
+                        const bool up = (i & k) == 0;
+                        if ((a > bb) == up) {
+                            key[i] = bb;
+                            key[p] = a;
                         }
                     }
                 }
-                float* o = out + (size_t)(rank + 1) * 3;
-                o[0] = xa / sa + offx;
-                o[1] = ya / sa + offy;
-                o[2] = s[(size_t)py * w + px];
+                __syncthreads();
             }
-            ++rank;
+        found = n < cap ? n : cap;
+        for (int r = tid; r < found; r += FT) refine_write(out, M, pln, key[r], r, offx, offy);
+    } else {
+        // overflow: ordered raster scan of the plane by this workgroup
+        const int lane = tid & 63, wave = tid >> 6;
+        const int quads = (w + 3) >> 2;
+        const int items = h * quads;
+        int count = 0;   // block-uniform
+        for (int base = 0; base < items && count < cap; base += FT) {
+            const int item = base + tid;
+            unsigned mask = 0;
+            int y = 0, x0 = 0;
+            if (item < items) {
+                y = item / quads;
+                x0 = (item - y * quads) << 2;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const int x = x0 + k;
+                    if (x < w && peak_at(get, w, h, th, x, y, get(x, y))) mask |= 1u << k;
+                }
+            }
+            const int cnt = __popc(mask);
+            if (!__syncthreads_or(cnt)) continue;
+            int incl = cnt;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const int t = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += t;
+            }
+            if (lane == 63) wave_tot[wave] = incl;
+            __syncthreads();
+            int before = 0, total = 0;
+            for (int i = 0; i < FT / 64; ++i) {
+                const int t = wave_tot[i];
+                before += (i < wave) ? t : 0;
+                total += t;
+            }
+            int rank = count + before + incl - cnt;
+            for (int k = 0; k < 4; ++k) {
+                if (!(mask & (1u << k))) continue;
+                if (rank < cap) refine_write(out, M, pln, y * w + x0 + k, rank, offx, offy);
+                ++rank;
+            }
+            count += total;
+            __syncthreads();
         }
-        count += total;
-        __syncthreads();   // wave_tot is rewritten by the next productive step
+        found = count < cap ? count : cap;
     }
-    const int found = count < cap ? count : cap;
     // slot 0 = {count, 0, 0}; unused slots zeroed (the reference leaves them stale)
-    for (int i = tid; i < (max_peaks1 - found) * 3; i += NT) {
-        const int idx = found * 3 + 3 + i;
-        if (idx < max_peaks1 * 3) out[idx] = 0.f;
-    }
+    for (int i = tid; i < (max_peaks1 - 1 - found) * 3; i += FT) out[found * 3 + 3 + i] = 0.f;
+    __syncthreads();
     if (tid == 0) {
         out[0] = (float)found;
         out[1] = 0.f;
         out[2] = 0.f;
+        plane[0] = 0;   // ready for the next call
     }
 }
 
 }  // namespace
 
-void launch_nms(float* peaks, const float* heat, int frames, int channels, int parts, int h, int w,
+size_t nms_scratch_ints(int frames, int parts) { return (size_t)frames * parts * (CAP + 1); }
+
+void launch_nms(float* peaks, int* scratch, const HeatMap& heat, int frames, int parts,
                 int max_peaks1, float threshold, float offx, float offy, hipStream_t stream)
 {
-    OPK_CHECK_ARG(frames > 0 && parts > 0 && parts <= channels, "bad channel counts");
+    const int h = heat.h, w = heat.w;
+    OPK_CHECK_ARG(frames > 0 && parts > 0 && parts <= heat.channels, "bad channel counts");
     OPK_CHECK_ARG(h > 0 && w > 0 && max_peaks1 >= 1, "bad sizes");
-    dim3 grid(parts, frames);
-    hipLaunchKernelGGL(nms_kernel, grid, dim3(NT), 0, stream, peaks, heat, channels, parts, h, w,
+    OPK_CHECK_ARG(heat.heat != nullptr || (heat.nsrc >= 1 && heat.nsrc <= kMaxResizeSources),
+                  "heat map: materialised or 1..8 lazy sources");
+    OPK_CHECK_ARG(scratch != nullptr, "NMS scratch required (zeroed once, nms_scratch_ints)");
+    OPK_CHECK_ARG((long)h * w < (1L << 31), "plane too large");
+    if (heat.heat) {
+        const int quads = (w + 3) >> 2;
+        dim3 g1((h * quads + DT - 1) / DT, parts, frames);
+        hipLaunchKernelGGL(nms_detect_kernel, g1, dim3(DT), 0, stream, scratch, heat.heat,
+                           heat.channels, parts, h, w, threshold);
+    } else {
+        dim3 g1((w + LOX - 1) / LOX, (h + LOY - 1) / LOY, frames * parts);
+        hipLaunchKernelGGL(nms_detect_lazy_kernel, g1, dim3(LT), 0, stream, scratch, heat, parts,
+                           threshold);
+    }
+    OPK_LAUNCH_CHECK();
+    dim3 g2(parts, frames);
+    hipLaunchKernelGGL(nms_finalize_kernel, g2, dim3(FT), 0, stream, peaks, scratch, heat, parts,
                        max_peaks1, threshold, offx, offy);
     OPK_LAUNCH_CHECK();
 }

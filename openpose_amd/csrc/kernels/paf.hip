@@ -11,6 +11,7 @@
 // Work is tiny (<= 26*127*127 line integrals of <= 25 samples; ~650 for 5 people) and latency-
 // bound: one workgroup per (pair, frame), lanes over (i, j).
 #include "kernels.h"
+#include "heat_dev.h"
 #include "../common.h"
 
 namespace opk {
@@ -19,11 +20,12 @@ namespace {
 
 __device__ __forceinline__ int round_pos(float a) { return int(a + 0.5f); }
 
-__device__ __forceinline__ float score_ab(const float* a, const float* b, const float* mx,
-                                          const float* my, int W, int H, float inter_th,
+__device__ __forceinline__ float score_ab(const float* a, const float* b, const HeatMap& M,
+                                          int plane_x, int plane_y, float inter_th,
                                           float inter_min_above, float reject_score,
                                           double near_dist)
 {
+    const int W = M.w, H = M.h;
     const float vx = b[0] - a[0];
     const float vy = b[1] - a[1];
     const float vmax = fmaxf(fabsf(vx), fabsf(vy));
@@ -37,8 +39,7 @@ __device__ __forceinline__ float score_ab(const float* a, const float* b, const 
     for (int s = 0; s < n; ++s) {
         const int px = max(0, min(W - 1, round_pos(a[0] + (float)s * stepx)));
         const int py = max(0, min(H - 1, round_pos(a[1] + (float)s * stepy)));
-        const size_t idx = (size_t)py * W + px;
-        const float v = ux * mx[idx] + uy * my[idx];
+        const float v = ux * heat_at(M, plane_x, px, py) + uy * heat_at(M, plane_y, px, py);
         if (v > inter_th) {
             sum += v;
             ++count;
@@ -50,9 +51,9 @@ __device__ __forceinline__ float score_ab(const float* a, const float* b, const 
 }
 
 struct PafArgs {
-    const float* heat;
+    HeatMap heat;
     const float* peaks;
-    int heat_channels, h, w, max_peaks;
+    int max_peaks;
     int npairs, nparts;
     const int* pairs;
     const int* mapx;
@@ -62,8 +63,7 @@ struct PafArgs {
 };
 
 __device__ __forceinline__ void pair_setup(const PafArgs& A, int b, int q, const float*& ca,
-                                           const float*& cb, const float*& mx, const float*& my,
-                                           int& na, int& nb)
+                                           const float*& cb, int& px, int& py, int& na, int& nb)
 {
     const size_t stride = (size_t)(A.max_peaks + 1) * 3;
     const float* pk = A.peaks + (size_t)b * A.nparts * stride;
@@ -71,23 +71,21 @@ __device__ __forceinline__ void pair_setup(const PafArgs& A, int b, int q, const
     cb = pk + A.pairs[2 * q + 1] * stride;
     na = round_pos(ca[0]);
     nb = round_pos(cb[0]);
-    const size_t area = (size_t)A.h * A.w;
-    const float* hm = A.heat + (size_t)b * A.heat_channels * area;
-    mx = hm + A.mapx[q] * area;
-    my = hm + A.mapy[q] * area;
+    px = b * A.heat.channels + A.mapx[q];
+    py = b * A.heat.channels + A.mapy[q];
 }
 
 __global__ __launch_bounds__(256) void paf_dense_kernel(float* __restrict__ scores, PafArgs A)
 {
     const int q = blockIdx.x, b = blockIdx.y;
-    const float *ca, *cb, *mx, *my;
-    int na, nb;
-    pair_setup(A, b, q, ca, cb, mx, my, na, nb);
+    const float *ca, *cb;
+    int plx, ply, na, nb;
+    pair_setup(A, b, q, ca, cb, plx, ply, na, nb);
     float* out = scores + ((size_t)b * A.npairs + q) * A.max_peaks * A.max_peaks;
     for (int t = threadIdx.x; t < na * nb; t += blockDim.x) {
         const int i = t / nb, j = t - (t / nb) * nb;
         out[(size_t)i * A.max_peaks + j] =
-            score_ab(ca + 3 * (i + 1), cb + 3 * (j + 1), mx, my, A.w, A.h, A.inter_th,
+            score_ab(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
                      A.inter_min_above, A.reject_score, A.near_dist);
     }
 }
@@ -98,9 +96,9 @@ __global__ __launch_bounds__(256) void paf_compact_kernel(float* __restrict__ re
                                                           int rec_floats, PafArgs A)
 {
     const int q = blockIdx.x, b = blockIdx.y;
-    const float *ca, *cb, *mx, *my;
-    int na, nb;
-    pair_setup(A, b, q, ca, cb, mx, my, na, nb);
+    const float *ca, *cb;
+    int plx, ply, na, nb;
+    pair_setup(A, b, q, ca, cb, plx, ply, na, nb);
     const size_t stride = (size_t)(A.max_peaks + 1) * 3;
     const float* pk = A.peaks + (size_t)b * A.nparts * stride;
     int offset = 0, total = 0;
@@ -116,21 +114,17 @@ __global__ __launch_bounds__(256) void paf_compact_kernel(float* __restrict__ re
     float* out = rec + 1 + offset;
     for (int t = threadIdx.x; t < na * nb; t += blockDim.x) {
         const int i = t / nb, j = t - (t / nb) * nb;
-        out[t] = score_ab(ca + 3 * (i + 1), cb + 3 * (j + 1), mx, my, A.w, A.h, A.inter_th,
+        out[t] = score_ab(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
                           A.inter_min_above, A.reject_score, A.near_dist);
     }
 }
 
-PafArgs make_args(const float* heat, const float* peaks, int heat_channels, int h, int w,
-                  int max_peaks, const PafPairTable& t, float inter_th, float inter_min_above,
-                  float reject_score, double near_dist)
+PafArgs make_args(const HeatMap& heat, const float* peaks, int max_peaks, const PafPairTable& t,
+                  float inter_th, float inter_min_above, float reject_score, double near_dist)
 {
     PafArgs a{};
     a.heat = heat;
     a.peaks = peaks;
-    a.heat_channels = heat_channels;
-    a.h = h;
-    a.w = w;
     a.max_peaks = max_peaks;
     a.npairs = t.npairs;
     a.nparts = t.nparts;
@@ -146,27 +140,26 @@ PafArgs make_args(const float* heat, const float* peaks, int heat_channels, int 
 
 }  // namespace
 
-void launch_paf_scores(float* scores, const float* heat, const float* peaks, int frames,
-                       int heat_channels, int h, int w, int max_peaks, const PafPairTable& t,
-                       float inter_th, float inter_min_above, float reject_score,
-                       double near_dist, hipStream_t stream)
+void launch_paf_scores(float* scores, const HeatMap& heat, const float* peaks, int frames,
+                       int max_peaks, const PafPairTable& t, float inter_th,
+                       float inter_min_above, float reject_score, double near_dist,
+                       hipStream_t stream)
 {
     OPK_CHECK_ARG(frames > 0 && t.npairs > 0 && max_peaks > 0, "bad sizes");
-    PafArgs a = make_args(heat, peaks, heat_channels, h, w, max_peaks, t, inter_th,
-                          inter_min_above, reject_score, near_dist);
+    PafArgs a = make_args(heat, peaks, max_peaks, t, inter_th, inter_min_above, reject_score,
+                          near_dist);
     hipLaunchKernelGGL(paf_dense_kernel, dim3(t.npairs, frames), dim3(256), 0, stream, scores, a);
     OPK_LAUNCH_CHECK();
 }
 
-void launch_paf_scores_compact(float* records, int rec_floats, const float* heat,
-                               const float* peaks, int frames, int heat_channels, int h, int w,
-                               int max_peaks, const PafPairTable& t, float inter_th,
-                               float inter_min_above, float reject_score, double near_dist,
-                               hipStream_t stream)
+void launch_paf_scores_compact(float* records, int rec_floats, const HeatMap& heat,
+                               const float* peaks, int frames, int max_peaks,
+                               const PafPairTable& t, float inter_th, float inter_min_above,
+                               float reject_score, double near_dist, hipStream_t stream)
 {
     OPK_CHECK_ARG(frames > 0 && t.npairs > 0 && max_peaks > 0 && rec_floats > 1, "bad sizes");
-    PafArgs a = make_args(heat, peaks, heat_channels, h, w, max_peaks, t, inter_th,
-                          inter_min_above, reject_score, near_dist);
+    PafArgs a = make_args(heat, peaks, max_peaks, t, inter_th, inter_min_above, reject_score,
+                          near_dist);
     hipLaunchKernelGGL(paf_compact_kernel, dim3(t.npairs, frames), dim3(256), 0, stream, records,
                        rec_floats, a);
     OPK_LAUNCH_CHECK();

@@ -13,6 +13,7 @@
 // LDS column, then forms the 16 vertical combinations.  Stores are row-contiguous (1 KiB per wave
 // instruction); source reads hit L1/L2 (the net output is 1.2 MB per frame).
 #include "kernels.h"
+#include "heat_dev.h"
 #include "../common.h"
 
 namespace opk {
@@ -30,18 +31,6 @@ struct ResizeArgs {
     float inv_n;
 };
 
-__device__ __forceinline__ int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
-
-// horizontal pass of one source row at output column x (CPU order: ((t0 + t1) + t2) + t3)
-__device__ __forceinline__ float hpass(const float* row, int sw, int x0, const float* a)
-{
-    const float v0 = row[clampi(x0 - 1, 0, sw - 1)];
-    const float v1 = row[clampi(x0, 0, sw - 1)];
-    const float v2 = row[clampi(x0 + 1, 0, sw - 1)];
-    const float v3 = row[clampi(x0 + 2, 0, sw - 1)];
-    return v0 * a[0] + v1 * a[1] + v2 * a[2] + v3 * a[3];
-}
-
 __global__ __launch_bounds__(TX) void resize_merge_kernel(float* __restrict__ dst, ResizeArgs args)
 {
     __shared__ float hbuf[MAXR * TX];
@@ -56,8 +45,8 @@ __global__ __launch_bounds__(TX) void resize_merge_kernel(float* __restrict__ ds
     for (int n = 0; n < args.nsrc; ++n) {
         const ResizeSource& S = args.s[n];
         const float* src = S.src + (size_t)plane * S.sh * S.sw;
-        const int r_lo = clampi(S.yofs[y0] - 1, 0, S.sh - 1);
-        const int r_hi = clampi(S.yofs[y1 - 1] + 2, 0, S.sh - 1);
+        const int r_lo = heat_clampi(S.yofs[y0] - 1, 0, S.sh - 1);
+        const int r_hi = heat_clampi(S.yofs[y1 - 1] + 2, 0, S.sh - 1);
         const int nrows = r_hi - r_lo + 1;
         int x0 = 0;
         float a[4] = {0.f, 0.f, 0.f, 0.f};
@@ -69,7 +58,7 @@ __global__ __launch_bounds__(TX) void resize_merge_kernel(float* __restrict__ ds
         const bool tiled = nrows <= MAXR;   // block-uniform
         if (tiled && x < dw)
             for (int r = 0; r < nrows; ++r)
-                hbuf[r * TX + tx] = hpass(src + (size_t)(r_lo + r) * S.sw, S.sw, x0, a);
+                hbuf[r * TX + tx] = cubic_hpass(src + (size_t)(r_lo + r) * S.sw, S.sw, x0, a);
 #pragma unroll
         for (int j = 0; j < TY; ++j) {
             const int y = y0 + j;
@@ -80,9 +69,9 @@ __global__ __launch_bounds__(TX) void resize_merge_kernel(float* __restrict__ ds
                 float h[4];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const int r = clampi(yb + k, 0, S.sh - 1);
+                    const int r = heat_clampi(yb + k, 0, S.sh - 1);
                     h[k] = tiled ? hbuf[(r - r_lo) * TX + tx]
-                                 : hpass(src + (size_t)r * S.sw, S.sw, x0, a);
+                                 : cubic_hpass(src + (size_t)r * S.sw, S.sw, x0, a);
                 }
                 v = h[0] * b.x + h[1] * b.y + h[2] * b.z + h[3] * b.w;
             }

@@ -82,10 +82,13 @@ def test_pose_injection_batch_bitexact(ctx):
                        np.random.default_rng(k).normal(0, 0.01, (78, 46, 82)).astype(np.float32)
                        for k in range(3)]).astype(np.float32)
     pose = PoseExtractor(ctx, None)
-    pose.forward_net_output(_dev(fields), (656, 368), (1280, 720))
+    net_out = _dev(fields)   # stays alive: heat maps are evaluated lazily from it
+    pose.forward_net_output(net_out, (656, 368), (1280, 720))
     s = pose.scale_net_to_output()
     assert abs(s - 1.959128) < 1e-5                  # poseExtractorCaffe.cpp:306-310
     off = float(np.float32(0.5 / np.float64(s)))
+    gpu_peaks = pose.peaks_numpy()
+    gpu_heat = pose.heatmaps_numpy()                 # materialised on request
     for k in range(3):
         heat = oracle.resize_merge([fields[k]], 368, 656)
         peaks = oracle.nms(heat, 0.05, 128, (off, off))
@@ -94,6 +97,11 @@ def test_pose_injection_batch_bitexact(ctx):
         assert len(kp) >= 1
         np.testing.assert_array_equal(kp, rk)
         np.testing.assert_array_equal(ks, rs)
+        for c in range(25):
+            n = int(peaks[c, 0, 0])
+            assert int(gpu_peaks[k, c, 0, 0]) == n
+            np.testing.assert_array_equal(gpu_peaks[k, c, 1:n + 1], peaks[c, 1:n + 1])
+        np.testing.assert_array_equal(gpu_heat[k], heat)
 
 
 def test_end_to_end_keypoints_within_tolerance(ctx):

@@ -48,13 +48,15 @@ def test_resize_multiscale_bitexact(ctx):
     np.testing.assert_array_equal(out.cpu().numpy()[0], ref)
 
 
-@pytest.mark.parametrize("kind", ["people", "noise", "noise_dense"])
+@pytest.mark.parametrize("kind", ["people", "noise", "noise_sorted", "noise_dense"])
 def test_nms_bitexact(ctx, kind):
     if kind == "people":
         f = np.stack([people_field(5, 368, 656, seed=s) for s in (1, 2)])
     elif kind == "noise":
         f = np.stack([noise_field(78, 64, 96, seed=s) for s in (3, 4)])
-    else:   # > 127 peaks per part: truncation at maxPeaks
+    elif kind == "noise_sorted":   # 128..1024 peaks per part: candidate sort + maxPeaks truncation
+        f = np.stack([noise_field(25, 100, 100, seed=s, levels=5, density=1.0) for s in (6, 7)])
+    else:   # > 1024 peaks per part (kNmsCandidates): the ordered re-scan fallback
         f = np.stack([noise_field(78, 200, 200, seed=s, levels=5, density=1.0) for s in (5,)])
     n = f.shape[0]
     peaks = torch.zeros((n, 25, 128, 3), device="cuda")
