@@ -103,6 +103,8 @@ def main():
     flops_frame = net.flops_per_frame(NET_H, NET_W)
     out_shape = (B, 78, NET_H // 8, NET_W // 8)
 
+    # Two-stage pipeline (opk_pose_submit / opk_pose_collect): the device work of batch i+1 is
+    # enqueued before the host assembly of batch i, which then overlaps it.
     def step(i, ev=None):
         x = frames[i % 2]
         if ev is not None:
@@ -110,10 +112,17 @@ def main():
         p, shape = net.forward(x)
         if ev is not None:
             ev[1].record()
-        pose.forward_net_output((p, shape), (NET_W, NET_H), PRODUCER)
+        pose.submit_net_output((p, shape), (NET_W, NET_H), PRODUCER)
+        if pose.pending() > 1:
+            pose.collect()
+
+    def drain():
+        while pose.pending() > 0:
+            pose.collect()
 
     for i in range(args.warmup):
         step(i)
+    drain()
     torch.cuda.synchronize()
     people = [pose.num_people(f) for f in range(B)]
     net.forward(frames[0])
@@ -128,6 +137,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i, events[i])
+    drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -147,6 +147,18 @@ int opk_pose_forward(opk_pose* pose, const float* frames_dev, int n, int net_h, 
  * [n][78][h][w]; net_h/net_w = the net input size it corresponds to */
 int opk_pose_forward_net_output(opk_pose* pose, const float* net_output_dev, int n, int out_h,
                                 int out_w, int net_h, int net_w, int producer_w, int producer_h);
+/* Pipelined use (the reference's producer/worker/consumer threads, wrapperAuxiliary.hpp, on one
+ * GPU): submit enqueues a batch's device work (net, NMS, PAF scores) and returns; collect waits
+ * for the OLDEST submitted batch, assembles its people on the host and makes it the batch the
+ * result accessors below refer to.  At most two batches in flight: submit(i+1) then collect(i)
+ * overlaps the host assembly of batch i with the device work of batch i+1.  opk_pose_forward* =
+ * submit + collect.  *frames (may be NULL) receives the collected batch's frame count. */
+int opk_pose_submit(opk_pose* pose, const float* frames_dev, int n, int net_h, int net_w,
+                    int producer_w, int producer_h);
+int opk_pose_submit_net_output(opk_pose* pose, const float* net_output_dev, int n, int out_h,
+                               int out_w, int net_h, int net_w, int producer_w, int producer_h);
+int opk_pose_collect(opk_pose* pose, int* frames);
+int opk_pose_pending(opk_pose* pose);   /* batches in flight, -1 for NULL */
 /* optional additive overlay on the net output before resize (synthetic-people workloads):
  * [n][78][out_h][out_w] device fp32, NULL to disable */
 int opk_pose_set_overlay(opk_pose* pose, const float* overlay_dev);
@@ -156,8 +168,8 @@ int opk_pose_keypoints(opk_pose* pose, int frame, float* keypoints_host, float* 
 /* device pointers of the last forward's heatmaps [n][78][H][W] and peaks [n][25][128][3].
  * The pipeline evaluates heat-map values lazily from the net output (NMS and PAF scoring compute
  * the resized values they touch, bit-identical to resizeAndMerge); opk_pose_heatmaps writes the
- * full stack on first request after a forward.  With opk_pose_forward_net_output the net output
- * buffer must stay unchanged until then. */
+ * full stack on first request after a collect, while no later batch is in flight.  With
+ * opk_pose_forward_net_output the net output buffer must stay unchanged until then. */
 int opk_pose_heatmaps(opk_pose* pose, float** heat_dev, int shape[4]);
 int opk_pose_peaks(opk_pose* pose, float** peaks_dev, int shape[4]);
 float opk_pose_scale_net_to_output(opk_pose* pose);

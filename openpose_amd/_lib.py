@@ -51,6 +51,10 @@ _SIGS = {
     "opk_pose_forward": (_i, [_p, _p, _i, _i, _i, _i, _i]),
     "opk_pose_forward_net_output": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i]),
     "opk_pose_set_overlay": (_i, [_p, _p]),
+    "opk_pose_submit": (_i, [_p, _p, _i, _i, _i, _i, _i]),
+    "opk_pose_submit_net_output": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i]),
+    "opk_pose_collect": (_i, [_p, _ip]),
+    "opk_pose_pending": (_i, [_p]),
     "opk_pose_num_people": (_i, [_p, _i]),
     "opk_pose_keypoints": (_i, [_p, _i, _p, _p, _i]),
     "opk_pose_heatmaps": (_i, [_p, _c.POINTER(_p), _ip]),

@@ -240,6 +240,31 @@ class PoseExtractor:
                                                  net_size[1], net_size[0], producer_size[0],
                                                  producer_size[1]))
 
+    def submit(self, frames, producer_size):
+        """Enqueue a batch's device work and return (pipelined use; see opk_pose_submit)."""
+        n, _, h, w = frames.shape
+        check(self.L.opk_pose_submit(self.h, _ptr(frames), n, h, w, producer_size[0],
+                                     producer_size[1]))
+
+    def submit_net_output(self, net_output, net_size, producer_size):
+        if isinstance(net_output, tuple):
+            ptr, shape = net_output
+            ptr = ctypes.c_void_p(ptr)
+        else:
+            ptr, shape = _ptr(net_output), net_output.shape
+        check(self.L.opk_pose_submit_net_output(self.h, ptr, shape[0], shape[2], shape[3],
+                                                net_size[1], net_size[0], producer_size[0],
+                                                producer_size[1]))
+
+    def collect(self):
+        """Wait for the oldest submitted batch, assemble its people; returns its frame count."""
+        n = ctypes.c_int(0)
+        check(self.L.opk_pose_collect(self.h, ctypes.byref(n)))
+        return n.value
+
+    def pending(self):
+        return self.L.opk_pose_pending(self.h)
+
     def num_people(self, frame):
         return self.L.opk_pose_num_people(self.h, frame)
 

@@ -166,6 +166,34 @@ int opk_pose_forward_net_output(opk_pose* p, const float* out, int n, int oh, in
     });
 }
 
+int opk_pose_submit(opk_pose* p, const float* frames, int n, int net_h, int net_w, int pw, int ph)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->submit(frames, n, net_h, net_w, pw, ph);
+    });
+}
+
+int opk_pose_submit_net_output(opk_pose* p, const float* out, int n, int oh, int ow, int net_h,
+                               int net_w, int pw, int ph)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->submit_net_output(out, n, oh, ow, net_h, net_w, pw, ph);
+    });
+}
+
+int opk_pose_collect(opk_pose* p, int* frames)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        const int n = p->pose->collect();
+        if (frames) *frames = n;
+    });
+}
+
+int opk_pose_pending(opk_pose* p) { return p ? p->pose->pending() : -1; }
+
 int opk_pose_set_overlay(opk_pose* p, const float* overlay)
 {
     return guarded_net([&] {

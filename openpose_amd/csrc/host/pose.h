@@ -8,9 +8,17 @@
 
 namespace opk {
 
+// Two-stage pipeline, the single-GPU equivalent of the reference's worker threads
+// (WPoseExtractor feeding the CPU-side consumers through WQueue, wrapper/wrapperAuxiliary.hpp):
+//   submit  -- enqueue the device work of a batch (net, NMS, PAF scores, D2H of the results) on
+//              the context stream and return;
+//   collect -- wait for the oldest submitted batch and assemble its people on the host.
+// With one batch in flight, the host assembly of batch i overlaps the device work of batch i+1.
+// forward() = submit + collect.
 class PoseHip {
 public:
     PoseHip(Context* ctx, NetHip* net, bool maximize_positives);
+    ~PoseHip();
 
     void set_property(int prop, double v);
     double property(int prop) const { return props_[prop]; }
@@ -19,32 +27,53 @@ public:
     void forward(const float* frames, int n, int net_h, int net_w, int prod_w, int prod_h);
     void forward_net_output(const float* net_out, int n, int out_h, int out_w, int net_h,
                             int net_w, int prod_w, int prod_h);
+    void submit(const float* frames, int n, int net_h, int net_w, int prod_w, int prod_h);
+    void submit_net_output(const float* net_out, int n, int out_h, int out_w, int net_h,
+                           int net_w, int prod_w, int prod_h);
+    int collect();                       // frames of the collected batch
+    int pending() const { return count_; }
 
+    // results of the last collected batch
     int frames() const { return (int)people_.size(); }
     int num_people(int f) const { return people_.at(f); }
     const std::vector<float>& keypoints(int f) const { return kp_.at(f); }
     const std::vector<float>& scores(int f) const { return ks_.at(f); }
-    // full-resolution heat maps of the last forward, materialised on first request (the pipeline
-    // itself evaluates them lazily from the net output: HeatMap in kernels.h)
+    // full-resolution heat maps of the last collected batch, materialised on first request (the
+    // pipeline evaluates them lazily from the net output: HeatMap in kernels.h); only while no
+    // later batch is in flight (its net forward overwrites the net output)
     float* heatmaps(int shape[4]);
     float* peaks(int shape[4]) const;
     float scale_net_to_output() const { return scale_net_to_output_; }
 
+    static constexpr int kMaxPeaks = kPoseMaxPeople;   // peaks blob [25][128][3]
+    static constexpr int kRecordHead = 16384;          // record floats copied eagerly per frame
+
 private:
+    struct Slot {
+        DevBuf peaks, records;
+        HostBuf hpeaks, hrecords;
+        hipEvent_t done = nullptr;
+        int n = 0, H = 0, W = 0;
+        float scale = 1.f;
+        HeatMap heat{};
+    };
+    size_t record_floats() const;        // per frame: 1 + every candidate pair of the model
+
     Context* ctx_;
     NetHip* net_;
     bool maximize_positives_;
     double props_[5];
     const float* overlay_ = nullptr;
-    float scale_net_to_output_ = 1.f;
+    hipStream_t copy_ = nullptr;         // D2H of collected batches (overlaps the next batch)
 
+    Slot slots_[2];
+    int head_ = 0, count_ = 0, last_ = -1;
+    std::vector<float> overflow_;        // records longer than kRecordHead
+
+    float scale_net_to_output_ = 1.f;
     int n_ = 0, hh_ = 0, hw_ = 0;
-    HeatMap lazy_{};            // last forward's heat maps as resize of the net output
-    bool heat_valid_ = false;   // heat_ holds them
-    DevBuf heat_, peaks_, records_, dense_;
-    HostBuf hpeaks_, hrecords_, hdense_;
-    static constexpr int kMaxPeaks = kPoseMaxPeople;   // peaks blob [25][128][3]
-    static constexpr int kRecordFloats = 16384;        // compact PAF scores per frame
+    bool heat_valid_ = false;
+    DevBuf heat_;
     std::vector<int> people_;
     std::vector<std::vector<float>> kp_, ks_;
 };

@@ -128,3 +128,31 @@ def test_end_to_end_keypoints_within_tolerance(ctx):
         np.testing.assert_array_equal(kp[..., 2] > 0, rk[..., 2] > 0)   # same parts found
         assert np.abs(kp[..., :2] - rk[..., :2]).max() / s <= KEYPOINT_TOL
         assert np.abs(ks - rs).max() <= KEYPOINT_TOL
+
+
+def test_pose_submit_collect_pipeline(ctx):
+    """Two batches in flight (opk_pose_submit / opk_pose_collect) give the synchronous results."""
+    def fields(seed):
+        return np.stack([synth.overlay(3, 46, 82, seed=seed + k) +
+                         np.random.default_rng(seed + k).normal(0, 0.01, (78, 46, 82))
+                         for k in range(2)]).astype(np.float32)
+
+    fa, fb = fields(700), fields(800)
+    sync = PoseExtractor(ctx, None)
+    ref = []
+    for f in (fa, fb):
+        d = _dev(f)
+        sync.forward_net_output(d, (656, 368), (1280, 720))
+        ref.append([sync.keypoints(k) for k in range(2)])
+    pipe = PoseExtractor(ctx, None)
+    da, db = _dev(fa), _dev(fb)
+    pipe.submit_net_output(da, (656, 368), (1280, 720))
+    pipe.submit_net_output(db, (656, 368), (1280, 720))
+    assert pipe.pending() == 2
+    for r in ref:
+        assert pipe.collect() == 2
+        for k in range(2):
+            kp, ks = pipe.keypoints(k)
+            np.testing.assert_array_equal(kp, r[k][0])
+            np.testing.assert_array_equal(ks, r[k][1])
+    assert pipe.pending() == 0
