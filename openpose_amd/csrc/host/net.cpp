@@ -221,7 +221,7 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
     // halo-kernel layout (conv3.hip): [cout_pad/BN][cin_pad/32][ky][kx][n BN][ci 32]
     std::vector<uint16_t> packed3;
     if (c.ntaps == 9 && !c.from_image) {
-        const int BN = conv3_shape(1, c.info.cout).bn;   // BN depends on cout only
+        const int BN = conv3_shape(1, 1, 1, c.info.cout).bn;   // BN depends on cout only
         const int nb = (c.info.cout + BN - 1) / BN, cpt = c.cin_pad / 32;
         packed3.assign((size_t)nb * cpt * 9 * BN * 32, 0);
         for (int co = 0; co < c.info.cout; ++co)
@@ -322,7 +322,7 @@ void NetHip::reshape(int n, int h, int w)
         a.ksteps = c.ksteps;
         c.use3 = allow3 && c.ntaps == 9 && !c.from_image && c.w3.ptr != nullptr && c.out32_coff < 0;
         if (c.use3) {
-            const Conv3Shape s3 = conv3_shape(W, c.info.cout);
+            const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout);
             a.sw = s3.sw;
             a.nstrips = s3.nstrips;
         }

@@ -28,6 +28,8 @@
 // registers (no LDS pass).
 #include "conv.h"
 
+#include <cstdlib>
+
 #include "../common.h"
 
 namespace opk {
@@ -116,19 +118,26 @@ struct Strips {
     }
 };
 
-template <int BM, int BN, int HR>
-__global__ __launch_bounds__(512, 1) void conv3_kernel(const ConvArgs a)
+// TAPU: taps per K unit (3 = one ky row of taps, 1 = a single tap); MINB: workgroups per CU the
+// LDS budget allows (2 -> 80 KB: the other workgroup's MFMAs cover this one's prologue, barrier
+// and epilogue stalls).
+template <int BM, int BN, int HR, int TAPU, int MINB>
+__global__ __launch_bounds__(512, MINB) void conv3_kernel(const ConvArgs a)
 {
     constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
     static_assert(WAVES_M * 64 == BM && WAVES_N * 64 == BN, "64 x 64 wave tiles");
+    static_assert(TAPU == 1 || TAPU == 3, "taps per unit");
     constexpr int MF = 4, NF = 4;
-    constexpr int AI = HR / 128;                  // halo DMA instructions per wave (16 rows each)
-    constexpr int BROWS = 3 * BN;                 // B rows per unit: kx-major, then channel n
+    constexpr int UPC = 9 / TAPU;                 // units per 32-channel chunk
+    constexpr int API = HR / 16;                  // halo DMA instructions per block (16 rows each)
+    constexpr int AIW = (API + 7) / 8;            // ... per wave, at most
+    constexpr int BROWS = TAPU * BN;              // B rows per unit: tap-major, then channel n
     constexpr int BPI = BROWS / 16;               // B DMA instructions per block per unit
     constexpr int ASLOT = HR * 4;                 // 16-byte pieces per halo slot
     constexpr int BSLOT = BROWS * 4;
     constexpr int LDS_PIECES = 2 * ASLOT + 3 * BSLOT;
-    static_assert(LDS_PIECES * 16 <= 160 * 1024, "LDS budget");
+    static_assert(HR % 16 == 0 && BROWS % 16 == 0, "DMA granularity");
+    static_assert(LDS_PIECES * 16 * MINB <= 160 * 1024, "LDS budget");
     __shared__ uint4 lds[LDS_PIECES];
 
     OPK3_STAMP(0);
@@ -148,32 +157,34 @@ __global__ __launch_bounds__(512, 1) void conv3_kernel(const ConvArgs a)
     // ---- DMA lane geometry: 16 rows x 4 pieces per wave instruction --------------------------
     const int lrow = lane >> 2, phys = lane & 3;
     const int cpt = a.cin_pad >> 5;               // 32-channel chunks
-    const int U = 3 * cpt;                        // units (chunk, ky)
+    const int U = UPC * cpt;                      // units (chunk, taps)
     // halo row hr = (i*8 + wave)*16 + lrow holds virtual position p0 - VW - 1 + hr; its image
     // address (chunk 0, swizzled piece) is fixed for the whole tile
-    const uint16_t* arow[AI];
+    const uint16_t* arow[AIW];
 #pragma unroll
-    for (int i = 0; i < AI; ++i) {
+    for (int i = 0; i < AIW; ++i) {
         const int hr = (i * 8 + wave) * 16 + lrow;
         const int lp = phys ^ (((hr >> 2) & 1) << 1);
         int yy, xx, s;
         const long pos = g.map(p0 - g.VW - 1 + hr, yy, xx, s);
         arow[i] = a.in + a.in_coff + pos * a.in_cs + lp * 8;
     }
-    // B: this wave issues instructions j*8 + wave < BPI of every unit
+    // this wave issues halo instructions i*8 + wave < API and B instructions j*8 + wave < BPI
+    const int ai = (API - wave + 7) / 8;
     const int bi = (BPI - wave + 7) / 8;
-    const uint16_t* wbase = a.w + (size_t)nb * cpt * 3 * BROWS * 32;
+    const uint16_t* wbase = a.w + (size_t)nb * cpt * 9 * BN * 32;
 
 #define OPK3_ISSUE(u_)                                                                        \
     do {                                                                                      \
-        const int c_ = (u_) / 3, ky_ = (u_) - 3 * ((u_) / 3);                                 \
-        if (ky_ == 0) {                                                                       \
+        const int c_ = (u_) / UPC;                                                            \
+        if ((u_) - c_ * UPC == 0) {                                                           \
             const int as_ = (c_ & 1) * ASLOT;                                                 \
-            _Pragma("unroll") for (int i_ = 0; i_ < AI; ++i_)                                 \
-                __builtin_amdgcn_global_load_lds(                                             \
-                    (const void*)(arow[i_] + c_ * 32),                                        \
-                    (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * 8 + wave) * 64]), \
-                    16, 0, 0);                                                                \
+            _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
+                if (API % 8 == 0 || i_ * 8 + wave < API)                                      \
+                    __builtin_amdgcn_global_load_lds(                                         \
+                        (const void*)(arow[i_] + c_ * 32),                                    \
+                        (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * 8 + wave) * 64]), \
+                        16, 0, 0);                                                            \
         }                                                                                     \
         const int bs_ = 2 * ASLOT + ((u_) % 3) * BSLOT;                                       \
         const uint16_t* ub_ = wbase + (size_t)(u_) * BROWS * 32;                              \
@@ -197,30 +208,36 @@ __global__ __launch_bounds__(512, 1) void conv3_kernel(const ConvArgs a)
 
     const int r16 = lane & 15, q = lane >> 4;
     // bias and negative-side multiplier (1: identity, 0: ReLU, slope: PReLU) of this lane's
-    // output channels, fetched before the K loop
+    // output channels; fetched before the K loop when registers allow (MINB == 1)
     float4_t bv[NF], mv[NF];
     const float neg = a.act == 1 ? 0.f : 1.f;
-#pragma unroll
-    for (int j = 0; j < NF; ++j) {   // bias/slope arrays are zero-padded to a multiple of 128
-        const int ch = n0 + wn * 64 + j * 16 + 4 * q;
-        bv[j] = *reinterpret_cast<const float4_t*>(a.bias + ch);
-        const float4_t sl = *reinterpret_cast<const float4_t*>(a.slope + ch);
-        mv[j] = a.act == 2 ? sl : float4_t{neg, neg, neg, neg};
-    }
+#define OPK3_BIAS()                                                                           \
+    do {                                                                                      \
+        _Pragma("unroll") for (int j_ = 0; j_ < NF; ++j_) {                                   \
+            /* bias/slope arrays are zero-padded to a multiple of 128 channels */             \
+            const int ch_ = n0 + wn * 64 + j_ * 16 + 4 * q;                                   \
+            bv[j_] = *reinterpret_cast<const float4_t*>(a.bias + ch_);                        \
+            const float4_t sl_ = *reinterpret_cast<const float4_t*>(a.slope + ch_);           \
+            mv[j_] = a.act == 2 ? sl_ : float4_t{neg, neg, neg, neg};                         \
+        }                                                                                     \
+    } while (0)
+    if constexpr (MINB == 1) OPK3_BIAS();
 
     OPK3_ISSUE(0);
     if (U > 1) OPK3_ISSUE(1);
     for (int u = 0; u < U; ++u) {
-        const int ky = u - 3 * (u / 3);
+        const int c = u / UPC, t = u - (u / UPC) * UPC;
         // this wave's loads of unit u have landed once only unit u+1's may still be in flight
-        vm_wait_rt(u + 1 < U ? bi + (ky == 2 ? AI : 0) : 0);
+        vm_wait_rt(u + 1 < U ? bi + (t == UPC - 1 ? ai : 0) : 0);
         __builtin_amdgcn_s_barrier();
         if (u == 0) OPK3_STAMP(1);
         if (u + 2 < U) OPK3_ISSUE(u + 2);
-        const uint4* As = lds + ((u / 3) & 1) * ASLOT;
+        const uint4* As = lds + (c & 1) * ASLOT;
         const uint4* Bs = lds + 2 * ASLOT + (u % 3) * BSLOT;
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) {
+        for (int k = 0; k < TAPU; ++k) {
+            const int tap = t * TAPU + k;         // ky*3 + kx
+            const int ky = tap / 3, kx = tap - 3 * (tap / 3);
             half8_t fa[MF], fb[NF];
             const int hoff = ky * g.VW + kx;
 #pragma unroll
@@ -228,7 +245,7 @@ __global__ __launch_bounds__(512, 1) void conv3_kernel(const ConvArgs a)
                 fa[i] = __builtin_bit_cast(half8_t, As[swz64(wm * 64 + i * 16 + r16 + hoff, q)]);
 #pragma unroll
             for (int j = 0; j < NF; ++j)
-                fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(kx * BN + wn * 64 + j * 16 + r16, q)]);
+                fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(k * BN + wn * 64 + j * 16 + r16, q)]);
 #pragma unroll
             for (int i = 0; i < MF; ++i)
 #pragma unroll
@@ -238,6 +255,8 @@ __global__ __launch_bounds__(512, 1) void conv3_kernel(const ConvArgs a)
     }
 #undef OPK3_ISSUE
     OPK3_STAMP(2);
+    if constexpr (MINB != 1) OPK3_BIAS();
+#undef OPK3_BIAS
 
     // ---- epilogue straight from registers ------------------------------------------------------
     // lane (q, r16) of fragment (i, j) holds output channels ch..ch+3 (ch = n0 + wn*64 + j*16 + 4q)
@@ -297,12 +316,26 @@ __global__ __launch_bounds__(512, 1) void conv3_kernel(const ConvArgs a)
 
 }  // namespace
 
-Conv3Shape conv3_shape(int W, int cout)
+Conv3Shape conv3_shape(int frames, int H, int W, int cout)
 {
+    static const bool small = [] {   // dev A/B switch: OPK_CONV3_SMALL=0 -> one workgroup per CU
+        const char* e = std::getenv("OPK_CONV3_SMALL");
+        return !(e && e[0] == '0');
+    }();
     Conv3Shape s;
     s.bn = cout <= 64 ? 64 : 128;
-    s.bm = s.bn == 64 ? 512 : 256;
-    s.nstrips = (W + kConv3MaxStrip - 1) / kConv3MaxStrip;
+    // two workgroups per CU pay off once every CU gets at least two 256-position tiles (measured:
+    // +10-17 % on the 92x164 / 184x328 / 512-channel layers, -20 % at one tile per CU)
+    const long tiles = ((long)frames * (H + 2) * (W + 2) / 256) * ((cout + 127) / 128);
+    if (s.bn == 128 && small && tiles >= 2 * 256) {   // 80 KB of LDS
+        s.bm = 256; s.hr = 448; s.tapu = 1; s.minb = 2;
+    } else if (s.bn == 128) {
+        s.bm = 256; s.hr = 512; s.tapu = 3; s.minb = 1;
+    } else {
+        s.bm = 512; s.hr = 768; s.tapu = 3; s.minb = 1;
+    }
+    const int max_strip = (s.hr - s.bm - 2) / 2 - 2;   // halo: BM + 2 * (sw + 2) + 2 rows
+    s.nstrips = (W + max_strip - 1) / max_strip;
     s.sw = (W + s.nstrips - 1) / s.nstrips;
     return s;
 }
@@ -314,15 +347,19 @@ void launch_conv3(const ConvArgs& a, hipStream_t stream)
     OPK_CHECK_ARG(a.in_coff + a.cin_pad <= a.in_cs, "input slice exceeds the buffer");
     OPK_CHECK_ARG(a.M > 0 && a.cout > 0 && a.ndst <= kConvMaxDst, "bad sizes");
     OPK_CHECK_ARG(a.out32 == nullptr, "the halo kernel has no fp32 NCHW output");
-    const Conv3Shape s = conv3_shape(a.W, a.cout);
+    const Conv3Shape s = conv3_shape(a.frames, a.H, a.W, a.cout);
     OPK_CHECK_ARG(a.sw == s.sw && a.nstrips == s.nstrips, "strip geometry differs from conv3_shape");
-    OPK_CHECK_ARG(2 * (s.sw + 2) + 2 <= 256, "strip too wide for the halo (HR = BM + 256)");
+    OPK_CHECK_ARG(s.bm + 2 * (s.sw + 2) + 2 <= s.hr, "strip too wide for the halo");
     const long total = (long)a.frames * s.nstrips * (a.H + 2) * (s.sw + 2);
     OPK_CHECK_ARG(total < (1L << 30), "too many positions");
     const int nn = (a.cout + s.bn - 1) / s.bn;
     dim3 grid((unsigned)(((total + s.bm - 1) / s.bm) * nn));
-    if (s.bn == 128) hipLaunchKernelGGL((conv3_kernel<256, 128, 512>), grid, dim3(512), 0, stream, a);
-    else hipLaunchKernelGGL((conv3_kernel<512, 64, 768>), grid, dim3(512), 0, stream, a);
+    if (s.bn == 128 && s.minb == 2)
+        hipLaunchKernelGGL((conv3_kernel<256, 128, 448, 1, 2>), grid, dim3(512), 0, stream, a);
+    else if (s.bn == 128)
+        hipLaunchKernelGGL((conv3_kernel<256, 128, 512, 3, 1>), grid, dim3(512), 0, stream, a);
+    else
+        hipLaunchKernelGGL((conv3_kernel<512, 64, 768, 3, 1>), grid, dim3(512), 0, stream, a);
     OPK_LAUNCH_CHECK();
 }
 

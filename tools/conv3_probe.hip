@@ -78,7 +78,7 @@ int main(int argc, char** argv)
     a.dst_cs[0] = cout;
     a.dst_coff[0] = 0;
 
-    const Conv3Shape s3 = conv3_shape(W, cout);
+    const Conv3Shape s3 = conv3_shape(frames, H, W, cout);
     a.sw = s3.sw;
     a.nstrips = s3.nstrips;
     const long vtot = (long)frames * s3.nstrips * (H + 2) * (s3.sw + 2);
