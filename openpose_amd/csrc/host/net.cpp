@@ -218,18 +218,18 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
                 dst[t * c.cin_pad + ci] = f2h(w[(((size_t)co * cin + ci) * k + ky) * k + kx]);
         }
     }
-    // halo-kernel layout (conv3.hip): [cout_pad/BN][cin_pad/32][ky][kx][n BN][ci 32]
+    // conv3.hip layout: [cout_pad/BN][cin_pad/32][ky][kx][n BN][ci 32]
     std::vector<uint16_t> packed3;
-    if (c.ntaps == 9 && !c.from_image) {
-        const int BN = conv3_shape(1, 1, 1, c.info.cout).bn;   // BN depends on cout only
-        const int nb = (c.info.cout + BN - 1) / BN, cpt = c.cin_pad / 32;
-        packed3.assign((size_t)nb * cpt * 9 * BN * 32, 0);
+    if (!c.from_image) {
+        const int BN = conv3_shape(1, 1, 1, c.info.cout, k).bn;   // BN depends on cout only
+        const int nb = (c.info.cout + BN - 1) / BN, cpt = c.cin_pad / 32, kt = k * k;
+        packed3.assign((size_t)nb * cpt * kt * BN * 32, 0);
         for (int co = 0; co < c.info.cout; ++co)
             for (int ci = 0; ci < cin; ++ci)
-                for (int t = 0; t < 9; ++t) {
-                    const size_t unit = ((size_t)(co / BN) * cpt + ci / 32) * 3 + t / 3;
-                    const size_t idx = ((unit * 3 + t % 3) * BN + co % BN) * 32 + ci % 32;
-                    packed3[idx] = f2h(w[(((size_t)co * cin + ci) * 3 + t / 3) * 3 + t % 3]);
+                for (int t = 0; t < kt; ++t) {
+                    const size_t idx =
+                        ((((size_t)(co / BN) * cpt + ci / 32) * kt + t) * BN + co % BN) * 32 + ci % 32;
+                    packed3[idx] = f2h(w[(((size_t)co * cin + ci) * k + t / k) * k + t % k]);
                 }
     }
     // bias/slope zero-padded to a multiple of 128 channels (conv3 reads whole 4-channel groups)
@@ -320,9 +320,9 @@ void NetHip::reshape(int n, int h, int w)
         else
             a.tapoff[0] = Wp + 1;
         a.ksteps = c.ksteps;
-        c.use3 = allow3 && c.ntaps == 9 && !c.from_image && c.w3.ptr != nullptr && c.out32_coff < 0;
+        c.use3 = allow3 && !c.from_image && c.w3.ptr != nullptr;
         if (c.use3) {
-            const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout);
+            const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, c.info.k);
             a.sw = s3.sw;
             a.nstrips = s3.nstrips;
         }

@@ -42,17 +42,18 @@ struct ConvArgs {
 void launch_conv(const ConvArgs& a, int bn, hipStream_t stream);
 // v2 (conv2.hip): 512 lanes, 256 x bn tile, LDS-DMA 3-slot ring; bn: 32, 64, 96, 128 or 256
 void launch_conv2(const ConvArgs& a, int bn, hipStream_t stream);
-// v3 (conv3.hip): 3x3 only, input halo staged once per 32-channel chunk over a "virtual image" of
-// column strips (sw interior columns each).  Tile BM x BN = 256 x 128 (80 KB LDS, two workgroups
-// per CU), or 512 x 64 for cout <= 64.
-// Weights packed [cout_pad/BN][cin_pad/32][ky][kx][BN][32].  Reads padded positions down to -1
+// v3 (conv3.hip): 3x3 and 1x1, input halo staged once per 32-channel chunk over a "virtual image" of
+// column strips (sw interior columns each).  Tile BM x BN = 256 x 128 / 96 (<= 80 KB LDS, two
+// workgroups per CU, or 136 KB, one), 512 x 64 for cout <= 64; optional fp32 NCHW output (out32).
+// Weights packed [cout_pad/BN][cin_pad/32][ky][kx][BN][32] (BN = conv3_shape(...).bn).  Reads padded positions down to -1
 // and the whole row past the last one: buffers carry zeroed guards (kConvGuardTail positions).
 constexpr int kConvGuardTail = 1024;   // positions
 struct Conv3Shape {
+    int ks;                       // 3 or 1
     int bm, bn, hr, tapu, minb;   // tile, halo rows, taps per K unit, workgroups per CU
     int sw, nstrips;
 };
-Conv3Shape conv3_shape(int frames, int H, int W, int cout);
+Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks);
 void launch_conv3(const ConvArgs& a, hipStream_t stream);
 
 // NCHW fp32 [frames][3][H][W] -> padded NHWC fp16 [frames][H+2][W+2][32] holding, at each pixel,

@@ -100,9 +100,10 @@ struct Strips {
     {
     }
     // padded-image position of virtual position v (any v; outside the image -> -1, a zeroed guard)
-    __device__ long map(int v, int& yy, int& xx, int& s) const
+    __device__ long map(int v, int& f, int& yy, int& xx, int& s) const
     {
         if (v < 0 || v >= total) {
+            f = 0;
             yy = -1;
             xx = -1;
             s = 0;
@@ -112,7 +113,7 @@ struct Strips {
         const int rem = v - vf * fposV;
         yy = rem / VW;
         xx = rem - yy * VW;
-        const int f = vf / nstrips;
+        f = vf / nstrips;
         s = vf - f * nstrips;
         return (long)(f * (H + 2) + yy) * Wp + s * sw + xx;
     }
@@ -121,21 +122,28 @@ struct Strips {
 // TAPU: taps per K unit (3 = one ky row of taps, 1 = a single tap); MINB: workgroups per CU the
 // LDS budget allows (2 -> 80 KB: the other workgroup's MFMAs cover this one's prologue, barrier
 // and epilogue stalls).
-template <int BM, int BN, int HR, int TAPU, int MINB>
-__global__ __launch_bounds__(512, MINB) void conv3_kernel(const ConvArgs a)
+// KS: 3 (3x3, pad 1) or 1 (1x1: the "halo" is the tile itself, one tap per chunk).
+template <int BM, int BN, int HR, int TAPU, int MINB, int KS>
+__global__ __launch_bounds__(512, MINB) __attribute__((amdgpu_waves_per_eu(2 * MINB)))
+void conv3_kernel(const ConvArgs a)
 {
-    constexpr int WAVES_N = BN / 64, WAVES_M = 8 / WAVES_N;
-    static_assert(WAVES_M * 64 == BM && WAVES_N * 64 == BN, "64 x 64 wave tiles");
+    constexpr int WAVES_N = BN % 64 == 0 ? BN / 64 : 2, WAVES_M = 8 / WAVES_N;
+    constexpr int WROWS = BM / WAVES_M;            // wave tile WROWS x WN
+    constexpr int WN = BN / WAVES_N;
+    static_assert(WROWS % 16 == 0 && WROWS <= 64 && WN % 16 == 0 && WN <= 64, "wave tiles");
     static_assert(TAPU == 1 || TAPU == 3, "taps per unit");
-    constexpr int MF = 4, NF = 4;
-    constexpr int UPC = 9 / TAPU;                 // units per 32-channel chunk
+    static_assert(KS == 3 || (KS == 1 && TAPU == 1 && HR == BM), "1x1: one tap, halo = tile");
+    constexpr int MF = WROWS / 16, NF = WN / 16;
+    constexpr int KT = KS * KS;                   // taps
+    constexpr int UPC = KT / TAPU;                // units per 32-channel chunk
     constexpr int API = HR / 16;                  // halo DMA instructions per block (16 rows each)
     constexpr int AIW = (API + 7) / 8;            // ... per wave, at most
     constexpr int BROWS = TAPU * BN;              // B rows per unit: tap-major, then channel n
     constexpr int BPI = BROWS / 16;               // B DMA instructions per block per unit
     constexpr int ASLOT = HR * 4;                 // 16-byte pieces per halo slot
+    constexpr int NAS = UPC >= 2 ? 2 : 3;         // halo slots: unit u+2 may start chunk c+2 if UPC == 1
     constexpr int BSLOT = BROWS * 4;
-    constexpr int LDS_PIECES = 2 * ASLOT + 3 * BSLOT;
+    constexpr int LDS_PIECES = NAS * ASLOT + 3 * BSLOT;
     static_assert(HR % 16 == 0 && BROWS % 16 == 0, "DMA granularity");
     static_assert(LDS_PIECES * 16 * MINB <= 160 * 1024, "LDS budget");
     __shared__ uint4 lds[LDS_PIECES];
@@ -166,19 +174,20 @@ __global__ __launch_bounds__(512, MINB) void conv3_kernel(const ConvArgs a)
         const int hr = (i * 8 + wave) * 16 + lrow;
         const int lp = phys ^ (((hr >> 2) & 1) << 1);
         int yy, xx, s;
-        const long pos = g.map(p0 - g.VW - 1 + hr, yy, xx, s);
+        int f;
+        const long pos = g.map(p0 - (KS == 3 ? g.VW + 1 : 0) + hr, f, yy, xx, s);
         arow[i] = a.in + a.in_coff + pos * a.in_cs + lp * 8;
     }
     // this wave issues halo instructions i*8 + wave < API and B instructions j*8 + wave < BPI
     const int ai = (API - wave + 7) / 8;
     const int bi = (BPI - wave + 7) / 8;
-    const uint16_t* wbase = a.w + (size_t)nb * cpt * 9 * BN * 32;
+    const uint16_t* wbase = a.w + (size_t)nb * cpt * KT * BN * 32;
 
 #define OPK3_ISSUE(u_)                                                                        \
     do {                                                                                      \
         const int c_ = (u_) / UPC;                                                            \
         if ((u_) - c_ * UPC == 0) {                                                           \
-            const int as_ = (c_ & 1) * ASLOT;                                                 \
+            const int as_ = (c_ % NAS) * ASLOT;                                               \
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
                 if (API % 8 == 0 || i_ * 8 + wave < API)                                      \
                     __builtin_amdgcn_global_load_lds(                                         \
@@ -186,7 +195,7 @@ __global__ __launch_bounds__(512, MINB) void conv3_kernel(const ConvArgs a)
                         (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * 8 + wave) * 64]), \
                         16, 0, 0);                                                            \
         }                                                                                     \
-        const int bs_ = 2 * ASLOT + ((u_) % 3) * BSLOT;                                       \
+        const int bs_ = NAS * ASLOT + ((u_) % 3) * BSLOT;                                     \
         const uint16_t* ub_ = wbase + (size_t)(u_) * BROWS * 32;                              \
         _Pragma("unroll") for (int j_ = 0; j_ < (BPI + 7) / 8; ++j_) {                        \
             if (BPI % 8 == 0 || j_ * 8 + wave < BPI) {                                        \
@@ -215,7 +224,7 @@ __global__ __launch_bounds__(512, MINB) void conv3_kernel(const ConvArgs a)
     do {                                                                                      \
         _Pragma("unroll") for (int j_ = 0; j_ < NF; ++j_) {                                   \
             /* bias/slope arrays are zero-padded to a multiple of 128 channels */             \
-            const int ch_ = n0 + wn * 64 + j_ * 16 + 4 * q;                                   \
+            const int ch_ = n0 + wn * WN + j_ * 16 + 4 * q;                                   \
             bv[j_] = *reinterpret_cast<const float4_t*>(a.bias + ch_);                        \
             const float4_t sl_ = *reinterpret_cast<const float4_t*>(a.slope + ch_);           \
             mv[j_] = a.act == 2 ? sl_ : float4_t{neg, neg, neg, neg};                         \
@@ -232,20 +241,20 @@ __global__ __launch_bounds__(512, MINB) void conv3_kernel(const ConvArgs a)
         __builtin_amdgcn_s_barrier();
         if (u == 0) OPK3_STAMP(1);
         if (u + 2 < U) OPK3_ISSUE(u + 2);
-        const uint4* As = lds + (c & 1) * ASLOT;
-        const uint4* Bs = lds + 2 * ASLOT + (u % 3) * BSLOT;
+        const uint4* As = lds + (c % NAS) * ASLOT;
+        const uint4* Bs = lds + NAS * ASLOT + (u % 3) * BSLOT;
 #pragma unroll
         for (int k = 0; k < TAPU; ++k) {
             const int tap = t * TAPU + k;         // ky*3 + kx
             const int ky = tap / 3, kx = tap - 3 * (tap / 3);
             half8_t fa[MF], fb[NF];
-            const int hoff = ky * g.VW + kx;
+            const int hoff = KS == 3 ? ky * g.VW + kx : 0;
 #pragma unroll
             for (int i = 0; i < MF; ++i)
-                fa[i] = __builtin_bit_cast(half8_t, As[swz64(wm * 64 + i * 16 + r16 + hoff, q)]);
+                fa[i] = __builtin_bit_cast(half8_t, As[swz64(wm * WROWS + i * 16 + r16 + hoff, q)]);
 #pragma unroll
             for (int j = 0; j < NF; ++j)
-                fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(k * BN + wn * 64 + j * 16 + r16, q)]);
+                fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(k * BN + wn * WN + j * 16 + r16, q)]);
 #pragma unroll
             for (int i = 0; i < MF; ++i)
 #pragma unroll
@@ -265,8 +274,8 @@ __global__ __launch_bounds__(512, MINB) void conv3_kernel(const ConvArgs a)
     bool pok[MF];
 #pragma unroll
     for (int i = 0; i < MF; ++i) {
-        int yy, xx, s;
-        prow[i] = g.map(p0 + wm * 64 + i * 16 + r16, yy, xx, s);
+        int f, yy, xx, s;
+        prow[i] = g.map(p0 + wm * WROWS + i * 16 + r16, f, yy, xx, s);
         pok[i] = yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
     }
     uint32_t pk[MF][NF][2];
@@ -282,8 +291,18 @@ __global__ __launch_bounds__(512, MINB) void conv3_kernel(const ConvArgs a)
             }
             pk[i][j][0] = (uint32_t)f2h_bits3(v[0]) | ((uint32_t)f2h_bits3(v[1]) << 16);
             pk[i][j][1] = (uint32_t)f2h_bits3(v[2]) | ((uint32_t)f2h_bits3(v[3]) << 16);
+            if (a.out32 && pok[i]) {   // fp32 NCHW net output (the activations before fp16)
+                const int ch = n0 + wn * WN + j * 16 + 4 * q;
+                int f, yy, xx, sx;
+                (void)g.map(p0 + wm * WROWS + i * 16 + r16, f, yy, xx, sx);
+                float* o = a.out32 + (((size_t)f * a.out32_c + a.out32_coff + ch) * a.H + yy - 1) *
+                                         a.W + sx * g.sw + xx - 1;
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                    if (ch + r < a.cout) o[(size_t)r * a.H * a.W] = v[r];
+            }
         }
-    const int chl = n0 + wn * 64 + 4 * q;   // this lane's first channel (fragment j adds 16 j)
+    const int chl = n0 + wn * WN + 4 * q;   // this lane's first channel (fragment j adds 16 j)
     for (int d = 0; d < a.ndst; ++d) {
         const int cs = a.dst_cs[d];
         uint16_t* base = a.dst[d] + a.dst_coff[d] + chl;
@@ -316,20 +335,30 @@ __global__ __launch_bounds__(512, MINB) void conv3_kernel(const ConvArgs a)
 
 }  // namespace
 
-Conv3Shape conv3_shape(int frames, int H, int W, int cout)
+Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
 {
     static const bool small = [] {   // dev A/B switch: OPK_CONV3_SMALL=0 -> one workgroup per CU
         const char* e = std::getenv("OPK_CONV3_SMALL");
         return !(e && e[0] == '0');
     }();
     Conv3Shape s;
-    s.bn = cout <= 64 ? 64 : 128;
+    s.ks = ks;
+    s.bn = cout <= 64 ? 64 : (cout <= 96 ? 96 : 128);
+    if (ks == 1) {   // no halo: small LDS (three tile slots), two workgroups per CU
+        s.bm = 256;
+        s.hr = s.bm;
+        s.tapu = 1;
+        s.minb = 2;
+        s.nstrips = 1;
+        s.sw = W;
+        return s;
+    }
     // two workgroups per CU pay off once every CU gets at least two 256-position tiles (measured:
     // +10-17 % on the 92x164 / 184x328 / 512-channel layers, -20 % at one tile per CU)
-    const long tiles = ((long)frames * (H + 2) * (W + 2) / 256) * ((cout + 127) / 128);
-    if (s.bn == 128 && small && tiles >= 2 * 256) {   // 80 KB of LDS
+    const long tiles = ((long)frames * (H + 2) * (W + 2) / 256) * ((cout + s.bn - 1) / s.bn);
+    if (s.bn != 64 && small && tiles >= 2 * 256) {   // <= 80 KB of LDS
         s.bm = 256; s.hr = 448; s.tapu = 1; s.minb = 2;
-    } else if (s.bn == 128) {
+    } else if (s.bn != 64) {
         s.bm = 256; s.hr = 512; s.tapu = 3; s.minb = 1;
     } else {
         s.bm = 512; s.hr = 768; s.tapu = 3; s.minb = 1;
@@ -342,24 +371,36 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout)
 
 void launch_conv3(const ConvArgs& a, hipStream_t stream)
 {
-    OPK_CHECK_ARG(a.ntaps == 9 && a.cin_pad % 32 == 0 && a.cin_pad > 0, "3x3, cin_pad % 32 == 0");
+    const int ks = a.ntaps == 9 ? 3 : 1;
+    OPK_CHECK_ARG((a.ntaps == 9 || a.ntaps == 1) && a.cin_pad % 32 == 0 && a.cin_pad > 0,
+                  "3x3 or 1x1, cin_pad % 32 == 0");
     OPK_CHECK_ARG(a.in_cs % 8 == 0 && a.in_coff % 8 == 0, "input slice must be 16-byte aligned");
     OPK_CHECK_ARG(a.in_coff + a.cin_pad <= a.in_cs, "input slice exceeds the buffer");
     OPK_CHECK_ARG(a.M > 0 && a.cout > 0 && a.ndst <= kConvMaxDst, "bad sizes");
-    OPK_CHECK_ARG(a.out32 == nullptr, "the halo kernel has no fp32 NCHW output");
-    const Conv3Shape s = conv3_shape(a.frames, a.H, a.W, a.cout);
+    const Conv3Shape s = conv3_shape(a.frames, a.H, a.W, a.cout, ks);
     OPK_CHECK_ARG(a.sw == s.sw && a.nstrips == s.nstrips, "strip geometry differs from conv3_shape");
-    OPK_CHECK_ARG(s.bm + 2 * (s.sw + 2) + 2 <= s.hr, "strip too wide for the halo");
+    OPK_CHECK_ARG(ks == 1 || s.bm + 2 * (s.sw + 2) + 2 <= s.hr, "strip too wide for the halo");
     const long total = (long)a.frames * s.nstrips * (a.H + 2) * (s.sw + 2);
     OPK_CHECK_ARG(total < (1L << 30), "too many positions");
     const int nn = (a.cout + s.bn - 1) / s.bn;
     dim3 grid((unsigned)(((total + s.bm - 1) / s.bm) * nn));
-    if (s.bn == 128 && s.minb == 2)
-        hipLaunchKernelGGL((conv3_kernel<256, 128, 448, 1, 2>), grid, dim3(512), 0, stream, a);
-    else if (s.bn == 128)
-        hipLaunchKernelGGL((conv3_kernel<256, 128, 512, 3, 1>), grid, dim3(512), 0, stream, a);
-    else
-        hipLaunchKernelGGL((conv3_kernel<512, 64, 768, 3, 1>), grid, dim3(512), 0, stream, a);
+#define OPK3_LAUNCH(BM_, BN_, HR_, TAPU_, MINB_, KS_)                                          \
+    hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, MINB_, KS_>), grid, dim3(512), 0,   \
+                       stream, a)
+    if (ks == 1) {
+        if (s.bn == 64) OPK3_LAUNCH(256, 64, 256, 1, 2, 1);
+        else if (s.bn == 96) OPK3_LAUNCH(256, 96, 256, 1, 2, 1);
+        else OPK3_LAUNCH(256, 128, 256, 1, 2, 1);
+    } else if (s.bn == 64) {
+        OPK3_LAUNCH(512, 64, 768, 3, 1, 3);
+    } else if (s.bn == 96) {
+        if (s.minb == 2) OPK3_LAUNCH(256, 96, 448, 1, 2, 3);
+        else OPK3_LAUNCH(256, 96, 512, 3, 1, 3);
+    } else {
+        if (s.minb == 2) OPK3_LAUNCH(256, 128, 448, 1, 2, 3);
+        else OPK3_LAUNCH(256, 128, 512, 3, 1, 3);
+    }
+#undef OPK3_LAUNCH
     OPK_LAUNCH_CHECK();
 }
 

@@ -39,7 +39,7 @@ int main(int argc, char** argv)
     const long head = Wp + 64, tail = kConvGuardTail;
     const long in_elems = (head + pos + tail) * cin_pad;
     const long out_elems = (head + pos + tail) * cout;
-    const long w_elems = (long)((cout + 127) / 128) * 128 * 9 * cin_pad;   // >= any BN packing
+    const long w_elems = (long)((cout + 63) / 64) * 128 * 9 * cin_pad;   // >= any BN packing
 
     std::vector<uint16_t> hin(in_elems);
     srand(1);
@@ -78,7 +78,7 @@ int main(int argc, char** argv)
     a.dst_cs[0] = cout;
     a.dst_coff[0] = 0;
 
-    const Conv3Shape s3 = conv3_shape(frames, H, W, cout);
+    const Conv3Shape s3 = conv3_shape(frames, H, W, cout, 3);
     a.sw = s3.sw;
     a.nstrips = s3.nstrips;
     const long vtot = (long)frames * s3.nstrips * (H + 2) * (s3.sw + 2);
