@@ -356,7 +356,7 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
     // two workgroups per CU pay off once every CU gets at least two 256-position tiles (measured:
     // +10-17 % on the 92x164 / 184x328 / 512-channel layers, -20 % at one tile per CU)
     const long tiles = ((long)frames * (H + 2) * (W + 2) / 256) * ((cout + s.bn - 1) / s.bn);
-    if (s.bn != 64 && small && tiles >= 2 * 256) {   // <= 80 KB of LDS
+    if (small && tiles >= 2 * 256) {   // <= 80 KB of LDS
         s.bm = 256; s.hr = 448; s.tapu = 1; s.minb = 2;
     } else if (s.bn != 64) {
         s.bm = 256; s.hr = 512; s.tapu = 3; s.minb = 1;
@@ -392,7 +392,8 @@ void launch_conv3(const ConvArgs& a, hipStream_t stream)
         else if (s.bn == 96) OPK3_LAUNCH(256, 96, 256, 1, 2, 1);
         else OPK3_LAUNCH(256, 128, 256, 1, 2, 1);
     } else if (s.bn == 64) {
-        OPK3_LAUNCH(512, 64, 768, 3, 1, 3);
+        if (s.minb == 2) OPK3_LAUNCH(256, 64, 448, 1, 2, 3);
+        else OPK3_LAUNCH(512, 64, 768, 3, 1, 3);
     } else if (s.bn == 96) {
         if (s.minb == 2) OPK3_LAUNCH(256, 96, 448, 1, 2, 3);
         else OPK3_LAUNCH(256, 96, 512, 3, 1, 3);
