@@ -37,11 +37,12 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=16, help="frames per step per GPU")
+    ap.add_argument("--batch", type=int, default=64,
+                    help="frames per step per GPU (throughput mode; DESIGN.md §5 lists 16 too)")
     ap.add_argument("--people", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample")
     return ap.parse_args()
 
 
@@ -65,12 +66,25 @@ def cpu_baseline(args, params, frames_np, overlays_np):
         people += len(kp)
         done += 1
         el = time.perf_counter() - t0
-        if el >= args.cpu_seconds or done >= 8:
+        if el >= args.cpu_seconds:
             break
     return {"value": done / el, "unit": "frames/s", "cores": args.cpu_threads, "kind": "port",
             "sample": "%d frame(s) of the full pipeline at 656x368 (CNN fp32 + resize + NMS + "
                       "connector), oracle/ CPU restatement, %.1f s, %d people found"
                       % (done, el, people)}
+
+
+def pmc_traffic(batch):
+    """HBM bytes of one CNN forward from the committed rocprofv3 PMC summary (FETCH_SIZE x2 on
+    gfx950 + WRITE_SIZE over every kernel of one forward; tools/pmc_summary.py), or None when the
+    summary was taken at another batch size."""
+    path = os.path.join(ROOT, "profiles", "round1", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return d.get("cnn_forward_hbm_bytes") if d.get("batch") == batch else None
 
 
 def main():
@@ -177,13 +191,14 @@ def main():
         },
         "roofline": {
             "bound": "mfma",
-            "kernel": "BODY_25 CNN forward (114 implicit-GEMM conv launches + 3 pools + im2col) "
-                      "per step of %d frames" % B,
+            "kernel": "BODY_25 CNN forward (113 halo implicit-GEMM conv launches + fused first "
+                      "conv + 3 pools) per step of %d frames" % B,
             "achieved": round(achieved, 2),
             "peak": PEAK_FP16_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
-            "traffic": None,
+            "traffic": pmc_traffic(B),
+            "traffic_unit": "bytes per launch (HBM, PMC)",
             "algorithmic_gflop_per_launch": round(flops_frame * B / 1e9, 2),
             "avg_launch_ms": round(net_ms, 3),
         },
