@@ -8,6 +8,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libopk_hip.so")
+if os.environ.get("OPK_LIB_PATH"):   # dev A/B of two builds in one process tree
+    LIB_PATH = os.environ["OPK_LIB_PATH"]
 
 _c = ctypes
 _p = _c.c_void_p

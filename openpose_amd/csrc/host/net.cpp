@@ -36,6 +36,10 @@ NetHip::NetHip(Context* ctx, std::vector<LayerDesc> layers, const std::string& o
     const char* v = std::getenv("OPK_CONV_V1");   // A/B switch to the v1 kernel (dev only)
     conv_v1_ = v && v[0] == '1';
     plan(layers);
+    if (ctx_->device >= 0) {
+        ctx_->bind();
+        OPK_HIP(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, ctx_->device));
+    }
 }
 
 void NetHip::plan(const std::vector<LayerDesc>& layers)
@@ -190,6 +194,29 @@ void NetHip::plan(const std::vector<LayerDesc>& layers)
         c.cout_pad = round_up(c.info.cout, c.bn);
         info_.push_back(c.info);
     }
+    // conv1_1 -> conv1_2 -> pool1 fusion (conv1_fused.hip): the first conv feeds only the second,
+    // whose output feeds only a pool, and nothing else reads either buffer
+    if (steps_.size() >= 3 && steps_[0].conv && steps_[1].conv && !steps_[2].conv) {
+        const ConvPlan& a = convs_[steps_[0].idx];
+        const ConvPlan& b = convs_[steps_[1].idx];
+        const PoolPlan& p = pools_[steps_[2].idx];
+        const int abuf = a.outs.size() == 1 ? a.outs[0].buf : -1;
+        const int bbuf = b.outs.size() == 1 ? b.outs[0].buf : -1;
+        int readers_a = 0, readers_b = 0;
+        for (const auto& c : convs_) {
+            readers_a += c.in.buf == abuf;
+            readers_b += c.in.buf == bbuf;
+        }
+        for (const auto& q : pools_) {
+            readers_a += q.in_buf == abuf;
+            readers_b += q.in_buf == bbuf;
+        }
+        if (a.from_image && a.info.k == 3 && a.info.cout == 64 && b.info.k == 3 &&
+            b.info.cin == 64 && b.info.cout == 64 && abuf >= 0 && bbuf >= 0 && abuf != bbuf &&
+            b.in.buf == abuf && p.in_buf == bbuf && readers_a == 1 && readers_b == 1 &&
+            a.out32_coff < 0 && b.out32_coff < 0)
+            fuse1_ = {steps_[0].idx, steps_[1].idx, steps_[2].idx, abuf, bbuf};
+    }
 }
 
 void NetHip::set_conv(const std::string& name, const float* w, const float* b, const float* slope)
@@ -288,9 +315,16 @@ void NetHip::reshape(int n, int h, int w)
     mem_.clear();
     std::vector<uint16_t*>& ptr = base_;
     ptr.assign(bufs_.size(), nullptr);
+    {
+        const char* e = std::getenv("OPK_CONV1_FUSED");   // dev A/B switch: 0 disables the fusion
+        fused1_active_ = fuse1_.a >= 0 && !conv_v1_ && !(e && e[0] == '0') &&
+                         conv1_fused_supported(h, w, 64, 64);
+    }
     for (size_t i = 0; i < bufs_.size(); ++i) {
         mem_.push_back(std::make_unique<DevBuf>());
         if ((int)i == image_buf_ && !conv_v1_) continue;   // conv_image reads the NCHW input itself
+        if (fused1_active_ && ((int)i == fuse1_.abuf || (int)i == fuse1_.bbuf))
+            continue;   // conv1_1 / conv1_2 outputs live only inside conv1_fused_kernel
         // zeroed guards: the kernels read up to W+3 positions before the first frame and up to
         // kConvGuardTail positions after the last one (conv.h)
         const int L = bufs_[i].level;
@@ -361,7 +395,34 @@ void NetHip::forward(const float* input, int n, int h, int w)
     if (n != n_ || h != h_ || w != w_) reshape(n, h, w);
     const std::vector<uint16_t*>& ptr = base_;
     if (conv_v1_) launch_im2col3(ptr[image_buf_], input, n, h, w, ctx_->stream);
-    for (const auto& s : steps_) {
+    size_t first = 0;
+    if (fused1_active_) {
+        const ConvPlan& a = convs_[fuse1_.a];
+        const ConvPlan& b = convs_[fuse1_.b];
+        const PoolPlan& p = pools_[fuse1_.p];
+        Conv1FusedArgs fa{};
+        fa.img = input;
+        fa.frames = n;
+        fa.H = h;
+        fa.W = w;
+        fa.w1 = static_cast<const uint16_t*>(a.w.ptr);
+        fa.b1 = static_cast<const float*>(a.bias.ptr);
+        fa.s1 = static_cast<const float*>(a.slope.ptr);
+        fa.act1 = a.info.act;
+        fa.w2 = static_cast<const uint16_t*>(b.w3.ptr);
+        fa.b2 = static_cast<const float*>(b.bias.ptr);
+        fa.s2 = static_cast<const float*>(b.slope.ptr);
+        fa.act2 = b.info.act;
+        fa.out = ptr[p.out_buf];
+        fa.out_cs = bufs_[p.out_buf].cs;
+        fa.out_coff = 0;
+        fa.OH = lh_[1];
+        fa.OW = lw_[1];
+        launch_conv1_fused(fa, cus_, ctx_->stream);
+        first = 3;
+    }
+    for (size_t si = first; si < steps_.size(); ++si) {
+        const Step& s = steps_[si];
         if (s.conv) {
             const ConvPlan& c = convs_[s.idx];
             if (conv_v1_) launch_conv(c.args, c.bn > 128 ? 128 : c.bn, ctx_->stream);

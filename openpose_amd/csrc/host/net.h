@@ -67,6 +67,10 @@ private:
     int out_level_ = 0, out_c_ = 0, nlevels_ = 1;
     int image_buf_ = -1;
     bool conv_v1_ = false;
+    struct Fuse1 { int a = -1, b = -1, p = -1, abuf = -1, bbuf = -1; };
+    Fuse1 fuse1_;                 // conv1_1 -> conv1_2 -> pool1 (conv1_fused.hip) when planned
+    bool fused1_active_ = false;  // ... and the input shape allows it
+    int cus_ = 256;               // compute units (persistent-kernel grid)
 
     // shape-dependent state
     int n_ = 0, h_ = 0, w_ = 0;

@@ -36,6 +36,7 @@ struct ConvArgs {
     float* out32;         // optional NCHW fp32 [frames][out32_c][H][W]
     int out32_c, out32_coff;
     int sw, nstrips;      // conv3 only: strip width and count (conv3_shape)
+    float rcp[3];         // conv3 only, set by launch_conv3: 1/((H+2)(sw+2)), 1/(sw+2), 1/nstrips
 };
 
 // v1 (conv.hip): 256 lanes, 128 x bn tile, register-staged; bn: 32, 64, 96 or 128
@@ -64,6 +65,25 @@ void launch_im2col3(uint16_t* out, const float* in, int frames, int H, int W, hi
 // First conv (3 input channels, 3x3, cout <= 64) straight from the fp32 NCHW input [frames][3][H][W]
 // (conv_image.hip); weights as packed for v1/v2 ([cout_pad][64], K order (ky*3 + kx)*3 + ci).
 void launch_conv_image(const ConvArgs& a, const float* image, hipStream_t stream);
+
+// conv1_1 (3 -> 64) + act -> conv1_2 (64 -> 64) + act -> 2x2/2 max pool in one persistent kernel
+// (conv1_fused.hip).  img: fp32 NCHW [frames][3][H][W]; w1: [64][64] (K order (ky*3+kx)*3+ci);
+// w2: conv3 packing for BN = 64; bias/slope arrays zero-padded to 128; out: the pooled padded NHWC
+// fp16 image [frames][OH+2][OW+2][out_cs] (slice at out_coff).  H and W even.
+struct Conv1FusedArgs {
+    const float* img;
+    int frames, H, W;
+    const uint16_t* w1;
+    const float *b1, *s1;
+    int act1;
+    const uint16_t* w2;
+    const float *b2, *s2;
+    int act2;
+    uint16_t* out;
+    int out_cs, out_coff, OH, OW;
+};
+bool conv1_fused_supported(int H, int W, int cout1, int cout2);
+void launch_conv1_fused(const Conv1FusedArgs& a, int workgroups, hipStream_t stream);
 
 // 2x2 stride-2 max pool with Caffe ceil sizing, padded NHWC fp16 -> padded NHWC fp16.
 void launch_maxpool2(uint16_t* out, const uint16_t* in, int frames, int H, int W, int C, int OH,

@@ -1,0 +1,282 @@
+// conv1_fused.hip -- conv1_1 -> ReLU -> conv1_2 -> ReLU -> pool1 of the VGG front end in ONE kernel.
+//
+// Reference layers (models/pose/body_25/pose_deploy.prototxt, run by NetCaffe::forwardPass,
+// netCaffe.cpp:248): conv1_1 (3 -> 64, 3x3) + relu1_1, conv1_2 (64 -> 64, 3x3) + relu1_2,
+// pool1_stage1 (2x2/2 max).  At 368x656 these are the only full-resolution layers; unfused they
+// write and re-read two 64-channel fp16 images (2 x 31 MB per frame) and are bound by that
+// traffic (profiles/round1: conv_image + conv1_2 + pool1 = 3.4 ms per 64 frames).
+//
+// Here a persistent workgroup per CU keeps conv1_2's weights (72 KB) resident in LDS and walks
+// tiles of TR x TC output pixels.  Per tile:
+//   1. the fp32 NCHW image patch (TR+4) x (TC+4) x 3 is staged in LDS (prefetched in registers
+//      during the previous tile's conv1_2);
+//   2. conv1_1 is evaluated for the (TR+2) x (TC+2) halo conv1_2 needs, as MFMAs with K = 27
+//      gathered from the patch; bias + activation, fp16, zero outside the image, written to LDS
+//      in the swizzled 64-byte-row layout conv3.hip uses for its A operand;
+//   3. conv1_2 is an implicit GEMM over the halo's "virtual image" of row width VW = 64
+//      (TR x 64 rows, columns >= TC discarded): 2 channel chunks x 9 taps, no barrier inside;
+//   4. bias + activation, fp16 tile to LDS, 2x2 max, one 16-byte store per 8 pooled channels.
+// Only the image is read and only pool1's output is written.
+#include "conv.h"
+
+#include <algorithm>
+
+#include "../common.h"
+
+namespace opk {
+
+namespace {
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef float float2_t __attribute__((ext_vector_type(2)));
+
+constexpr int TR = 6, TC = 62, VW = 64;       // tile rows / columns; virtual row width
+constexpr int MT = TR * VW;                   // GEMM rows per tile (384)
+constexpr int HROWS = (TR + 2) * VW + 8;      // halo rows (+ overflow of the last taps)
+constexpr int PR = TR + 4, PC = TC + 4;       // image patch
+constexpr int PATCH = 3 * PR * PC;            // floats
+constexpr int NT = 512;                       // lanes per workgroup (8 waves)
+constexpr int PPL = (PATCH + NT - 1) / NT;    // patch floats per lane
+constexpr int TSTRIDE = 72;                   // epilogue tile row stride in halves (16-B rows)
+constexpr int W2_PIECES = 18 * 64 * 4;        // 2 chunks x 9 taps x 64 rows x 4 x 16 B
+constexpr int HALO_PIECES = 2 * HROWS * 4;
+constexpr int LDS_BYTES = (W2_PIECES + HALO_PIECES) * 16 + (PATCH * 4 + 15) / 16 * 16;
+static_assert(MT * TSTRIDE * 2 <= HALO_PIECES * 16, "epilogue tile fits in the halo");
+static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
+
+__device__ __forceinline__ int swz64(int row, int piece) { return row * 4 + (piece ^ (((row >> 2) & 1) << 1)); }
+
+__device__ __forceinline__ uint32_t hmax2(uint32_t a, uint32_t b)
+{
+    const half2_t x = __builtin_bit_cast(half2_t, a), y = __builtin_bit_cast(half2_t, b);
+    half2_t r;
+    r[0] = (float)y[0] > (float)x[0] ? y[0] : x[0];   // maxpool2_kernel's comparison
+    r[1] = (float)y[1] > (float)x[1] ? y[1] : x[1];
+    return __builtin_bit_cast(uint32_t, r);
+}
+
+__global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs a)
+{
+    __shared__ uint4 lds[LDS_BYTES / 16];
+    uint4* W2 = lds;
+    uint4* HALO = lds + W2_PIECES;
+    float* patch = reinterpret_cast<float*>(lds + W2_PIECES + HALO_PIECES);
+    uint16_t* T = reinterpret_cast<uint16_t*>(HALO);
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, q = lane >> 4;
+    const int H = a.H, W = a.W;
+    const int tiles_x = (W + TC - 1) / TC, tiles_y = (H + TR - 1) / TR;
+    const int ntiles = a.frames * tiles_x * tiles_y;
+
+    // ---- resident conv1_2 weights: conv3 packing [c][ky][kx][64 n][32 ci], swizzled rows ------
+    {
+        const int lrow = lane >> 2, phys = lane & 3;
+#pragma unroll
+        for (int k = 0; k < W2_PIECES / NT; ++k) {
+            const int inst = k * 8 + wave;            // 1 KiB = 16 rows of one unit
+            const int row = inst * 16 + lrow;         // global row over all 18 units
+            const int lp = phys ^ (((row >> 2) & 1) << 1);
+            __builtin_amdgcn_global_load_lds((const void*)(a.w2 + (size_t)row * 32 + lp * 8),
+                                             (__attribute__((address_space(3))) void*)(&W2[inst * 64]),
+                                             16, 0, 0);
+        }
+    }
+    // conv1_1 weights as MFMA A operand (rows = output channels g*16 + r16, K = 8q .. 8q+7)
+    half8_t w1f[4];
+    float4_t b1[4], m1[4], b2[4], m2[4];
+    const float neg1 = a.act1 == 1 ? 0.f : 1.f, neg2 = a.act2 == 1 ? 0.f : 1.f;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+        w1f[g] = *reinterpret_cast<const half8_t*>(a.w1 + (size_t)(g * 16 + r16) * 64 + 8 * q);
+        const int ch = g * 16 + 4 * q;   // bias/slope arrays are zero-padded to 128 channels
+        b1[g] = *reinterpret_cast<const float4_t*>(a.b1 + ch);
+        const float4_t s1 = *reinterpret_cast<const float4_t*>(a.s1 + ch);
+        m1[g] = a.act1 == 2 ? s1 : float4_t{neg1, neg1, neg1, neg1};
+        b2[g] = *reinterpret_cast<const float4_t*>(a.b2 + ch);
+        const float4_t s2 = *reinterpret_cast<const float4_t*>(a.s2 + ch);
+        m2[g] = a.act2 == 2 ? s2 : float4_t{neg2, neg2, neg2, neg2};
+    }
+    // this lane's 8 conv1_1 K values: patch offset of (ci, ky, kx) for k = 8q + e, -1 past 26
+    int off[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+        const int k = 8 * q + e;
+        const int t = k / 3, ci = k - 3 * (k / 3);
+        off[e] = k < 27 ? (ci * PR + t / 3) * PC + (t - 3 * (t / 3)) : -1;
+    }
+
+#define OPK1_ORIGIN(tile_, f_, y0_, x0_)                                                       \
+    do {                                                                                      \
+        const int tx_ = (tile_) % tiles_x;                                                    \
+        const int rest_ = (tile_) / tiles_x;                                                  \
+        y0_ = (rest_ % tiles_y) * TR;                                                         \
+        f_ = rest_ / tiles_y;                                                                 \
+        x0_ = tx_ * TC;                                                                       \
+    } while (0)
+    // image patch of a tile: rows y0-2 .. y0+TR+1, columns x0-2 .. x0+TC+1, zero outside
+    float pre[PPL];
+#define OPK1_LOAD_PATCH(tile_)                                                                \
+    do {                                                                                      \
+        int f_, y0_, x0_;                                                                     \
+        OPK1_ORIGIN(tile_, f_, y0_, x0_);                                                     \
+        const float* src_ = a.img + (size_t)f_ * 3 * H * W;                                   \
+        _Pragma("unroll") for (int k_ = 0; k_ < PPL; ++k_) {                                  \
+            const int i_ = tid + k_ * NT;                                                     \
+            float v_ = 0.f;                                                                   \
+            if (i_ < PATCH && (tile_) < ntiles) {                                             \
+                const int ci_ = i_ / (PR * PC);                                               \
+                const int rem_ = i_ - ci_ * (PR * PC);                                        \
+                const int r_ = rem_ / PC, c_ = rem_ - (rem_ / PC) * PC;                       \
+                const int y_ = y0_ - 2 + r_, x_ = x0_ - 2 + c_;                               \
+                if (y_ >= 0 && y_ < H && x_ >= 0 && x_ < W)                                   \
+                    v_ = src_[((size_t)ci_ * H + y_) * W + x_];                               \
+            }                                                                                 \
+            pre[k_] = v_;                                                                     \
+        }                                                                                     \
+    } while (0)
+
+    int tile = blockIdx.x;
+    OPK1_LOAD_PATCH(tile);
+    for (; tile < ntiles; tile += gridDim.x) {
+        int f, y0, x0;
+        OPK1_ORIGIN(tile, f, y0, x0);
+        __syncthreads();   // previous tile's pooling reads of T (aliasing the halo) are done
+#pragma unroll
+        for (int k = 0; k < PPL; ++k)
+            if (tid + k * NT < PATCH) patch[tid + k * NT] = pre[k];
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // resident weights (first tile)
+        __syncthreads();
+
+        // ---- conv1_1 over the (TR+2) x 64 halo: 32 groups of 16 positions, 4 per wave ------
+#pragma unroll
+        for (int gi = 0; gi < 4; ++gi) {
+            const int mh = (wave * 4 + gi) * 16 + r16;       // halo position
+            const int hr = mh >> 6, hc = mh & 63;
+            half8_t xf;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                xf[e] = off[e] >= 0 ? (_Float16)patch[off[e] + hr * PC + hc] : (_Float16)0.f;
+            const int y = y0 - 1 + hr, x = x0 - 1 + hc;
+            const bool in = y >= 0 && y < H && x >= 0 && x < W;
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float4_t c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1f[g], xf, float4_t{0.f, 0.f, 0.f, 0.f},
+                                                                     0, 0, 0);
+                const float4_t t = c1 + b1[g];
+                const float4_t tm = t * m1[g];
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = in ? (t[r] > 0.f ? t[r] : tm[r]) : 0.f;
+                uint2 pk;
+                pk.x = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+                pk.y = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                // channels g*16 + 4q .. +3: chunk g/2, 16-byte piece (g&1)*2 + q/2, half q&1
+                char* dst = reinterpret_cast<char*>(HALO + (g >> 1) * HROWS * 4 +
+                                                    swz64(mh, (g & 1) * 2 + (q >> 1))) + (q & 1) * 8;
+                *reinterpret_cast<uint2*>(dst) = pk;
+            }
+        }
+        __syncthreads();
+
+        // ---- prefetch the next tile's patch; conv1_2 from LDS only -----------------------------
+        OPK1_LOAD_PATCH(tile + gridDim.x);
+        float4_t acc[3][4];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+            const uint4* As = HALO + c * HROWS * 4;
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+                const uint4* Bs = W2 + (c * 9 + tap) * 256;
+                half8_t fa[3], fb[4];
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+                    fa[i] = __builtin_bit_cast(half8_t, As[swz64(wave * 48 + i * 16 + r16 + ky * VW + kx, q)]);
+#pragma unroll
+                for (int j = 0; j < 4; ++j)
+                    fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(j * 16 + r16, q)]);
+#pragma unroll
+                for (int i = 0; i < 3; ++i)
+#pragma unroll
+                    for (int j = 0; j < 4; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+            }
+        }
+        __syncthreads();   // every wave is done reading the halo: T may overwrite it
+
+        // ---- bias + activation -> fp16 tile [m][64 ch] -----------------------------------------
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int m = wave * 48 + i * 16 + r16;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float4_t t = acc[i][j] + b2[j];
+                const float4_t tm = t * m2[j];
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
+                uint2 pk;
+                pk.x = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+                pk.y = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                *reinterpret_cast<uint2*>(T + m * TSTRIDE + j * 16 + 4 * q) = pk;
+            }
+        }
+        __syncthreads();
+
+        // ---- 2x2 max pool: (TR/2) x (TC/2) pooled pixels x 8 channel groups ---------------------
+        for (int task = tid; task < (TR / 2) * (TC / 2) * 8; task += NT) {
+            const int cg = task & 7;
+            const int pp = task >> 3;
+            const int pr = pp / (TC / 2), pc = pp - (pp / (TC / 2)) * (TC / 2);
+            const int oy = y0 / 2 + pr, ox = x0 / 2 + pc;
+            if (2 * oy + 1 >= H || 2 * ox + 1 >= W) continue;
+            const int m0 = (2 * pr) * VW + 2 * pc;
+            const uint16_t* s0 = T + m0 * TSTRIDE + cg * 8;
+            uint4 v0 = *reinterpret_cast<const uint4*>(s0);
+            const uint4 v1 = *reinterpret_cast<const uint4*>(s0 + TSTRIDE);
+            const uint4 v2 = *reinterpret_cast<const uint4*>(s0 + VW * TSTRIDE);
+            const uint4 v3 = *reinterpret_cast<const uint4*>(s0 + (VW + 1) * TSTRIDE);
+            // Caffe window order (y, x), (y, x+1), (y+1, x), (y+1, x+1)
+            v0.x = hmax2(hmax2(hmax2(v0.x, v1.x), v2.x), v3.x);
+            v0.y = hmax2(hmax2(hmax2(v0.y, v1.y), v2.y), v3.y);
+            v0.z = hmax2(hmax2(hmax2(v0.z, v1.z), v2.z), v3.z);
+            v0.w = hmax2(hmax2(hmax2(v0.w, v1.w), v2.w), v3.w);
+            uint16_t* dst = a.out + (((size_t)f * (a.OH + 2) + oy + 1) * (a.OW + 2) + ox + 1) * a.out_cs +
+                            a.out_coff + cg * 8;
+            *reinterpret_cast<uint4*>(dst) = v0;
+        }
+    }
+#undef OPK1_LOAD_PATCH
+#undef OPK1_ORIGIN
+}
+
+}  // namespace
+
+bool conv1_fused_supported(int H, int W, int cout1, int cout2)
+{
+    return cout1 == 64 && cout2 == 64 && H % 2 == 0 && W % 2 == 0 && H >= 2 && W >= 2;
+}
+
+void launch_conv1_fused(const Conv1FusedArgs& a, int workgroups, hipStream_t stream)
+{
+    OPK_CHECK_ARG(a.img && a.w1 && a.w2 && a.out && a.b1 && a.b2 && a.s1 && a.s2, "NULL argument");
+    OPK_CHECK_ARG(a.frames > 0 && conv1_fused_supported(a.H, a.W, 64, 64), "conv1 fusion: sizes");
+    OPK_CHECK_ARG(a.OH == a.H / 2 && a.OW == a.W / 2, "conv1 fusion: pooled size");
+    OPK_CHECK_ARG(a.out_cs % 8 == 0 && a.out_coff % 8 == 0 && a.out_coff + 64 <= a.out_cs,
+                  "conv1 fusion: 16-byte aligned output slice");
+    const long tiles = (long)a.frames * ((a.W + TC - 1) / TC) * ((a.H + TR - 1) / TR);
+    OPK_CHECK_ARG(tiles < (1L << 31), "conv1 fusion: too many tiles");
+    const int grid = (int)std::min<long>(tiles, workgroups > 0 ? workgroups : 256);
+    hipLaunchKernelGGL(conv1_fused_kernel, dim3(grid), dim3(NT), 0, stream, a);
+    OPK_LAUNCH_CHECK();
+}
+
+}  // namespace opk

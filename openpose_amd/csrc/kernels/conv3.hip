@@ -38,6 +38,8 @@ namespace {
 
 typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef float float2_t __attribute__((ext_vector_type(2)));
+typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ int swz64(int row, int piece) { return row * 4 + (piece ^ (((row >> 2) & 1) << 1)); }
 
@@ -91,15 +93,29 @@ __device__ __forceinline__ void vm_wait_rt(int n)
     }
 }
 
+// n / d for 0 <= n < 2^24, 0 < d (float reciprocal estimate, then one correction step): a few VALU
+// instead of the ~40-instruction integer division sequence
+__device__ __forceinline__ int fdiv(int n, int d, float rd)
+{
+    int q = (int)((float)n * rd);
+    const int r = n - q * d;
+    q += (r >= d) ? 1 : 0;
+    q -= (r < 0) ? 1 : 0;
+    return q;
+}
+
 // virtual-image geometry (see the header comment)
 struct Strips {
     int H, Wp, sw, VW, nstrips, fposV, total;
+    float rf, rv, rs;   // reciprocals of fposV, VW, nstrips
     __device__ Strips(const ConvArgs& a)
         : H(a.H), Wp(a.W + 2), sw(a.sw), VW(a.sw + 2), nstrips(a.nstrips),
-          fposV((a.H + 2) * (a.sw + 2)), total(a.frames * a.nstrips * (a.H + 2) * (a.sw + 2))
+          fposV((a.H + 2) * (a.sw + 2)), total(a.frames * a.nstrips * (a.H + 2) * (a.sw + 2)),
+          rf(a.rcp[0]), rv(a.rcp[1]), rs(a.rcp[2])
     {
     }
     // padded-image position of virtual position v (any v; outside the image -> -1, a zeroed guard)
+    template <bool FAST = true>
     __device__ long map(int v, int& f, int& yy, int& xx, int& s) const
     {
         if (v < 0 || v >= total) {
@@ -109,11 +125,11 @@ struct Strips {
             s = 0;
             return -1;
         }
-        const int vf = v / fposV;
+        const int vf = FAST ? fdiv(v, fposV, rf) : v / fposV;
         const int rem = v - vf * fposV;
-        yy = rem / VW;
+        yy = FAST ? fdiv(rem, VW, rv) : rem / VW;
         xx = rem - yy * VW;
-        f = vf / nstrips;
+        f = FAST ? fdiv(vf, nstrips, rs) : vf / nstrips;
         s = vf - f * nstrips;
         return (long)(f * (H + 2) + yy) * Wp + s * sw + xx;
     }
@@ -175,7 +191,7 @@ void conv3_kernel(const ConvArgs a)
         const int lp = phys ^ (((hr >> 2) & 1) << 1);
         int yy, xx, s;
         int f;
-        const long pos = g.map(p0 - (KS == 3 ? g.VW + 1 : 0) + hr, f, yy, xx, s);
+        const long pos = g.template map<false>(p0 - (KS == 3 ? g.VW + 1 : 0) + hr, f, yy, xx, s);
         arow[i] = a.in + a.in_coff + pos * a.in_cs + lp * 8;
     }
     // this wave issues halo instructions i*8 + wave < API and B instructions j*8 + wave < BPI
@@ -264,7 +280,7 @@ void conv3_kernel(const ConvArgs a)
     }
 #undef OPK3_ISSUE
     OPK3_STAMP(2);
-    if constexpr (MINB != 1) OPK3_BIAS();
+    if constexpr (MINB != 1) OPK3_BIAS();   // two workgroups per CU: not kept across the K loop
 #undef OPK3_BIAS
 
     // ---- epilogue straight from registers ------------------------------------------------------
@@ -272,61 +288,73 @@ void conv3_kernel(const ConvArgs a)
     // of virtual position p0 + wm*64 + i*16 + r16; border and out-of-image positions are dropped.
     long prow[MF];
     bool pok[MF];
-#pragma unroll
-    for (int i = 0; i < MF; ++i) {
+    int pbase = p0 + wm * WROWS + r16;
+    asm volatile("" : "+v"(pbase));   // keep the position math after the K loop (register pressure)
+    {   // fragment i is 16 virtual positions after fragment i-1: step the coordinates
         int f, yy, xx, s;
-        prow[i] = g.map(p0 + wm * WROWS + i * 16 + r16, f, yy, xx, s);
-        pok[i] = yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
+        prow[0] = g.map(pbase, f, yy, xx, s);
+        pok[0] = yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
+#pragma unroll
+        for (int i = 1; i < MF; ++i) {
+            if (g.VW > 16) {
+                xx += 16;
+                if (xx >= g.VW) {
+                    xx -= g.VW;
+                    if (++yy == a.H + 2) {
+                        yy = 0;
+                        if (++s == g.nstrips) {
+                            s = 0;
+                            ++f;
+                        }
+                    }
+                }
+                const bool in = pbase + i * 16 < g.total;
+                prow[i] = in ? (long)(f * (a.H + 2) + yy) * g.Wp + s * g.sw + xx : -1;
+                pok[i] = in && yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
+            } else {
+                int f2, yy2, xx2, s2;
+                prow[i] = g.map(pbase + i * 16, f2, yy2, xx2, s2);
+                pok[i] = yy2 >= 1 && yy2 <= a.H && xx2 >= 1 && xx2 <= g.sw && s2 * g.sw + xx2 <= a.W;
+            }
+        }
     }
-    uint32_t pk[MF][NF][2];
+    const int chl = n0 + wn * WN + 4 * q;   // this lane's first channel (fragment j adds 16 j)
+    const bool vec = (a.cout & 3) == 0;
+    // fragment column j outer, row i inner: each (i, j) is activated, packed and stored at once
 #pragma unroll
-    for (int i = 0; i < MF; ++i)
+    for (int j = 0; j < NF; ++j) {
+        const float4_t bj = bv[j], mj = mv[j];
+        const int ch = chl + j * 16;
 #pragma unroll
-        for (int j = 0; j < NF; ++j) {
+        for (int i = 0; i < MF; ++i) {
+            // packed f32 math (v_pk_add/v_pk_mul) and v_cvt_pk_f16_f32 (round to nearest even)
+            const float4_t t = acc[i][j] + bj;
+            const float4_t tm = t * mj;
             float v[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const float t = acc[i][j][r] + bv[j][r];
-                v[r] = t > 0.f ? t : t * mv[j][r];
+            for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
+            if (!pok[i] || ch >= a.cout) continue;
+            const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+            const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+            for (int d = 0; d < a.ndst; ++d) {
+                const int cs = a.dst_cs[d];
+                uint16_t* p = a.dst[d] + a.dst_coff[d] + ch + prow[i] * cs;
+                if (vec && ((a.dst_coff[d] | cs) & 3) == 0) {
+                    *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+                } else {
+#pragma unroll
+                    for (int e = 0; e < 4; ++e)
+                        if (ch + e < a.cout) p[e] = (uint16_t)((e < 2 ? lo : hi) >> (16 * (e & 1)));
+                }
             }
-            pk[i][j][0] = (uint32_t)f2h_bits3(v[0]) | ((uint32_t)f2h_bits3(v[1]) << 16);
-            pk[i][j][1] = (uint32_t)f2h_bits3(v[2]) | ((uint32_t)f2h_bits3(v[3]) << 16);
-            if (a.out32 && pok[i]) {   // fp32 NCHW net output (the activations before fp16)
-                const int ch = n0 + wn * WN + j * 16 + 4 * q;
+            if (a.out32) {   // fp32 NCHW net output (the activations before fp16)
                 int f, yy, xx, sx;
-                (void)g.map(p0 + wm * WROWS + i * 16 + r16, f, yy, xx, sx);
+                (void)g.map(pbase + i * 16, f, yy, xx, sx);
                 float* o = a.out32 + (((size_t)f * a.out32_c + a.out32_coff + ch) * a.H + yy - 1) *
                                          a.W + sx * g.sw + xx - 1;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     if (ch + r < a.cout) o[(size_t)r * a.H * a.W] = v[r];
-            }
-        }
-    const int chl = n0 + wn * WN + 4 * q;   // this lane's first channel (fragment j adds 16 j)
-    for (int d = 0; d < a.ndst; ++d) {
-        const int cs = a.dst_cs[d];
-        uint16_t* base = a.dst[d] + a.dst_coff[d] + chl;
-        if (((a.dst_coff[d] | cs | a.cout) & 3) == 0) {
-#pragma unroll
-            for (int i = 0; i < MF; ++i) {
-                if (!pok[i]) continue;
-                uint16_t* p = base + prow[i] * cs;
-#pragma unroll
-                for (int j = 0; j < NF; ++j)
-                    if (chl + j * 16 < a.cout)
-                        *reinterpret_cast<uint2*>(p + j * 16) = make_uint2(pk[i][j][0], pk[i][j][1]);
-            }
-        } else {
-#pragma unroll
-            for (int i = 0; i < MF; ++i) {
-                if (!pok[i]) continue;
-                uint16_t* p = base + prow[i] * cs;
-#pragma unroll
-                for (int j = 0; j < NF; ++j)
-#pragma unroll
-                    for (int e = 0; e < 4; ++e)
-                        if (chl + j * 16 + e < a.cout)
-                            p[j * 16 + e] = (uint16_t)(pk[i][j][e >> 1] >> (16 * (e & 1)));
             }
         }
     }
@@ -369,8 +397,12 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
     return s;
 }
 
-void launch_conv3(const ConvArgs& a, hipStream_t stream)
+void launch_conv3(const ConvArgs& args, hipStream_t stream)
 {
+    ConvArgs a = args;   // + the reciprocals of the strip geometry (Strips::map, kernel arguments)
+    a.rcp[0] = (float)(1.0 / ((double)(a.H + 2) * (a.sw + 2)));
+    a.rcp[1] = (float)(1.0 / (double)(a.sw + 2));
+    a.rcp[2] = (float)(1.0 / (double)(a.nstrips > 0 ? a.nstrips : 1));
     const int ks = a.ntaps == 9 ? 3 : 1;
     OPK_CHECK_ARG((a.ntaps == 9 || a.ntaps == 1) && a.cin_pad % 32 == 0 && a.cin_pad > 0,
                   "3x3 or 1x1, cin_pad % 32 == 0");
@@ -381,7 +413,7 @@ void launch_conv3(const ConvArgs& a, hipStream_t stream)
     OPK_CHECK_ARG(a.sw == s.sw && a.nstrips == s.nstrips, "strip geometry differs from conv3_shape");
     OPK_CHECK_ARG(ks == 1 || s.bm + 2 * (s.sw + 2) + 2 <= s.hr, "strip too wide for the halo");
     const long total = (long)a.frames * s.nstrips * (a.H + 2) * (s.sw + 2);
-    OPK_CHECK_ARG(total < (1L << 30), "too many positions");
+    OPK_CHECK_ARG(total + s.bm + 2L * (s.sw + 2) < (1L << 24), "too many positions per launch");
     const int nn = (a.cout + s.bn - 1) / s.bn;
     dim3 grid((unsigned)(((total + s.bm - 1) / s.bm) * nn));
 #define OPK3_LAUNCH(BM_, BN_, HR_, TAPU_, MINB_, KS_)                                          \

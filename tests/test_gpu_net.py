@@ -95,3 +95,26 @@ def test_body25_vs_oracle(ctx, n, h, w):
     err = rel_l2(got, ref)
     print("BODY_25 %dx%dx%d rel-L2 %.3e" % (n, h, w, err))
     assert err < BODY25_TOL
+
+
+@pytest.mark.parametrize("hw,acts", [((24, 40), ("relu", "relu")), ((26, 130), ("relu", "prelu")),
+                                     ((14, 6), ("prelu", "relu"))])
+def test_conv1_fused_matches_unfused(ctx, hw, acts):
+    """conv1_1 -> conv1_2 -> pool1 in one kernel (conv1_fused.hip) gives the bits of the three
+    separate kernels (same MFMA operands and accumulation order, same epilogue, same max)."""
+    L = conv("c1", "image", 64, 3, acts[0]) + conv("c2", "c1", 64, 3, acts[1])
+    L.append(dict(name="pool1", type="Pooling", bottom=["c2"], top=["pool1"], pool="MAX",
+                  kernel_size=2, stride=2))
+    L += conv("c3", "pool1", 32, 3, "relu") + conv("c4", "c3", 16, 1)
+    L.append(dict(name="net_output", type="Concat", bottom=["c4"], top=["net_output"]))
+    x = np.random.default_rng(7).uniform(-0.5, 0.5, (3, 3) + hw).astype(np.float32)
+    outs = []
+    for fused in ("1", "0"):
+        os.environ["OPK_CONV1_FUSED"] = fused
+        try:
+            got, ref = run_graph(ctx, L, x, seed=3)
+        finally:
+            os.environ.pop("OPK_CONV1_FUSED", None)
+        assert rel_l2(got, ref) < SMALL_TOL
+        outs.append(got)
+    np.testing.assert_array_equal(outs[0], outs[1])
