@@ -52,6 +52,7 @@ constexpr int kConvGuardTail = 1024;   // positions
 struct Conv3Shape {
     int ks;                       // 3 or 1
     int bm, bn, hr, tapu, minb;   // tile, halo rows, taps per K unit, workgroups per CU
+    int nw;                       // waves per workgroup
     int sw, nstrips;
 };
 Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks);

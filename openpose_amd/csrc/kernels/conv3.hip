@@ -49,6 +49,10 @@ __device__ __forceinline__ uint16_t f2h_bits3(float v)
     return __builtin_bit_cast(uint16_t, h);
 }
 
+#ifndef OPK3_ABLATE
+#define OPK3_ABLATE 0
+#endif
+
 #ifdef OPK3_STAMPS   // dev probe (tools/conv3_probe.hip): per-block phase timestamps
 __device__ unsigned long long* opk3_stamps;
 #define OPK3_STAMP(k_)                                                                        \
@@ -139,11 +143,12 @@ struct Strips {
 // LDS budget allows (2 -> 80 KB: the other workgroup's MFMAs cover this one's prologue, barrier
 // and epilogue stalls).
 // KS: 3 (3x3, pad 1) or 1 (1x1: the "halo" is the tile itself, one tap per chunk).
-template <int BM, int BN, int HR, int TAPU, int MINB, int KS>
-__global__ __launch_bounds__(512, MINB) __attribute__((amdgpu_waves_per_eu(2 * MINB)))
+// NW: waves per workgroup (8, or 16 for the 512-row tiles of the one-per-CU variant).
+template <int BM, int BN, int HR, int TAPU, int MINB, int KS, int NW = 8>
+__global__ __launch_bounds__(64 * NW, MINB) __attribute__((amdgpu_waves_per_eu(NW / 4 * MINB)))
 void conv3_kernel(const ConvArgs a)
 {
-    constexpr int WAVES_N = BN % 64 == 0 ? BN / 64 : 2, WAVES_M = 8 / WAVES_N;
+    constexpr int WAVES_N = BN % 64 == 0 ? BN / 64 : 2, WAVES_M = NW / WAVES_N;
     constexpr int WROWS = BM / WAVES_M;            // wave tile WROWS x WN
     constexpr int WN = BN / WAVES_N;
     static_assert(WROWS % 16 == 0 && WROWS <= 64 && WN % 16 == 0 && WN <= 64, "wave tiles");
@@ -153,7 +158,7 @@ void conv3_kernel(const ConvArgs a)
     constexpr int KT = KS * KS;                   // taps
     constexpr int UPC = KT / TAPU;                // units per 32-channel chunk
     constexpr int API = HR / 16;                  // halo DMA instructions per block (16 rows each)
-    constexpr int AIW = (API + 7) / 8;            // ... per wave, at most
+    constexpr int AIW = (API + NW - 1) / NW;      // ... per wave, at most
     constexpr int BROWS = TAPU * BN;              // B rows per unit: tap-major, then channel n
     constexpr int BPI = BROWS / 16;               // B DMA instructions per block per unit
     constexpr int ASLOT = HR * 4;                 // 16-byte pieces per halo slot
@@ -187,7 +192,7 @@ void conv3_kernel(const ConvArgs a)
     const uint16_t* arow[AIW];
 #pragma unroll
     for (int i = 0; i < AIW; ++i) {
-        const int hr = (i * 8 + wave) * 16 + lrow;
+        const int hr = (i * NW + wave) * 16 + lrow;
         const int lp = phys ^ (((hr >> 2) & 1) << 1);
         int yy, xx, s;
         int f;
@@ -195,8 +200,8 @@ void conv3_kernel(const ConvArgs a)
         arow[i] = a.in + a.in_coff + pos * a.in_cs + lp * 8;
     }
     // this wave issues halo instructions i*8 + wave < API and B instructions j*8 + wave < BPI
-    const int ai = (API - wave + 7) / 8;
-    const int bi = (BPI - wave + 7) / 8;
+    const int ai = (API - wave + NW - 1) / NW;
+    const int bi = (BPI - wave + NW - 1) / NW;
     const uint16_t* wbase = a.w + (size_t)nb * cpt * KT * BN * 32;
 
 #define OPK3_ISSUE(u_)                                                                        \
@@ -205,17 +210,17 @@ void conv3_kernel(const ConvArgs a)
         if ((u_) - c_ * UPC == 0) {                                                           \
             const int as_ = (c_ % NAS) * ASLOT;                                               \
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
-                if (API % 8 == 0 || i_ * 8 + wave < API)                                      \
+                if (API % NW == 0 || i_ * NW + wave < API)                                    \
                     __builtin_amdgcn_global_load_lds(                                         \
                         (const void*)(arow[i_] + c_ * 32),                                    \
-                        (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * 8 + wave) * 64]), \
+                        (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * NW + wave) * 64]), \
                         16, 0, 0);                                                            \
         }                                                                                     \
         const int bs_ = NAS * ASLOT + ((u_) % 3) * BSLOT;                                     \
         const uint16_t* ub_ = wbase + (size_t)(u_) * BROWS * 32;                              \
-        _Pragma("unroll") for (int j_ = 0; j_ < (BPI + 7) / 8; ++j_) {                        \
-            if (BPI % 8 == 0 || j_ * 8 + wave < BPI) {                                        \
-                const int rb_ = (j_ * 8 + wave) * 16 + lrow;                                  \
+        _Pragma("unroll") for (int j_ = 0; j_ < (BPI + NW - 1) / NW; ++j_) {                  \
+            if (BPI % NW == 0 || j_ * NW + wave < BPI) {                                      \
+                const int rb_ = (j_ * NW + wave) * 16 + lrow;                                 \
                 const int lp_ = phys ^ (((rb_ >> 2) & 1) << 1);                               \
                 __builtin_amdgcn_global_load_lds(                                             \
                     (const void*)(ub_ + rb_ * 32 + lp_ * 8),                                  \
@@ -246,7 +251,8 @@ void conv3_kernel(const ConvArgs a)
             mv[j_] = a.act == 2 ? sl_ : float4_t{neg, neg, neg, neg};                         \
         }                                                                                     \
     } while (0)
-    if constexpr (MINB == 1) OPK3_BIAS();
+    constexpr bool BIAS_EARLY = MINB == 1 && NW == 8;   // registers to spare across the K loop
+    if constexpr (BIAS_EARLY) OPK3_BIAS();
 
     OPK3_ISSUE(0);
     if (U > 1) OPK3_ISSUE(1);
@@ -254,9 +260,15 @@ void conv3_kernel(const ConvArgs a)
         const int c = u / UPC, t = u - (u / UPC) * UPC;
         // this wave's loads of unit u have landed once only unit u+1's may still be in flight
         vm_wait_rt(u + 1 < U ? bi + (t == UPC - 1 ? ai : 0) : 0);
+#if OPK3_ABLATE != 3   // dev probe only (3): no block barrier
         __builtin_amdgcn_s_barrier();
+#endif
         if (u == 0) OPK3_STAMP(1);
+#if OPK3_ABLATE == 2   // dev probe only: no DMA after the prologue (MFMA + LDS-read floor)
+        if (u + 2 < U && u + 2 < 3) OPK3_ISSUE(u + 2);
+#else
         if (u + 2 < U) OPK3_ISSUE(u + 2);
+#endif
         const uint4* As = lds + (c % NAS) * ASLOT;
         const uint4* Bs = lds + NAS * ASLOT + (u % 3) * BSLOT;
 #pragma unroll
@@ -265,22 +277,33 @@ void conv3_kernel(const ConvArgs a)
             const int ky = tap / 3, kx = tap - 3 * (tap / 3);
             half8_t fa[MF], fb[NF];
             const int hoff = KS == 3 ? ky * g.VW + kx : 0;
+#if OPK3_ABLATE == 4   // dev probe only: no fragment reads (register operands)
+#pragma unroll
+            for (int i = 0; i < MF; ++i) fa[i] = (half8_t)(_Float16)(hoff + i);
+#pragma unroll
+            for (int j = 0; j < NF; ++j) fb[j] = (half8_t)(_Float16)(k + j);
+#else
 #pragma unroll
             for (int i = 0; i < MF; ++i)
                 fa[i] = __builtin_bit_cast(half8_t, As[swz64(wm * WROWS + i * 16 + r16 + hoff, q)]);
 #pragma unroll
             for (int j = 0; j < NF; ++j)
                 fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(k * BN + wn * WN + j * 16 + r16, q)]);
+#endif
 #pragma unroll
             for (int i = 0; i < MF; ++i)
 #pragma unroll
                 for (int j = 0; j < NF; ++j)
+#if OPK3_ABLATE == 1   // dev probe only: no MFMAs (data movement + sync floor)
+                    acc[i][j][0] += (float)fb[j][0] * (float)fa[i][0];
+#else
                     acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+#endif
         }
     }
 #undef OPK3_ISSUE
     OPK3_STAMP(2);
-    if constexpr (MINB != 1) OPK3_BIAS();   // two workgroups per CU: not kept across the K loop
+    if constexpr (!BIAS_EARLY) OPK3_BIAS();   // 128-VGPR variants: not kept across the K loop
 #undef OPK3_BIAS
 
     // ---- epilogue straight from registers ------------------------------------------------------
@@ -373,6 +396,7 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
     s.ks = ks;
     s.bn = cout <= 64 ? 64 : (cout <= 96 ? 96 : 128);
     if (ks == 1) {   // no halo: small LDS (three tile slots), two workgroups per CU
+        s.nw = 8;
         s.bm = 256;
         s.hr = s.bm;
         s.tapu = 1;
@@ -384,7 +408,14 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
     // two workgroups per CU pay off once every CU gets at least two 256-position tiles (measured:
     // +10-17 % on the 92x164 / 184x328 / 512-channel layers, -20 % at one tile per CU)
     const long tiles = ((long)frames * (H + 2) * (W + 2) / 256) * ((cout + s.bn - 1) / s.bn);
-    if (small && tiles >= 2 * 256) {   // <= 80 KB of LDS
+    s.nw = 8;
+    static const int big16 = [] {   // dev A/B: OPK_CONV3_W16=0 disables the 16-wave tiles
+        const char* e = std::getenv("OPK_CONV3_W16");
+        return e ? std::atoi(e) : 1;
+    }();
+    if (s.bn == 128 && big16 && tiles >= 3 * 256) {   // 512 x 128 tiles, 16 waves, 160 KB
+        s.bm = 512; s.hr = 704; s.tapu = 3; s.minb = 1; s.nw = 16;
+    } else if (small && tiles >= 2 * 256) {   // <= 80 KB of LDS
         s.bm = 256; s.hr = 448; s.tapu = 1; s.minb = 2;
     } else if (s.bn != 64) {
         s.bm = 256; s.hr = 512; s.tapu = 3; s.minb = 1;
@@ -430,7 +461,10 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
         if (s.minb == 2) OPK3_LAUNCH(256, 96, 448, 1, 2, 3);
         else OPK3_LAUNCH(256, 96, 512, 3, 1, 3);
     } else {
-        if (s.minb == 2) OPK3_LAUNCH(256, 128, 448, 1, 2, 3);
+        if (s.nw == 16)
+            hipLaunchKernelGGL((conv3_kernel<512, 128, 704, 3, 1, 3, 16>), grid, dim3(1024), 0,
+                               stream, a);
+        else if (s.minb == 2) OPK3_LAUNCH(256, 128, 448, 1, 2, 3);
         else OPK3_LAUNCH(256, 128, 512, 3, 1, 3);
     }
 #undef OPK3_LAUNCH
