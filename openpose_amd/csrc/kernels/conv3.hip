@@ -413,7 +413,7 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
         const char* e = std::getenv("OPK_CONV3_W16");
         return e ? std::atoi(e) : 1;
     }();
-    if (s.bn == 128 && big16 && tiles >= 3 * 256) {   // 512 x 128 tiles, 16 waves, 160 KB
+    if (s.bn != 64 && big16 && tiles >= 3 * 256) {   // 512 x {128,96} tiles, 16 waves
         s.bm = 512; s.hr = 704; s.tapu = 3; s.minb = 1; s.nw = 16;
     } else if (small && tiles >= 2 * 256) {   // <= 80 KB of LDS
         s.bm = 256; s.hr = 448; s.tapu = 1; s.minb = 2;
@@ -458,7 +458,10 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
         if (s.minb == 2) OPK3_LAUNCH(256, 64, 448, 1, 2, 3);
         else OPK3_LAUNCH(512, 64, 768, 3, 1, 3);
     } else if (s.bn == 96) {
-        if (s.minb == 2) OPK3_LAUNCH(256, 96, 448, 1, 2, 3);
+        if (s.nw == 16)
+            hipLaunchKernelGGL((conv3_kernel<512, 96, 704, 3, 1, 3, 16>), grid, dim3(1024), 0,
+                               stream, a);
+        else if (s.minb == 2) OPK3_LAUNCH(256, 96, 448, 1, 2, 3);
         else OPK3_LAUNCH(256, 96, 512, 3, 1, 3);
     } else {
         if (s.nw == 16)
