@@ -340,6 +340,7 @@ void NetHip::reshape(int n, int h, int w)
     const bool allow3 = !conv_v1_ && !(e3 && e3[0] == '0');
     const size_t out_bytes = (size_t)n * out_c_ * lh_[out_level_] * lw_[out_level_] * 4;
     out32_ = static_cast<float*>(out_mem_.get(out_bytes));
+    void* sink = sink_.get(kConv3SinkBytes);
     for (auto& c : convs_) {
         ConvArgs& a = c.args;
         a = ConvArgs{};
@@ -359,6 +360,8 @@ void NetHip::reshape(int n, int h, int w)
             const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, c.info.k);
             a.sw = s3.sw;
             a.nstrips = s3.nstrips;
+            a.sink = sink;
+            a.cus = cus_;
         }
         a.w = static_cast<const uint16_t*>(c.use3 ? c.w3.ptr : c.w.ptr);
         a.bias = static_cast<const float*>(c.bias.ptr);

@@ -78,6 +78,7 @@ private:
     std::vector<std::unique_ptr<DevBuf>> mem_;
     std::vector<uint16_t*> base_;   // first position of each buffer (past its head guard)
     DevBuf out_mem_;
+    DevBuf sink_;                 // persistent conv3: target of masked-off stores
     float* out32_ = nullptr;
 };
 

@@ -37,6 +37,8 @@ struct ConvArgs {
     int out32_c, out32_coff;
     int sw, nstrips;      // conv3 only: strip width and count (conv3_shape)
     float rcp[3];         // conv3 only, set by launch_conv3: 1/((H+2)(sw+2)), 1/(sw+2), 1/nstrips
+    void* sink;           // conv3 persistent variant: >= kConv3SinkBytes of scratch (masked stores)
+    int cus;              // conv3 persistent variant: compute units (grid size); 0 disables it
 };
 
 // v1 (conv.hip): 256 lanes, 128 x bn tile, register-staged; bn: 32, 64, 96 or 128
@@ -49,11 +51,13 @@ void launch_conv2(const ConvArgs& a, int bn, hipStream_t stream);
 // Weights packed [cout_pad/BN][cin_pad/32][ky][kx][BN][32] (BN = conv3_shape(...).bn).  Reads padded positions down to -1
 // and the whole row past the last one: buffers carry zeroed guards (kConvGuardTail positions).
 constexpr int kConvGuardTail = 1024;   // positions
+constexpr size_t kConv3SinkBytes = (size_t)1024 * 1024 * 8;   // 1024 lanes x 1024 workgroups x 8 B
 struct Conv3Shape {
     int ks;                       // 3 or 1
     int bm, bn, hr, tapu, minb;   // tile, halo rows, taps per K unit, workgroups per CU
     int nw;                       // waves per workgroup
     int sw, nstrips;
+    bool persist;                 // 16-wave tiles: persistent kernel (conv3p) when the launch allows
 };
 Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks);
 void launch_conv3(const ConvArgs& a, hipStream_t stream);

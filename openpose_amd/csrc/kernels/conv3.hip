@@ -28,6 +28,7 @@
 // registers (no LDS pass).
 #include "conv.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 #include "../common.h"
@@ -224,7 +225,7 @@ void conv3_kernel(const ConvArgs a)
                 const int lp_ = phys ^ (((rb_ >> 2) & 1) << 1);                               \
                 __builtin_amdgcn_global_load_lds(                                             \
                     (const void*)(ub_ + rb_ * 32 + lp_ * 8),                                  \
-                    (__attribute__((address_space(3))) void*)(&lds[bs_ + (j_ * 8 + wave) * 64]), \
+                    (__attribute__((address_space(3))) void*)(&lds[bs_ + (j_ * NW + wave) * 64]), \
                     16, 0, 0);                                                                \
             }                                                                                 \
         }                                                                                     \
@@ -363,7 +364,11 @@ void conv3_kernel(const ConvArgs a)
                 const int cs = a.dst_cs[d];
                 uint16_t* p = a.dst[d] + a.dst_coff[d] + ch + prow[i] * cs;
                 if (vec && ((a.dst_coff[d] | cs) & 3) == 0) {
+#if OPK3_ABLATE == 5   // dev probe only: no output stores
+                    asm volatile("" ::"v"(lo), "v"(hi), "v"(p));
+#else
                     *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+#endif
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
@@ -384,16 +389,263 @@ void conv3_kernel(const ConvArgs a)
     OPK3_STAMP(5);
 }
 
+// ---- persistent 16-wave variant ---------------------------------------------------------------
+// conv3p_kernel: the 512 x BN (128 or 96) tile with 3-tap K units of conv3_kernel<..., 16>, made
+// persistent: one workgroup per CU walks its tiles and issues the next tile's first two K units
+// during the current tile's last two, so every prologue (halo + weight DMA latency) overlaps the
+// previous tile's epilogue.  Bias/slopes live in LDS for the whole launch.
+//
+// vmcnt counts stores as well as loads on gfx950 and retires in issue order, so the counted waits
+// must know how many stores an epilogue issued: every (fragment, destination) pair issues exactly
+// one 8-byte store (lanes of border positions write to a scratch "sink"), S = MF*NF*ndst.
+#define OPK3_VM_CASE(n_) case n_: vm_wait<n_>(); break;
+__device__ __forceinline__ void vm_wait_rt64(int n)
+{
+    switch (n) {
+        OPK3_VM_CASE(0) OPK3_VM_CASE(1) OPK3_VM_CASE(2) OPK3_VM_CASE(3) OPK3_VM_CASE(4)
+        OPK3_VM_CASE(5) OPK3_VM_CASE(6) OPK3_VM_CASE(7) OPK3_VM_CASE(8) OPK3_VM_CASE(9)
+        OPK3_VM_CASE(10) OPK3_VM_CASE(11) OPK3_VM_CASE(12) OPK3_VM_CASE(13) OPK3_VM_CASE(14)
+        OPK3_VM_CASE(15) OPK3_VM_CASE(16) OPK3_VM_CASE(17) OPK3_VM_CASE(18) OPK3_VM_CASE(19)
+        OPK3_VM_CASE(20) OPK3_VM_CASE(21) OPK3_VM_CASE(22) OPK3_VM_CASE(23) OPK3_VM_CASE(24)
+        OPK3_VM_CASE(25) OPK3_VM_CASE(26) OPK3_VM_CASE(27) OPK3_VM_CASE(28) OPK3_VM_CASE(29)
+        OPK3_VM_CASE(30) OPK3_VM_CASE(31) OPK3_VM_CASE(32) OPK3_VM_CASE(33) OPK3_VM_CASE(34)
+        OPK3_VM_CASE(35) OPK3_VM_CASE(36) OPK3_VM_CASE(37) OPK3_VM_CASE(38) OPK3_VM_CASE(39)
+        OPK3_VM_CASE(40) OPK3_VM_CASE(41) OPK3_VM_CASE(42) OPK3_VM_CASE(43) OPK3_VM_CASE(44)
+        OPK3_VM_CASE(45) OPK3_VM_CASE(46) OPK3_VM_CASE(47) OPK3_VM_CASE(48) OPK3_VM_CASE(49)
+        OPK3_VM_CASE(50) OPK3_VM_CASE(51) OPK3_VM_CASE(52) OPK3_VM_CASE(53) OPK3_VM_CASE(54)
+        OPK3_VM_CASE(55) OPK3_VM_CASE(56) OPK3_VM_CASE(57) OPK3_VM_CASE(58) OPK3_VM_CASE(59)
+        OPK3_VM_CASE(60) OPK3_VM_CASE(61) OPK3_VM_CASE(62) OPK3_VM_CASE(63)
+    default: vm_wait<0>(); break;
+    }
+}
+#undef OPK3_VM_CASE
+
+constexpr int kP_BM = 512, kP_HR = 688, kP_NW = 16;
+
+template <int BN>
+__global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
+{
+    constexpr int NW = kP_NW, BM = kP_BM, HR = kP_HR;
+    constexpr int WAVES_N = 2, WAVES_M = NW / WAVES_N;
+    constexpr int WROWS = BM / WAVES_M, WN = BN / WAVES_N;
+    static_assert(WROWS == 64 && WN % 16 == 0 && WN <= 64, "wave tiles");
+    constexpr int MF = WROWS / 16, NF = WN / 16;
+    constexpr int API = HR / 16, AIW = (API + NW - 1) / NW;
+    constexpr int BROWS = 3 * BN, BPI = BROWS / 16, BIW = (BPI + NW - 1) / NW;
+    constexpr int ASLOT = HR * 4, BSLOT = BROWS * 4;
+    constexpr int LDS_PIECES = 2 * ASLOT + 3 * BSLOT + BN / 2;   // + bias and slope floats
+    static_assert(LDS_PIECES * 16 <= 160 * 1024, "LDS budget");
+    __shared__ uint4 lds[LDS_PIECES];
+    float* lbias = reinterpret_cast<float*>(lds + 2 * ASLOT + 3 * BSLOT);
+    float* lmul = lbias + BN;
+
+    OPK3_STAMP(0);
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WAVES_N, wn = wave - (wave / WAVES_N) * WAVES_N;
+    const int r16 = lane & 15, q = lane >> 4;
+    const Strips g(a);
+    const int nn = a.cout / BN;                   // cout % BN == 0 (host)
+    const int ntm = (g.total + BM - 1) / BM;
+    // XCD-aware bijective order; block -> (n-block, first m-tile); m-tiles stride by G / nn
+    const int G = gridDim.x;
+    const int xcd = blockIdx.x & 7, qq = G >> 3, rr = G & 7;
+    const int tix = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (blockIdx.x >> 3);
+    const int per_n = G / nn;
+    const int nb = tix % nn;
+    int m = tix / nn;
+    const int n0 = nb * BN;
+    if (m >= ntm) return;
+
+    // bias and negative-side multiplier of this n-block, for the whole launch
+    if (tid < BN) {
+        const float neg = a.act == 1 ? 0.f : 1.f;
+        lbias[tid] = a.bias[n0 + tid];
+        lmul[tid] = a.act == 2 ? a.slope[n0 + tid] : neg;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    const int lrow = lane >> 2, phys = lane & 3;
+    const int cpt = a.cin_pad >> 5;
+    const int U = 3 * cpt;
+    const int ai = (API - wave + NW - 1) / NW, bi = (BPI - wave + NW - 1) / NW;
+    const uint16_t* wbase = a.w + (size_t)nb * cpt * 9 * BN * 32;
+    int boff[BIW];
+#pragma unroll
+    for (int j = 0; j < BIW; ++j) {
+        const int rb = (j * NW + wave) * 16 + lrow;
+        boff[j] = rb * 32 + (phys ^ (((rb >> 2) & 1) << 1)) * 8;
+    }
+    // halo rows as 32-bit byte offsets from the position before the image (map() >= -1; buffers
+    // hold < 2^31 elements): one VGPR each, SGPR base + VGPR offset addressing
+    const char* abase = reinterpret_cast<const char*>(a.in + a.in_coff - a.in_cs);
+    uint32_t aoff[AIW];
+#define OPK3P_AROW(mt_)                                                                       \
+    do {                                                                                      \
+        _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_) {                                  \
+            const int hr_ = (i_ * NW + wave) * 16 + lrow;                                     \
+            const int lp_ = phys ^ (((hr_ >> 2) & 1) << 1);                                   \
+            int f_, yy_, xx_, s_;                                                             \
+            const long pos_ = g.map((mt_) * BM - g.VW - 1 + hr_, f_, yy_, xx_, s_);           \
+            aoff[i_] = (uint32_t)(((pos_ + 1) * a.in_cs + lp_ * 8) * 2);                      \
+        }                                                                                     \
+    } while (0)
+    // K unit (chunk c_, tap row ky_) of the tile whose halo rows arow points at
+#define OPK3P_ISSUE(c_, ky_, aslot_, bslot_)                                                  \
+    do {                                                                                      \
+        if ((ky_) == 0) {                                                                     \
+            const int as_ = (aslot_) * ASLOT;                                                 \
+            _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
+                if (API % NW == 0 || i_ * NW + wave < API)                                    \
+                    __builtin_amdgcn_global_load_lds(                                         \
+                        (const void*)(abase + (c_) * 64 + aoff[i_]),                          \
+                        (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * NW + wave) * 64]), \
+                        16, 0, 0);                                                            \
+        }                                                                                     \
+        const int bs_ = 2 * ASLOT + (bslot_) * BSLOT;                                         \
+        const uint16_t* ub_ = wbase + (size_t)((c_) * 3 + (ky_)) * BROWS * 32;                \
+        _Pragma("unroll") for (int j_ = 0; j_ < BIW; ++j_)                                    \
+            if (BPI % NW == 0 || j_ * NW + wave < BPI)                                        \
+                __builtin_amdgcn_global_load_lds(                                             \
+                    (const void*)(ub_ + boff[j_]),                                            \
+                    (__attribute__((address_space(3))) void*)(&lds[bs_ + (j_ * NW + wave) * 64]), \
+                    16, 0, 0);                                                                \
+    } while (0)
+
+    const int S = MF * NF * a.ndst;               // store instructions per epilogue and wave
+    const bool exact = S + ai + bi <= 63;
+
+    OPK3P_AROW(m);
+    OPK3P_ISSUE(0, 0, 0, 0);
+    OPK3P_ISSUE(0, 1, 0, 1);
+    int gc = 0;                                   // running chunk index of this tile's chunk 0
+    for (int it = 0;; ++it) {
+        const int mn = m + per_n;
+        const bool has_next = mn < ntm;
+        const int p0 = m * BM;
+        float4_t acc[MF][NF];
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+            for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+        for (int u = 0; u < U; ++u) {
+            const int c = u / 3, ky = u - 3 * (u / 3);
+            // outstanding VMEM ops younger than unit u's loads: unit u+1's loads (this tile or the
+            // next tile's unit 0), plus the previous epilogue's stores for units 0 and 1
+            int younger = u + 1 < U ? bi + ((u + 1) % 3 == 0 ? ai : 0) : (has_next ? bi + ai : 0);
+            if (it > 0 && u < 2 && exact) younger += S;
+            vm_wait_rt64(younger);
+            __builtin_amdgcn_s_barrier();
+            if (u == 0 && it == 0) OPK3_STAMP(1);
+            if (u + 2 < U) {
+                const int c2 = (u + 2) / 3;
+                OPK3P_ISSUE(c2, (u + 2) - 3 * c2, (gc + c2) & 1, (u + 2) % 3);
+            } else if (has_next) {
+                if (u + 2 == U) OPK3P_AROW(mn);
+                OPK3P_ISSUE(0, u + 2 - U, (gc + cpt) & 1, (u + 2) % 3);
+            }
+            const uint4* As = lds + ((gc + c) & 1) * ASLOT;
+            const uint4* Bs = lds + 2 * ASLOT + (u % 3) * BSLOT;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+                half8_t fa[MF], fb[NF];
+                const int hoff = ky * g.VW + kx;
+#pragma unroll
+                for (int i = 0; i < MF; ++i)
+                    fa[i] = __builtin_bit_cast(half8_t, As[swz64(wm * WROWS + i * 16 + r16 + hoff, q)]);
+#pragma unroll
+                for (int j = 0; j < NF; ++j)
+                    fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(kx * BN + wn * WN + j * 16 + r16, q)]);
+#pragma unroll
+                for (int i = 0; i < MF; ++i)
+#pragma unroll
+                    for (int j = 0; j < NF; ++j)
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+            }
+        }
+        if (it == 0) OPK3_STAMP(2);
+
+        // ---- epilogue: one 8-byte store per (fragment, destination), border lanes to the sink ----
+        long prow[MF];
+        bool pok[MF];
+        {
+            int pbase = p0 + wm * WROWS + r16;
+            asm volatile("" : "+v"(pbase));
+            int f, yy, xx, s;
+            prow[0] = g.map(pbase, f, yy, xx, s);
+            pok[0] = yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
+#pragma unroll
+            for (int i = 1; i < MF; ++i) {   // VW > 16 (host): step 16 positions
+                xx += 16;
+                if (xx >= g.VW) {
+                    xx -= g.VW;
+                    if (++yy == a.H + 2) {
+                        yy = 0;
+                        if (++s == g.nstrips) {
+                            s = 0;
+                            ++f;
+                        }
+                    }
+                }
+                const bool in = pbase + i * 16 < g.total;
+                prow[i] = in ? (long)(f * (a.H + 2) + yy) * g.Wp + s * g.sw + xx : 0;
+                pok[i] = in && yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
+            }
+        }
+        const int chl = n0 + wn * WN + 4 * q;
+        int sidx = blockIdx.x * 64 * NW + tid;    // this lane's sink slot
+        asm volatile("" : "+v"(sidx));
+        uint2* sink = reinterpret_cast<uint2*>(a.sink) + sidx;
+#pragma unroll
+        for (int j = 0; j < NF; ++j) {
+            const int cl = wn * WN + j * 16 + 4 * q;   // channel within the n-block
+            const float4_t bj = *reinterpret_cast<const float4_t*>(lbias + cl);
+            const float4_t mj = *reinterpret_cast<const float4_t*>(lmul + cl);
+#pragma unroll
+            for (int i = 0; i < MF; ++i) {
+                const float4_t t = acc[i][j] + bj;
+                const float4_t tm = t * mj;
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
+                const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+                const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                for (int d = 0; d < a.ndst; ++d) {
+                    uint2* p = reinterpret_cast<uint2*>(a.dst[d] + a.dst_coff[d] + chl + j * 16 +
+                                                        prow[i] * a.dst_cs[d]);
+                    *(pok[i] ? p : sink) = make_uint2(lo, hi);
+                }
+            }
+        }
+        if (!has_next) break;
+        m = mn;
+        gc += cpt;
+    }
+#undef OPK3P_ISSUE
+#undef OPK3P_AROW
+    OPK3_STAMP(5);
+}
+
+}  // namespace
+
+namespace {
+int env_int(const char* name, int dflt)
+{
+    const char* e = std::getenv(name);
+    return e && e[0] ? std::atoi(e) : dflt;
+}
 }  // namespace
 
 Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
 {
-    static const bool small = [] {   // dev A/B switch: OPK_CONV3_SMALL=0 -> one workgroup per CU
-        const char* e = std::getenv("OPK_CONV3_SMALL");
-        return !(e && e[0] == '0');
-    }();
+    // dev A/B switches (read per call so tests can compare variants in one process):
+    // OPK_CONV3_SMALL=0 -> no two-per-CU tiles, OPK_CONV3_W16=0 -> no 16-wave tiles,
+    // OPK_CONV3_PERSIST=0 -> 16-wave tiles without the persistent kernel
+    const bool small = env_int("OPK_CONV3_SMALL", 1) != 0;
+    const int big16 = env_int("OPK_CONV3_W16", 1);
     Conv3Shape s;
     s.ks = ks;
+    s.persist = false;
     s.bn = cout <= 64 ? 64 : (cout <= 96 ? 96 : 128);
     if (ks == 1) {   // no halo: small LDS (three tile slots), two workgroups per CU
         s.nw = 8;
@@ -409,12 +661,10 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
     // +10-17 % on the 92x164 / 184x328 / 512-channel layers, -20 % at one tile per CU)
     const long tiles = ((long)frames * (H + 2) * (W + 2) / 256) * ((cout + s.bn - 1) / s.bn);
     s.nw = 8;
-    static const int big16 = [] {   // dev A/B: OPK_CONV3_W16=0 disables the 16-wave tiles
-        const char* e = std::getenv("OPK_CONV3_W16");
-        return e ? std::atoi(e) : 1;
-    }();
     if (s.bn != 64 && big16 && tiles >= 3 * 256) {   // 512 x {128,96} tiles, 16 waves
-        s.bm = 512; s.hr = 704; s.tapu = 3; s.minb = 1; s.nw = 16;
+        s.persist = env_int("OPK_CONV3_PERSIST", 1) != 0;
+        // the persistent kernel keeps bias/slopes in LDS: 688 halo rows (strips <= 85 columns)
+        s.bm = 512; s.hr = s.persist ? kP_HR : 704; s.tapu = 3; s.minb = 1; s.nw = 16;
     } else if (small && tiles >= 2 * 256) {   // <= 80 KB of LDS
         s.bm = 256; s.hr = 448; s.tapu = 1; s.minb = 2;
     } else if (s.bn != 64) {
@@ -446,7 +696,25 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     const long total = (long)a.frames * s.nstrips * (a.H + 2) * (s.sw + 2);
     OPK_CHECK_ARG(total + s.bm + 2L * (s.sw + 2) < (1L << 24), "too many positions per launch");
     const int nn = (a.cout + s.bn - 1) / s.bn;
-    dim3 grid((unsigned)(((total + s.bm - 1) / s.bm) * nn));
+    const long ntiles = ((total + s.bm - 1) / s.bm) * nn;
+    dim3 grid((unsigned)ntiles);
+    // measured: +3-10 % on the single-n-block layers, 3-8 % slower with 2-4 n-blocks (kept 16-wave)
+    if (s.nw == 16 && s.persist && nn == 1 && a.sink && a.cus >= nn && a.cout % s.bn == 0 && !a.out32 &&
+        s.sw + 2 > 16) {
+        bool aligned = true;
+        for (int d = 0; d < a.ndst; ++d) aligned = aligned && ((a.dst_coff[d] | a.dst_cs[d]) & 3) == 0;
+        if (aligned) {   // one workgroup per CU, n-blocks spread evenly over the grid
+            const long per_n = std::min<long>(a.cus / nn, (ntiles + nn - 1) / nn);
+            const unsigned G = (unsigned)(per_n * nn);
+            OPK_CHECK_ARG(G <= 1024, "persistent grid exceeds the sink");
+            if (s.bn == 96)
+                hipLaunchKernelGGL(conv3p_kernel<96>, dim3(G), dim3(1024), 0, stream, a);
+            else
+                hipLaunchKernelGGL(conv3p_kernel<128>, dim3(G), dim3(1024), 0, stream, a);
+            OPK_LAUNCH_CHECK();
+            return;
+        }
+    }
 #define OPK3_LAUNCH(BM_, BN_, HR_, TAPU_, MINB_, KS_)                                          \
     hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, MINB_, KS_>), grid, dim3(512), 0,   \
                        stream, a)

@@ -1,24 +1,67 @@
-"""Per-layer timing report from a rocprofv3 kernel trace of bench.py (dev tool)."""
-import csv, sys
+"""Per-layer timing report from a rocprofv3 kernel trace of bench.py (dev tool).
+
+    python tools/layer_report.py <kernel_trace.csv> <frames_per_step> [--layers]
+
+Maps the kernels of one forward (the second to last) onto the BODY_25 conv/pool layers; a
+conv1_fused_kernel launch stands for conv1_1 + conv1_2 + pool1_stage1.
+"""
+import csv
+import sys
+
 sys.path.insert(0, '.')
-from oracle import body25
+from oracle import body25  # noqa: E402
+
 rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r['Start_Timestamp']))
 frames = int(sys.argv[2]) if len(sys.argv) > 2 else 16
-ks = [r for r in rows if 'conv' in r['Kernel_Name'] and 'kernel' in r['Kernel_Name'] or 'maxpool' in r['Kernel_Name']]
+per_layer = '--layers' in sys.argv
+ks = [r for r in rows if ('conv' in r['Kernel_Name'] and 'kernel' in r['Kernel_Name'])
+      or 'maxpool' in r['Kernel_Name']]
+starts = [i for i, r in enumerate(ks) if 'conv1_fused' in r['Kernel_Name'] or 'conv_image' in r['Kernel_Name']]
+fw = ks[starts[-2]:starts[-1]]
 L = [l for l in body25.layers() if l['type'] in ('Convolution', 'Pooling')]
-per = len(L)
-nfw = len(ks) // per
-fw = ks[per * (nfw - 2): per * (nfw - 1)]
-lvl = 0; H = [368, 184, 92, 46]; W = [656, 328, 164, 82]
-tot = 0; byn = {}
-for l, r in zip(L, fw):
+H = [368, 184, 92, 46]
+W = [656, 328, 164, 82]
+
+
+def flops(l, lvl):
+    return 2 * frames * H[lvl] * W[lvl] * l['num_output'] * l['cin'] * l['kernel_size'] ** 2
+
+
+lvl = 0
+tot = 0
+byn = {}
+li = 0
+for r in fw:
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
-    if l['type'] == 'Pooling':
-        lvl += 1; continue
-    fl = 2 * frames * H[lvl] * W[lvl] * l['num_output'] * l['cin'] * l['kernel_size'] ** 2
+    name = r['Kernel_Name']
+    if 'conv1_fused' in name:   # conv1_1 + conv1_2 + pool1
+        fl = flops(L[0], 0) + flops(L[1], 0)
+        key = ('conv1_1+conv1_2+pool1', 3, 0)
+        li += 3
+        lvl = 1
+        if per_layer:
+            print('%-28s %8.1f us %7.1f TF/s' % (key[0], d, fl / d / 1e6))
+    else:
+        l = L[li]
+        li += 1
+        if l['type'] == 'Pooling':
+            lvl += 1
+            if per_layer:
+                print('%-28s %8.1f us' % (l['name'], d))
+            tot += d
+            continue
+        fl = flops(l, lvl)
+        key = (l['num_output'], l['kernel_size'], lvl)
+        if per_layer:
+            print('%-28s cin=%4d cout=%4d k=%d lvl=%d %8.1f us %7.1f TF/s' %
+                  (l['name'], l['cin'], l['num_output'], l['kernel_size'], lvl, d, fl / d / 1e6))
     tot += d
-    k = (l['num_output'], l['kernel_size'], lvl)
-    a = byn.setdefault(k, [0, 0, 0]); a[0] += d; a[1] += fl; a[2] += 1
+    a = byn.setdefault(key, [0, 0, 0])
+    a[0] += d
+    a[1] += fl
+    a[2] += 1
 for k, (d, fl, n) in sorted(byn.items(), key=lambda kv: -kv[1][0]):
-    print('N=%4d k=%d lvl=%d  n=%3d  %8.1f us  %6.1f TF/s' % (k[0], k[1], k[2], n, d, fl / d / 1e6))
-print('total conv us', round(tot, 1))
+    label = k[0] if isinstance(k[0], str) else 'N=%4d k=%d lvl=%d' % k
+    print('%-24s n=%3d  %9.1f us  %7.1f TF/s' % (label, n, d, fl / d / 1e6))
+print('total CNN us (convs + pools)', round(tot, 1))
