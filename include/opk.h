@@ -27,11 +27,31 @@ extern "C" {
 #define OPK_ERR_STATE 3    /* call out of order (e.g. forward before weights)                   */
 #define OPK_ERR_UNSUPPORTED 4
 
-/* PoseModel values (include/openpose/pose/enumClasses.hpp:9-30) */
+/* PoseModel values (include/openpose/pose/enumClasses.hpp:9-30); the tables of every model are
+ * generated from the reference's poseParameters.cpp (tools/gen_pose_tables.py) */
 #define OPK_BODY_25 0
 #define OPK_COCO_18 1
 #define OPK_MPI_15 2
 #define OPK_MPI_15_4 3
+#define OPK_BODY_19 4
+#define OPK_BODY_19_X2 5
+#define OPK_BODY_19N 6
+#define OPK_BODY_25E 7
+#define OPK_CAR_12 8
+#define OPK_BODY_25D 9
+#define OPK_BODY_23 10
+#define OPK_CAR_22 11
+#define OPK_BODY_19E 12
+#define OPK_BODY_25B 13
+#define OPK_BODY_135 14
+
+/* Connector semantics.  OPK_CONNECT_CPU: connectBodyPartsCpu (bodyPartConnectorBase.cpp:1327-1377,
+ * per-pair greedy matching; the reference accepts BODY_25 / COCO_18 / MPI_15(_4) only).
+ * OPK_CONNECT_GPU: connectBodyPartsGpu's host assembly (bodyPartConnectorBase.cu:147-250:
+ * pafPtrIntoVector's global sort + pafVectorIntoPeopleVector; every model, BODY_135 included).
+ * Pair scores are the same getScoreAB integrals in both. */
+#define OPK_CONNECT_CPU 0
+#define OPK_CONNECT_GPU 1
 
 const char* opk_last_error(void);
 int opk_version(void);
@@ -105,6 +125,31 @@ int opk_assemble_people(float* keypoints_host, float* scores_host, int max_peopl
                         int min_subset_cnt, float min_subset_score, float scale_factor,
                         int maximize_positives);
 
+/* The same two with a connector semantics (OPK_CONNECT_CPU / OPK_CONNECT_GPU); the GPU
+ * semantics replace op::connectBodyPartsGpu<float> for every model. */
+int opk_assemble_people_semantics(float* keypoints_host, float* scores_host, int max_people,
+                                  int* num_people, const float* pair_scores_host,
+                                  const float* peaks_host, int pose_model, int max_peaks,
+                                  int min_subset_cnt, float min_subset_score, float scale_factor,
+                                  int maximize_positives, int semantics);
+int opk_connect_body_parts_semantics(opk_ctx* ctx, float* keypoints_host, float* scores_host,
+                                     int max_people, int* num_people, const float* heat_dev,
+                                     const float* peaks_dev, int pose_model, int heat_channels,
+                                     int heat_h, int heat_w, int max_peaks,
+                                     float inter_min_above_threshold, float inter_threshold,
+                                     int min_subset_cnt, float min_subset_score,
+                                     float default_nms_threshold, float scale_factor,
+                                     int maximize_positives, int semantics);
+
+/* Pose tables (getPoseNumberBodyParts, addBkgChannel, getPosePartPairs, getPoseMapIndex;
+ * poseParameters.hpp:17-34).  Any output pointer may be NULL; pairs gets 2*npairs entries,
+ * map_idx the model's map-index entries (heat_channels - parts - bkg). */
+int opk_pose_model_info(int pose_model, int* parts, int* bkg, int* npairs, int* heat_channels,
+                        int* pairs, int* map_idx);
+/* getPoseDefaultNmsThreshold / getPoseDefaultConnectInterThreshold (poseParameters.hpp:29-31) */
+int opk_pose_default_thresholds(int pose_model, int maximize_positives, float* nms_threshold,
+                                float* inter_threshold);
+
 /* ---- Net: replaces op::Net / op::NetCaffe (include/openpose/net/net.hpp:8-18,
  *      netCaffe.hpp:12-13).  prototxt: a Caffe prototxt path, or "builtin:BODY_25".
  *      caffemodel: path or NULL (then weights must be supplied with opk_net_set_conv). */
@@ -137,6 +182,11 @@ typedef struct opk_pose opk_pose;
 #define OPK_PROP_MIN_SUBSET_SCORE 4
 int opk_pose_create(opk_ctx* ctx, opk_net* net /* may be NULL: net output injected */,
                     int maximize_positives, opk_pose** out);
+/* any pose model (the net output / injected heat maps carry its heat_channels) and connector
+ * semantics; opk_pose_create = (BODY_25, OPK_CONNECT_CPU).  OPK_CONNECT_CPU with a model the
+ * reference's CPU connector rejects fails with OPK_ERR_UNSUPPORTED. */
+int opk_pose_create_model(opk_ctx* ctx, opk_net* net, int pose_model, int maximize_positives,
+                          int semantics, opk_pose** out);
 int opk_pose_destroy(opk_pose* pose);
 int opk_pose_set_property(opk_pose* pose, int property, double value);
 /* frames: [n][3][net_h][net_w] device fp32; producer_w/h: original frame size (for
@@ -144,7 +194,8 @@ int opk_pose_set_property(opk_pose* pose, int property, double value);
 int opk_pose_forward(opk_pose* pose, const float* frames_dev, int n, int net_h, int net_w,
                      int producer_w, int producer_h);
 /* heat-map injection (poseNetOutput path, poseExtractorCaffe.cpp:249-262): net output on device
- * [n][78][h][w]; net_h/net_w = the net input size it corresponds to */
+ * [n][heat_channels][h][w] (78 for BODY_25, 439 for BODY_135); net_h/net_w = the net input size
+ * it corresponds to */
 int opk_pose_forward_net_output(opk_pose* pose, const float* net_output_dev, int n, int out_h,
                                 int out_w, int net_h, int net_w, int producer_w, int producer_h);
 /* Pipelined use (the reference's producer/worker/consumer threads, wrapperAuxiliary.hpp, on one
@@ -163,9 +214,11 @@ int opk_pose_pending(opk_pose* pose);   /* batches in flight, -1 for NULL */
  * [n][78][out_h][out_w] device fp32, NULL to disable */
 int opk_pose_set_overlay(opk_pose* pose, const float* overlay_dev);
 int opk_pose_num_people(opk_pose* pose, int frame);
+/* keypoints_host [max_people][parts][3], scores_host [max_people] of one collected frame */
 int opk_pose_keypoints(opk_pose* pose, int frame, float* keypoints_host, float* scores_host,
                        int max_people);
-/* device pointers of the last forward's heatmaps [n][78][H][W] and peaks [n][25][128][3].
+/* device pointers of the last forward's heatmaps [n][heat_channels][H][W] and peaks
+ * [n][parts][128][3].
  * The pipeline evaluates heat-map values lazily from the net output (NMS and PAF scoring compute
  * the resized values they touch, bit-identical to resizeAndMerge); opk_pose_heatmaps writes the
  * full stack on first request after a collect, while no later batch is in flight.  With

@@ -39,6 +39,11 @@ _SIGS = {
     "opk_connect_body_parts": (_i, [_p, _p, _p, _i, _ip, _p, _p, _i, _i, _i, _i, _i, _f, _f, _i,
                                     _f, _f, _f, _i]),
     "opk_assemble_people": (_i, [_p, _p, _i, _ip, _p, _p, _i, _i, _i, _f, _f, _i]),
+    "opk_connect_body_parts_semantics": (_i, [_p, _p, _p, _i, _ip, _p, _p, _i, _i, _i, _i, _i, _f,
+                                              _f, _i, _f, _f, _f, _i, _i]),
+    "opk_assemble_people_semantics": (_i, [_p, _p, _i, _ip, _p, _p, _i, _i, _i, _f, _f, _i, _i]),
+    "opk_pose_model_info": (_i, [_i, _ip, _ip, _ip, _ip, _p, _p]),
+    "opk_pose_default_thresholds": (_i, [_i, _i, _fp, _fp]),
     "opk_net_create": (_i, [_p, _c.c_char_p, _c.c_char_p, _c.POINTER(_p)]),
     "opk_net_destroy": (_i, [_p]),
     "opk_net_num_convs": (_i, [_p]),
@@ -48,6 +53,7 @@ _SIGS = {
     "opk_net_flops_per_frame": (_i, [_p, _i, _i, _c.POINTER(_d)]),
     "opk_net_output": (_i, [_p, _c.POINTER(_p), _ip]),
     "opk_pose_create": (_i, [_p, _p, _i, _c.POINTER(_p)]),
+    "opk_pose_create_model": (_i, [_p, _p, _i, _i, _i, _c.POINTER(_p)]),
     "opk_pose_destroy": (_i, [_p]),
     "opk_pose_set_property": (_i, [_p, _i, _d]),
     "opk_pose_forward": (_i, [_p, _p, _i, _i, _i, _i, _i]),

@@ -4,14 +4,17 @@ Device memory is handed over as torch CUDA tensors (PyTorch is plumbing here: al
 torch.distributed); every computation runs in libopk_hip.so.  The function names mirror the
 reference operators they replace (include/opk.h lists the reference file:line of each).
 """
+import atexit
 import ctypes
+import weakref
 
 import numpy as np
 import torch
 
 from . import _lib
 from ._lib import check, int4
-from .pose_tables import (BODY_25, CONNECT_INTER_MIN_ABOVE_THRESHOLD, CONNECT_INTER_THRESHOLD,
+from .pose_tables import (BODY_25, CONNECT_CPU, CONNECT_GPU, CONNECT_INTER_MIN_ABOVE_THRESHOLD,
+                          CONNECT_INTER_THRESHOLD,
                           CONNECT_MIN_SUBSET_CNT, CONNECT_MIN_SUBSET_SCORE, NMS_THRESHOLD)
 
 
@@ -20,6 +23,21 @@ def _ptr(t):
         return None
     assert t.is_cuda and t.is_contiguous(), "device tensors must be contiguous CUDA tensors"
     return ctypes.c_void_p(t.data_ptr())
+
+
+# Handles still open at interpreter exit (e.g. held by a test traceback) are closed before the HIP
+# runtime's own teardown: poses, then nets, then contexts.
+_LIVE = {"pose": weakref.WeakSet(), "net": weakref.WeakSet(), "ctx": weakref.WeakSet()}
+
+
+@atexit.register
+def _close_live():
+    for kind in ("pose", "net", "ctx"):
+        for obj in list(_LIVE[kind]):
+            try:
+                obj.close()
+            except Exception:
+                pass
 
 
 class Context:
@@ -34,6 +52,7 @@ class Context:
         h = ctypes.c_void_p()
         check(self.L.opk_ctx_create(device, ctypes.c_void_p(s.cuda_stream), ctypes.byref(h)))
         self.h = h
+        _LIVE["ctx"].add(self)
 
     def close(self):
         if self.h:
@@ -59,6 +78,7 @@ class Context:
         h = ctypes.c_void_p()
         check(self.L.opk_ctx_create(-1, None, ctypes.byref(h)))
         self.h = h
+        _LIVE["ctx"].add(self)
         return self
 
     # ---- operators ---------------------------------------------------------------------------
@@ -85,25 +105,46 @@ class Context:
                            inter_min_above=CONNECT_INTER_MIN_ABOVE_THRESHOLD,
                            inter_th=CONNECT_INTER_THRESHOLD, min_subset_cnt=CONNECT_MIN_SUBSET_CNT,
                            min_subset_score=CONNECT_MIN_SUBSET_SCORE, nms_th=NMS_THRESHOLD,
-                           maximize_positives=False):
-        """One frame: heat [C,H,W] / [1,C,H,W], peaks [parts,maxPeaks+1,3] (connectBodyPartsGpu)."""
+                           maximize_positives=False, semantics=CONNECT_CPU):
+        """One frame: heat [C,H,W] / [1,C,H,W], peaks [parts,maxPeaks+1,3] (connectBodyPartsGpu
+        replacement; semantics CONNECT_CPU / CONNECT_GPU picks the people assembly)."""
         c, h, w = heat.shape[-3:]
         parts = peaks.shape[-3]
         kp = np.zeros((max_people, parts, 3), np.float32)
         ks = np.zeros(max_people, np.float32)
         n = ctypes.c_int()
-        check(self.L.opk_connect_body_parts(
+        check(self.L.opk_connect_body_parts_semantics(
             self.h, kp.ctypes.data_as(ctypes.c_void_p), ks.ctypes.data_as(ctypes.c_void_p),
             max_people, ctypes.byref(n), _ptr(heat), _ptr(peaks), pose_model, c, h, w,
             peaks.shape[-2] - 1, inter_min_above, inter_th, min_subset_cnt, min_subset_score,
-            nms_th, scale, int(maximize_positives)))
+            nms_th, scale, int(maximize_positives), semantics))
         k = min(n.value, max_people)
         return kp[:k].copy(), ks[:k].copy()
 
 
+def pose_model_info(pose_model):
+    """Tables of a PoseModel from libopk_hip: dict(parts, bkg, pairs, map_idx, heat_channels,
+    nms_threshold, inter_threshold)."""
+    L = _lib.load()
+    parts, bkg, npairs, hc = (ctypes.c_int() for _ in range(4))
+    check(L.opk_pose_model_info(pose_model, ctypes.byref(parts), ctypes.byref(bkg),
+                                ctypes.byref(npairs), ctypes.byref(hc), None, None))
+    pairs = np.zeros(2 * npairs.value, np.int32)
+    nmap = hc.value - parts.value - bkg.value
+    mi = np.zeros(max(nmap, 1), np.int32)
+    check(L.opk_pose_model_info(pose_model, None, None, None, None,
+                                pairs.ctypes.data_as(ctypes.c_void_p),
+                                mi.ctypes.data_as(ctypes.c_void_p)))
+    nms, inter = ctypes.c_float(), ctypes.c_float()
+    check(L.opk_pose_default_thresholds(pose_model, 0, ctypes.byref(nms), ctypes.byref(inter)))
+    return dict(id=pose_model, parts=parts.value, bkg=bool(bkg.value), pairs=pairs.tolist(),
+                map_idx=mi[:nmap].tolist(), heat_channels=hc.value, nms_threshold=nms.value,
+                inter_threshold=inter.value)
+
+
 def assemble_people(pair_scores, peaks, pose_model=BODY_25, scale=1.0, max_people=512,
                     min_subset_cnt=CONNECT_MIN_SUBSET_CNT, min_subset_score=CONNECT_MIN_SUBSET_SCORE,
-                    maximize_positives=False):
+                    maximize_positives=False, semantics=CONNECT_CPU):
     """Host-only assembly from numpy pair scores [npairs,mp,mp] + peaks [parts,mp+1,3]."""
     L = _lib.load()
     pair_scores = np.ascontiguousarray(pair_scores, np.float32)
@@ -112,12 +153,13 @@ def assemble_people(pair_scores, peaks, pose_model=BODY_25, scale=1.0, max_peopl
     kp = np.zeros((max_people, parts, 3), np.float32)
     ks = np.zeros(max_people, np.float32)
     n = ctypes.c_int()
-    check(L.opk_assemble_people(kp.ctypes.data_as(ctypes.c_void_p),
-                                ks.ctypes.data_as(ctypes.c_void_p), max_people, ctypes.byref(n),
-                                pair_scores.ctypes.data_as(ctypes.c_void_p),
-                                peaks.ctypes.data_as(ctypes.c_void_p), pose_model,
-                                peaks.shape[1] - 1, min_subset_cnt, min_subset_score, scale,
-                                int(maximize_positives)))
+    check(L.opk_assemble_people_semantics(kp.ctypes.data_as(ctypes.c_void_p),
+                                          ks.ctypes.data_as(ctypes.c_void_p), max_people,
+                                          ctypes.byref(n),
+                                          pair_scores.ctypes.data_as(ctypes.c_void_p),
+                                          peaks.ctypes.data_as(ctypes.c_void_p), pose_model,
+                                          peaks.shape[1] - 1, min_subset_cnt, min_subset_score,
+                                          scale, int(maximize_positives), semantics))
     k = min(n.value, max_people)
     return kp[:k].copy(), ks[:k].copy()
 
@@ -131,6 +173,7 @@ class Net:
         h = ctypes.c_void_p()
         check(self.L.opk_net_create(ctx.h, prototxt.encode(), None, ctypes.byref(h)))
         self.h = h
+        _LIVE["net"].add(self)
 
     def close(self):
         if self.h:
@@ -197,14 +240,17 @@ class Net:
 class PoseExtractor:
     """op::PoseExtractorCaffe replacement for batches of frames (PoseHip)."""
 
-    def __init__(self, ctx, net=None, maximize_positives=False):
+    def __init__(self, ctx, net=None, maximize_positives=False, pose_model=BODY_25,
+                 semantics=CONNECT_CPU):
         self.ctx = ctx
         self.L = ctx.L
         h = ctypes.c_void_p()
-        check(self.L.opk_pose_create(ctx.h, net.h if net is not None else None,
-                                     int(maximize_positives), ctypes.byref(h)))
+        check(self.L.opk_pose_create_model(ctx.h, net.h if net is not None else None, pose_model,
+                                           int(maximize_positives), semantics, ctypes.byref(h)))
         self.h = h
+        _LIVE["pose"].add(self)
         self.net = net
+        self.parts = pose_model_info(pose_model)["parts"]
 
     def close(self):
         if self.h:
@@ -230,7 +276,7 @@ class PoseExtractor:
                                       producer_size[1]))
 
     def forward_net_output(self, net_output, net_size, producer_size):
-        """net_output: [n, 78, h, w] CUDA tensor (or (ptr, shape)); net_size = (w, h)."""
+        """net_output: [n, heat_channels, h, w] CUDA tensor (or (ptr, shape)); net_size = (w, h)."""
         if isinstance(net_output, tuple):
             ptr, shape = net_output
             ptr = ctypes.c_void_p(ptr)
@@ -270,7 +316,7 @@ class PoseExtractor:
 
     def keypoints(self, frame):
         n = self.num_people(frame)
-        kp = np.zeros((max(n, 1), 25, 3), np.float32)
+        kp = np.zeros((max(n, 1), self.parts, 3), np.float32)
         ks = np.zeros(max(n, 1), np.float32)
         check(self.L.opk_pose_keypoints(self.h, frame, kp.ctypes.data_as(ctypes.c_void_p),
                                         ks.ctypes.data_as(ctypes.c_void_p), n))

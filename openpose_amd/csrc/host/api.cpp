@@ -1,4 +1,5 @@
 // api.cpp -- C-ABI (include/opk.h): context, memory, resizeAndMerge, NMS, PAF scores, connector.
+#include <algorithm>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -210,17 +211,53 @@ int opk_paf_scores(opk_ctx* ctx, float* pair_scores, const float* heat, const fl
     });
 }
 
+int opk_pose_model_info(int pose_model, int* parts, int* bkg, int* npairs, int* heat_channels,
+                        int* pairs, int* map_idx)
+{
+    return guarded([&] {
+        const auto& m = opk::pose_model(pose_model);
+        if (parts) *parts = m.parts;
+        if (bkg) *bkg = m.bkg ? 1 : 0;
+        if (npairs) *npairs = m.npairs();
+        if (heat_channels) *heat_channels = m.heat_channels();
+        if (pairs) std::copy(m.pairs.begin(), m.pairs.end(), pairs);
+        if (map_idx) std::copy(m.map_idx.begin(), m.map_idx.end(), map_idx);
+    });
+}
+
+int opk_pose_default_thresholds(int pose_model, int maxpos, float* nms_threshold,
+                                float* inter_threshold)
+{
+    return guarded([&] {
+        const auto& m = opk::pose_model(pose_model);
+        if (nms_threshold) *nms_threshold = maxpos ? m.nms_th_maxpos : m.nms_th;
+        if (inter_threshold) *inter_threshold = maxpos ? m.inter_th_maxpos : m.inter_th;
+    });
+}
+
 int opk_assemble_people(float* kp_out, float* ks_out, int max_people, int* num_people,
                         const float* pair_scores, const float* peaks, int pose_model,
                         int max_peaks, int min_cnt, float min_score, float scale, int maxpos)
 {
+    return opk_assemble_people_semantics(kp_out, ks_out, max_people, num_people, pair_scores, peaks,
+                                         pose_model, max_peaks, min_cnt, min_score, scale, maxpos,
+                                         OPK_CONNECT_CPU);
+}
+
+int opk_assemble_people_semantics(float* kp_out, float* ks_out, int max_people, int* num_people,
+                                  const float* pair_scores, const float* peaks, int pose_model,
+                                  int max_peaks, int min_cnt, float min_score, float scale,
+                                  int maxpos, int semantics)
+{
     return guarded([&] {
+        OPK_CHECK_ARG(semantics == OPK_CONNECT_CPU || semantics == OPK_CONNECT_GPU,
+                      "unknown connector semantics");
         OPK_CHECK_ARG(pair_scores && peaks && num_people, "NULL argument");
         const auto& m = opk::pose_model(pose_model);
         opk::PairScores ps;
         ps.data = pair_scores;
         ps.max_peaks = max_peaks;
-        opk::ConnectParams p{min_cnt, min_score, scale, maxpos != 0};
+        opk::ConnectParams p{min_cnt, min_score, scale, maxpos != 0, semantics};
         std::vector<float> kp, ks;
         const int n = opk::assemble_people(m, peaks, max_peaks, ps, p, kp, ks);
         *num_people = n;
@@ -236,7 +273,22 @@ int opk_connect_body_parts(opk_ctx* ctx, float* kp_out, float* ks_out, int max_p
                            int max_peaks, float inter_min_above, float inter_th, int min_cnt,
                            float min_score, float nms_th, float scale, int maxpos)
 {
+    return opk_connect_body_parts_semantics(ctx, kp_out, ks_out, max_people, num_people, heat,
+                                            peaks_dev, pose_model, heat_channels, heat_h, heat_w,
+                                            max_peaks, inter_min_above, inter_th, min_cnt,
+                                            min_score, nms_th, scale, maxpos, OPK_CONNECT_CPU);
+}
+
+int opk_connect_body_parts_semantics(opk_ctx* ctx, float* kp_out, float* ks_out, int max_people,
+                                     int* num_people, const float* heat, const float* peaks_dev,
+                                     int pose_model, int heat_channels, int heat_h, int heat_w,
+                                     int max_peaks, float inter_min_above, float inter_th,
+                                     int min_cnt, float min_score, float nms_th, float scale,
+                                     int maxpos, int semantics)
+{
     return guarded([&] {
+        OPK_CHECK_ARG(semantics == OPK_CONNECT_CPU || semantics == OPK_CONNECT_GPU,
+                      "unknown connector semantics");
         OPK_CHECK_ARG(ctx && heat && peaks_dev && num_people, "NULL argument");
         const auto& m = opk::pose_model(pose_model);
         OPK_CHECK_ARG(heat_channels >= m.heat_channels(), "too few heat-map channels");
@@ -259,7 +311,7 @@ int opk_connect_body_parts(opk_ctx* ctx, float* kp_out, float* ks_out, int max_p
         opk::PairScores ps;
         ps.data = hsc;
         ps.max_peaks = max_peaks;
-        opk::ConnectParams p{min_cnt, min_score, scale, maxpos != 0};
+        opk::ConnectParams p{min_cnt, min_score, scale, maxpos != 0, semantics};
         std::vector<float> kp, ks;
         const int n = opk::assemble_people(m, hpk, max_peaks, ps, p, kp, ks);
         *num_people = n;

@@ -132,6 +132,16 @@ int opk_pose_create(opk_ctx* ctx, opk_net* net, int maxpos, opk_pose** out)
     });
 }
 
+int opk_pose_create_model(opk_ctx* ctx, opk_net* net, int pose_model, int maxpos, int semantics,
+                          opk_pose** out)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ctx && out, "NULL argument");
+        *out = new opk_pose{ctx, std::make_unique<opk::PoseHip>(ctx, net ? net->net.get() : nullptr,
+                                                                maxpos != 0, pose_model, semantics)};
+    });
+}
+
 int opk_pose_destroy(opk_pose* p)
 {
     return guarded_net([&] {
@@ -215,7 +225,8 @@ int opk_pose_keypoints(opk_pose* p, int frame, float* kp, float* ks, int max_peo
         const int n = std::min(max_people, p->pose->num_people(frame));
         const auto& k = p->pose->keypoints(frame);
         const auto& s = p->pose->scores(frame);
-        if (kp && n > 0) std::memcpy(kp, k.data(), sizeof(float) * n * 25 * 3);
+        const int parts = opk::pose_model(p->pose->model()).parts;
+        if (kp && n > 0) std::memcpy(kp, k.data(), sizeof(float) * n * parts * 3);
         if (ks && n > 0) std::memcpy(ks, s.data(), sizeof(float) * n);
     });
 }

@@ -1,9 +1,14 @@
 // connector.cpp -- host people assembly (product code, runs on the GPU worker's host thread).
 //
-// Semantics of the reference CPU path, /root/reference/src/openpose/net/bodyPartConnectorBase.cpp:
-//   createPeopleVector (:156-472) fed by precomputed pair scores (its :321-340 input),
-//   removePeopleBelowThresholdsAndFillFaces (:720-884) for <= 65-part models,
-//   peopleVectorToPeopleArray (:886-934).
+// Two assembly semantics of /root/reference/src/openpose/net/bodyPartConnectorBase.cpp:
+//   CPU path (connectBodyPartsCpu :1327-1377, BODY_25 / COCO / MPI only): createPeopleVector
+//     (:156-472) fed by precomputed pair scores (its :321-340 input);
+//   GPU path (connectBodyPartsGpu, bodyPartConnectorBase.cu:147-250, every model incl. BODY_135):
+//     pafPtrIntoVector (:474-541, one global sort of all connections) + pafVectorIntoPeopleVector
+//     (:543-718, create / extend / merge people);
+// then, for both, removePeopleBelowThresholdsAndFillFaces (:720-884, with the >= 135-part hand and
+// face counting and the face-fragment merge via getKeypointsRoi, utilities/keypoint.cpp:586-632)
+// and peopleVectorToPeopleArray (:886-934).
 // The PAF line integrals come from the GPU (kernels/paf.hip); this file only sorts, matches and
 // groups.  People are stored flat (one int row of `parts` score indices per person) instead of a
 // vector of vectors; the arithmetic on scores follows the reference operation for operation
@@ -12,6 +17,10 @@
 
 #include <algorithm>
 #include <cmath>
+#include <limits>
+#include <string>
+
+#include "../common.h"
 
 namespace opk {
 
@@ -62,13 +71,14 @@ int compact_offsets(const PoseModelInfo& m, const float* peaks, int max_peaks,
     return off;
 }
 
-int assemble_people(const PoseModelInfo& m, const float* peaks, int max_peaks,
-                    const PairScores& scores, const ConnectParams& prm, std::vector<float>& kp,
-                    std::vector<float>& ks)
+namespace {
+
+// createPeopleVector (CPU path): pair by pair, greedy one-to-one matching per pair
+void people_per_pair(People& people, const PoseModelInfo& m, const float* peaks, int max_peaks,
+                     const PairScores& scores)
 {
     const int P = m.parts;
     const int stride = 3 * (max_peaks + 1);
-    People people{P, {}, {}, {}};
     std::vector<Cand> cand;
     std::vector<int> chosenA, chosenB;
     std::vector<double> chosenS;
@@ -155,28 +165,243 @@ int assemble_people(const PoseModelInfo& m, const float* peaks, int max_peaks,
         }
     }
 
-    // thresholds (removePeopleBelowThresholdsAndFillFaces, <= 65-part models), with the
-    // second pass at maximizePositives = true when nobody survives
-    std::vector<int> keep;
-    auto select = [&](bool maxpos) {
-        keep.clear();
+}
+
+// pafPtrIntoVector + pafVectorIntoPeopleVector (GPU path): every connection of every pair sorted
+// once by paf + 0.1 (score A + score B), then people are created, extended or merged
+struct Conn {
+    float total, paf;
+    int q, i, j;
+};
+inline bool conn_greater(const Conn& a, const Conn& b)   // std::greater on the tuple
+{
+    if (a.total != b.total) return a.total > b.total;
+    if (a.paf != b.paf) return a.paf > b.paf;
+    if (a.q != b.q) return a.q > b.q;
+    if (a.i != b.i) return a.i > b.i;
+    return a.j > b.j;
+}
+
+void people_global_sort(People& people, const PoseModelInfo& m, const float* peaks, int max_peaks,
+                        const PairScores& scores)
+{
+    const int P = m.parts;
+    const int stride = 3 * (max_peaks + 1);
+    std::vector<Conn> conn;
+    for (int q = 0; q < m.npairs(); ++q) {
+        const int pa = m.pairs[2 * q], pb = m.pairs[2 * q + 1];
+        const int na = round_pos(peaks[pa * stride]);
+        const int nb = round_pos(peaks[pb * stride]);
+        for (int i = 1; i <= na; ++i)
+            for (int j = 1; j <= nb; ++j) {
+                const float s = scores.at(q, i, j, nb);
+                if (!(s > 1e-6)) continue;
+                const float total = s + 0.1f * peaks[pa * stride + i * 3 + 2] +
+                                    0.1f * peaks[pb * stride + j * 3 + 2];
+                conn.push_back({total, s, q, i, j});
+            }
+    }
+    std::sort(conn.begin(), conn.end(), conn_greater);
+
+    std::vector<int> owner((size_t)P * max_peaks, -1);   // person holding (part, peak)
+    std::vector<int> dead;
+    for (const Conn& c : conn) {
+        const int pa = m.pairs[2 * c.q], pb = m.pairs[2 * c.q + 1];
+        const int sa = pa * stride + c.i * 3 + 2, sb = pb * stride + c.j * 3 + 2;
+        int& oa = owner[(size_t)pa * max_peaks + c.i - 1];
+        int& ob = owner[(size_t)pb * max_peaks + c.j - 1];
+        if (oa < 0 && ob < 0) {            // 1. new person
+            const int p = people.add();
+            people.row(p)[pa] = sa;
+            people.row(p)[pb] = sb;
+            people.found[p] = 2;
+            people.score[p] = peaks[sa] + peaks[sb] + c.paf;
+            oa = ob = p;
+        } else if ((oa < 0) != (ob < 0)) {   // 2./3. extend the person holding one end
+            const int p = oa >= 0 ? oa : ob;
+            const int part2 = oa >= 0 ? pb : pa, s2 = oa >= 0 ? sb : sa;
+            if (people.row(p)[part2] == 0) {
+                people.row(p)[part2] = s2;
+                people.found[p]++;
+                people.score[p] += peaks[s2] + c.paf;
+                (oa >= 0 ? ob : oa) = p;
+            }
+        } else if (oa == ob) {               // 4. redundant connection inside one person
+            people.score[oa] += c.paf;
+        } else {                             // 5. merge two people with disjoint parts
+            const int p1 = std::min(oa, ob), p2 = std::max(oa, ob);
+            int* r1 = people.row(p1);
+            const int* r2 = people.row(p2);
+            bool disjoint = true;
+            for (int k = 0; k < P && disjoint; ++k) disjoint = !(r1[k] > 0 && r2[k] > 0);
+            if (!disjoint) continue;
+            for (int k = 0; k < P; ++k)
+                if (r1[k] == 0) r1[k] = r2[k];
+            people.found[p1] += people.found[p2];
+            people.score[p1] += people.score[p2] + c.paf;
+            dead.push_back(p2);
+            for (int& o : owner)
+                if (o == p2) o = p1;
+        }
+    }
+    if (!dead.empty()) {   // erase merged-away people, keeping the order of the others
+        std::sort(dead.begin(), dead.end());
+        dead.erase(std::unique(dead.begin(), dead.end()), dead.end());
+        People kept{P, {}, {}, {}};
+        size_t d = 0;
         for (int p = 0; p < people.size(); ++p) {
-            int counter = people.found[p];
-            if (!maxpos && (P == 25 || P > 70)) {
-                int foot = 0;
-                for (int k = 19; k < 25; ++k) foot += people.row(p)[k] > 0;
-                if (foot > 0) {
-                    counter -= foot;
-                    if (counter <= 4) continue;
+            if (d < dead.size() && dead[d] == p) { ++d; continue; }
+            const int k = kept.add();
+            std::copy(people.row(p), people.row(p) + P, kept.row(k));
+            kept.found[k] = people.found[p];
+            kept.score[k] = people.score[p];
+        }
+        people = std::move(kept);
+    }
+}
+
+// getRoiDiameterAndBounds (bodyPartConnectorBase.cpp:98-154): x, y, width, height
+struct Roi {
+    float x, y, w, h;
+};
+void roi_and_bounds(Roi& r, int& first, int& last, const int* row, const float* peaks, int from,
+                    int to, float margin)
+{
+    r = {std::numeric_limits<float>::max(), std::numeric_limits<float>::max(), 0.f, 0.f};
+    first = last = -1;
+    for (int k = from; k < to; ++k) {
+        const int s = row[k];
+        if (s <= 0 || !(peaks[s] > 0)) continue;
+        const float x = peaks[s - 2], y = peaks[s - 1];
+        if (r.x > x) r.x = x;
+        if (r.y > y) r.y = y;
+        if (r.w < x) r.w = x;
+        if (r.h < y) r.h = y;
+        if (first < 0) first = k;
+        last = k;
+    }
+    if (last > -1) {
+        const float mx = r.w * margin, my = r.h * margin;
+        r.x -= mx;
+        r.y -= my;
+        r.w += 2 * mx;
+        r.h += 2 * my;
+        ++last;
+        r.w += 1 - r.x;
+        r.h += 1 - r.y;
+    }
+}
+
+// getKeypointsRoi (utilities/keypoint.cpp:586-632): intersection over union of two boxes after
+// shifting both so that neither has a negative corner
+float roi_overlap(Roi a, Roi b)
+{
+    const float bx = std::min(std::min(0.f, a.x), b.x);
+    if (bx != 0) { a.x -= bx; b.x -= bx; }
+    const float by = std::min(std::min(0.f, a.y), b.y);
+    if (by != 0) { a.y -= by; b.y -= by; }
+    const float x0 = std::max(a.x, b.x), y0 = std::max(a.y, b.y);
+    const float x1 = std::min(a.x + a.w, b.x + b.w), y1 = std::min(a.y + a.h, b.y + b.h);
+    if (!(x0 < x1 && y0 < y1)) return 0.f;
+    const float inter = (x1 - x0) * (y1 - y0);
+    return inter / (a.w * a.h + b.w * b.h - inter);
+}
+
+// getKeypointCounter (bodyPartConnectorBase.cpp:77-96)
+void discount(int& counter, const int* row, int from, int to, int minimum)
+{
+    int k = 0;
+    for (int i = from; i < to; ++i) k += row[i] > 0;
+    if (k > minimum) counter += minimum - k;
+}
+
+// removePeopleBelowThresholdsAndFillFaces (bodyPartConnectorBase.cpp:720-884)
+void select_people(std::vector<int>& keep, People& people, const float* peaks,
+                   const ConnectParams& prm, bool maxpos)
+{
+    const int P = people.parts;
+    keep.clear();
+    std::vector<int> face_valid, face_invalid;
+    for (int p = 0; p < people.size(); ++p) {
+        const int* r = people.row(p);
+        int counter = people.found[p];
+        if (P >= 135) {   // hands and face count once each
+            const int before = counter;
+            discount(counter, r, 65, 135, 1);
+            if (counter == 1) {
+                face_invalid.push_back(p);
+                continue;
+            }
+            if (counter != before) face_valid.push_back(p);
+            discount(counter, r, 45, 65, 1);
+            discount(counter, r, 25, 45, 1);
+        }
+        if (!maxpos && (P == 25 || P > 70)) {   // feet do not count
+            const int before = counter;
+            discount(counter, r, 19, 25, 0);
+            if (counter != before && counter <= 4) continue;
+        }
+        if (counter >= prm.min_subset_cnt && (people.score[p] / counter) >= prm.min_subset_score)
+            keep.push_back(p);
+        else if ((counter < 1 && P != 25 && P < 70) || counter < 0)
+            throw Error(1, "Bad personCounter (" + std::to_string(counter) +
+                               "). Bug in this function if this happens.");
+    }
+    if (!keep.empty()) {   // face-only fragments join the best-overlapping valid face
+        for (int bad : face_invalid) {
+            Roi rb;
+            int fb, lb;
+            roi_and_bounds(rb, fb, lb, people.row(bad), peaks, 65, 135, 0.2f);
+            float best = 0.f;
+            int besti = -1;
+            for (int v = 0; v < (int)face_valid.size(); ++v) {
+                Roi rv;
+                int fv, lv;
+                roi_and_bounds(rv, fv, lv, people.row(face_valid[v]), peaks, 65, 135, 0.1f);
+                const float o = roi_overlap(rv, rb);
+                if (best < o) {
+                    best = o;
+                    besti = v;
                 }
             }
-            if (counter >= prm.min_subset_cnt && (people.score[p] / counter) >= prm.min_subset_score)
-                keep.push_back(p);
+            if (!(best > 0.3f || (best > 0.01f && face_valid.size() < 3))) continue;
+            const int good = face_valid[besti];
+            int* g = people.row(good);
+            const int* src = people.row(bad);
+            for (int k = fb; k < lb; ++k) {
+                if (src[k] == 0) continue;
+                const float si = peaks[src[k]];
+                if (g[k] == 0) {
+                    g[k] = src[k];
+                    people.score[good] += si;
+                } else if (peaks[g[k]] < si) {
+                    people.score[good] += si - peaks[g[k]];
+                    g[k] = src[k];
+                }
+            }
         }
-    };
-    select(prm.maximize_positives);
-    if (keep.empty() && !prm.maximize_positives) select(true);
+    }
+    if (keep.empty() && !maxpos) select_people(keep, people, peaks, prm, true);
+}
 
+}  // namespace
+
+int assemble_people(const PoseModelInfo& m, const float* peaks, int max_peaks,
+                    const PairScores& scores, const ConnectParams& prm, std::vector<float>& kp,
+                    std::vector<float>& ks)
+{
+    const int P = m.parts;
+    People people{P, {}, {}, {}};
+    if (prm.semantics == kConnectGpu) {
+        people_global_sort(people, m, peaks, max_peaks, scores);
+    } else {
+        if (!m.cpu_connector())   // bodyPartConnectorBase.cpp:165-167
+            throw Error(4, std::string("connectBodyPartsCpu: only BODY_25, COCO_18 and MPI_15 are "
+                                       "supported (") + m.name + "); use the GPU-path semantics");
+        people_per_pair(people, m, peaks, max_peaks, scores);
+    }
+    std::vector<int> keep;
+    select_people(keep, people, peaks, prm, prm.maximize_positives);
     const int n = (int)keep.size();
     kp.assign((size_t)n * P * 3, 0.f);
     ks.assign(n, 0.f);

@@ -19,15 +19,20 @@ struct PairScores {
     }
 };
 
+constexpr int kConnectCpu = 0;   // connectBodyPartsCpu assembly (BODY_25 / COCO / MPI)
+constexpr int kConnectGpu = 1;   // connectBodyPartsGpu assembly (every model, BODY_135 included)
+
 struct ConnectParams {
     int min_subset_cnt = 3;
     float min_subset_score = 0.4f;
     float scale = 1.f;
     bool maximize_positives = false;
+    int semantics = kConnectCpu;
 };
 
-// connectBodyPartsCpu semantics (bodyPartConnectorBase.cpp:1327-1377) fed by precomputed pair
-// scores.  peaks: [parts][max_peaks+1][3] host.  Fills kp [P][parts][3] and ks [P]; returns P.
+// People assembly from precomputed pair scores with the connectBodyPartsCpu
+// (bodyPartConnectorBase.cpp:1327-1377) or connectBodyPartsGpu (bodyPartConnectorBase.cu:147-250)
+// semantics.  peaks: [parts][max_peaks+1][3] host.  Fills kp [P][parts][3] and ks [P]; returns P.
 int assemble_people(const PoseModelInfo& model, const float* peaks, int max_peaks,
                     const PairScores& scores, const ConnectParams& p, std::vector<float>& kp,
                     std::vector<float>& ks);

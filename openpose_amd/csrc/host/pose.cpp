@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <string>
 
 #include "../../../include/opk.h"
 
@@ -27,13 +28,18 @@ double resize_scale_factor(int iw, int ih, int tw, int th)
     return rw < rh ? rw : rh;
 }
 
-PoseHip::PoseHip(Context* ctx, NetHip* net, bool maxpos)
-    : ctx_(ctx), net_(net), maximize_positives_(maxpos)
+PoseHip::PoseHip(Context* ctx, NetHip* net, bool maxpos, int pose_model_id, int semantics)
+    : ctx_(ctx), net_(net), maximize_positives_(maxpos), model_(pose_model_id), semantics_(semantics)
 {
-    // defaults: poseParameters.cpp:677-756 (BODY_25)
-    props_[OPK_PROP_NMS_THRESHOLD] = maxpos ? 0.02f : 0.05f;
+    const PoseModelInfo& m = pose_model(model_);   // throws for unknown models
+    OPK_CHECK_ARG(semantics == kConnectCpu || semantics == kConnectGpu, "unknown connector semantics");
+    if (semantics == kConnectCpu && !m.cpu_connector())   // bodyPartConnectorBase.cpp:165-167
+        throw Error(4, std::string("connectBodyPartsCpu supports BODY_25, COCO_18 and MPI_15 only (") +
+                           m.name + "): use the GPU-path connector semantics");
+    // defaults: poseParameters.cpp:677-756 (per model where they differ)
+    props_[OPK_PROP_NMS_THRESHOLD] = maxpos ? m.nms_th_maxpos : m.nms_th;
     props_[OPK_PROP_INTER_MIN_ABOVE_THRESHOLD] = maxpos ? 0.75f : 0.95f;
-    props_[OPK_PROP_INTER_THRESHOLD] = maxpos ? 0.01f : 0.05f;
+    props_[OPK_PROP_INTER_THRESHOLD] = maxpos ? m.inter_th_maxpos : m.inter_th;
     props_[OPK_PROP_MIN_SUBSET_CNT] = maxpos ? 2u : 3u;
     props_[OPK_PROP_MIN_SUBSET_SCORE] = maxpos ? 0.05f : 0.4f;
     if (ctx_->device >= 0) {
@@ -61,7 +67,7 @@ void PoseHip::set_property(int prop, double v)
 
 size_t PoseHip::record_floats() const
 {
-    const PoseModelInfo& m = pose_model(0);
+    const PoseModelInfo& m = pose_model(model_);
     return 1 + (size_t)m.npairs() * kMaxPeaks * kMaxPeaks;
 }
 
@@ -85,7 +91,7 @@ float* PoseHip::heatmaps(int shape[4])
 float* PoseHip::peaks(int shape[4]) const
 {
     OPK_CHECK_ARG(last_ >= 0, "no collected batch");
-    shape[0] = n_; shape[1] = pose_model(0).parts; shape[2] = kMaxPeaks + 1; shape[3] = 3;
+    shape[0] = n_; shape[1] = pose_model(model_).parts; shape[2] = kMaxPeaks + 1; shape[3] = 3;
     return static_cast<float*>(slots_[last_].peaks.ptr);
 }
 
@@ -116,7 +122,7 @@ void PoseHip::submit(const float* frames, int n, int net_h, int net_w, int prod_
 void PoseHip::submit_net_output(const float* net_out, int n, int oh, int ow, int net_h,
                                 int net_w, int prod_w, int prod_h)
 {
-    const PoseModelInfo& m = pose_model(0);
+    const PoseModelInfo& m = pose_model(model_);
     const int C = m.heat_channels();
     OPK_CHECK_ARG(net_out && n > 0 && oh > 0 && ow > 0, "empty net output");
     OPK_CHECK_ARG(count_ < 2, "two batches already in flight: collect first");
@@ -159,7 +165,7 @@ void PoseHip::submit_net_output(const float* net_out, int n, int oh, int ow, int
     const float inter_min = (float)props_[OPK_PROP_INTER_MIN_ABOVE_THRESHOLD];
     const double near = std::sqrt((double)(W * H)) / 150;
     const float reject = float(nms_th + 1e-6);   // defaultNmsThreshold = NMSThreshold (:325)
-    const auto& pt = ctx_->pose_table(0);
+    const auto& pt = ctx_->pose_table(model_);
     const size_t rf = record_floats();
     float* rec = static_cast<float*>(sl.records.get((size_t)n * rf * 4));
     launch_paf_scores_compact(rec, (int)rf, heat, peaks, n, kMaxPeaks, pt, inter_th, inter_min,
@@ -179,7 +185,7 @@ int PoseHip::collect()
     ctx_->bind();
     const int si = head_;
     Slot& sl = slots_[si];
-    const PoseModelInfo& m = pose_model(0);
+    const PoseModelInfo& m = pose_model(model_);
     const int n = sl.n;
     const size_t peak_floats = (size_t)m.parts * (kMaxPeaks + 1) * 3;
     const size_t rf = record_floats();
@@ -194,7 +200,7 @@ int PoseHip::collect()
     OPK_HIP(hipStreamSynchronize(copy_));
 
     ConnectParams cp{(int)props_[OPK_PROP_MIN_SUBSET_CNT], (float)props_[OPK_PROP_MIN_SUBSET_SCORE],
-                     sl.scale, maximize_positives_};
+                     sl.scale, maximize_positives_, semantics_};
     people_.assign(n, 0);
     kp_.assign(n, {});
     ks_.assign(n, {});

@@ -17,7 +17,9 @@ namespace opk {
 // forward() = submit + collect.
 class PoseHip {
 public:
-    PoseHip(Context* ctx, NetHip* net, bool maximize_positives);
+    // pose_model: PoseModel id (pose_model.h); semantics: kConnectCpu / kConnectGpu (connector.h)
+    PoseHip(Context* ctx, NetHip* net, bool maximize_positives, int pose_model = 0,
+            int semantics = kConnectCpu);
     ~PoseHip();
 
     void set_property(int prop, double v);
@@ -44,8 +46,9 @@ public:
     float* heatmaps(int shape[4]);
     float* peaks(int shape[4]) const;
     float scale_net_to_output() const { return scale_net_to_output_; }
+    int model() const { return model_; }
 
-    static constexpr int kMaxPeaks = kPoseMaxPeople;   // peaks blob [25][128][3]
+    static constexpr int kMaxPeaks = kPoseMaxPeople;   // peaks blob [parts][128][3]
     static constexpr int kRecordHead = 16384;          // record floats copied eagerly per frame
 
 private:
@@ -62,6 +65,7 @@ private:
     Context* ctx_;
     NetHip* net_;
     bool maximize_positives_;
+    int model_, semantics_;
     double props_[5];
     const float* overlay_ = nullptr;
     hipStream_t copy_ = nullptr;         // D2H of collected batches (overlaps the next batch)

@@ -18,8 +18,13 @@ BODY25_NUM_PAIRS = len(BODY25_PAIRS) // 2
 POSE_MAX_PEOPLE = 127
 NET_DECREASE_FACTOR = 8
 
-# PoseModel enum values (include/openpose/pose/enumClasses.hpp:9-30)
+# PoseModel enum values (include/openpose/pose/enumClasses.hpp:9-30); the tables of every model
+# are in libopk_hip (api.pose_model_info)
 BODY_25, COCO_18, MPI_15, MPI_15_4 = 0, 1, 2, 3
+BODY_25B, BODY_135 = 13, 14
+
+# connector semantics (include/opk.h): connectBodyPartsCpu / connectBodyPartsGpu assembly
+CONNECT_CPU, CONNECT_GPU = 0, 1
 
 # defaults (maximizePositives = false)
 NMS_THRESHOLD = 0.05

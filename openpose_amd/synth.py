@@ -37,13 +37,71 @@ def people(n, h, w, seed, min_height=0.35, max_height=0.9):
     return out
 
 
-def render_field(skeletons, h, w, sigma, paf_width, background=True):
-    """Render [78, h, w] float32 (BODY_25 net_output layout) from skeletons [n, 25, 2]."""
-    field = np.zeros((78, h, w), np.float32)
+BODY25_TABLE = dict(id=0, name="BODY_25", parts=25, bkg=True, pairs=list(BODY25_PAIRS),
+                    map_idx=list(BODY25_MAP_IDX))
+
+
+def tree_template(table):
+    """Unit-height skeleton [parts, 2] for any pose model: the parts laid out breadth-first along
+    the model's pair graph from part pairs[0] (fixed directions, shrinking steps).  Only the
+    topology matters for the synthetic workloads (the PAF of every pair runs from A to B)."""
+    P = table["parts"]
+    pairs = table["pairs"]
+    adj = [[] for _ in range(P)]
+    for q in range(len(pairs) // 2):
+        a, b = pairs[2 * q], pairs[2 * q + 1]
+        adj[a].append(b)
+        adj[b].append(a)
+    pos = np.full((P, 2), np.nan)
+    depth = np.zeros(P, np.int64)
+    order = [pairs[0]]
+    pos[pairs[0]] = (0.0, -0.3)
+    golden = np.pi * (3 - np.sqrt(5))
+    k = 0
+    while order:
+        nxt = []
+        for u in order:
+            for v in adj[u]:
+                if np.isnan(pos[v, 0]):
+                    k += 1
+                    depth[v] = depth[u] + 1
+                    step = 0.16 / np.sqrt(depth[v])
+                    th = golden * k
+                    pos[v] = pos[u] + step * np.array([np.cos(th), 0.6 * np.abs(np.sin(th)) + 0.2])
+                    nxt.append(v)
+        order = nxt
+    missing = np.isnan(pos[:, 0])   # parts outside every pair: spread below the root
+    pos[missing] = np.stack([np.linspace(-0.2, 0.2, missing.sum()), np.full(missing.sum(), 0.45)], 1) \
+        if missing.any() else pos[missing]
+    return pos
+
+
+def people_model(table, n, h, w, seed, min_height=0.35, max_height=0.9):
+    """n random skeletons [n, parts, 2] of any pose model (BODY_25: people())."""
+    if table["parts"] == 25 and list(table["pairs"]) == list(BODY25_PAIRS):
+        return people(n, h, w, seed, min_height, max_height)
+    tpl = tree_template(table)
+    rng = np.random.default_rng(seed)
+    out = np.zeros((n, table["parts"], 2), np.float64)
+    for p in range(n):
+        ph = h * rng.uniform(min_height, max_height) / max(1.0, np.sqrt(n) / 2)
+        cx = rng.uniform(0.1 * w, 0.9 * w)
+        cy = rng.uniform(0.3 * h, 0.7 * h)
+        out[p] = tpl * ph + (cx, cy) + rng.normal(0, ph * 0.01, tpl.shape)
+    return out
+
+
+def render_field(skeletons, h, w, sigma, paf_width, background=True, table=None):
+    """Render the net_output layout [parts + bkg + PAFs, h, w] float32 of a pose model (default
+    BODY_25: [78, h, w]) from skeletons [n, parts, 2]."""
+    t = table or BODY25_TABLE
+    P, npairs = t["parts"], len(t["pairs"]) // 2
+    base = P + (1 if t["bkg"] else 0)
+    field = np.zeros((base + len(t["map_idx"]), h, w), np.float32)
     yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
     rad = int(np.ceil(4 * sigma))
     for sk in skeletons:
-        for k in range(25):
+        for k in range(P):
             x, y = sk[k]
             x0, x1 = max(0, int(x) - rad), min(w, int(x) + rad + 2)
             y0, y1 = max(0, int(y) - rad), min(h, int(y) + rad + 2)
@@ -52,12 +110,12 @@ def render_field(skeletons, h, w, sigma, paf_width, background=True):
             d2 = (xx[y0:y1, x0:x1] - x) ** 2 + (yy[y0:y1, x0:x1] - y) ** 2
             g = np.exp(-d2 / (2 * sigma * sigma)).astype(np.float32)
             np.maximum(field[k, y0:y1, x0:x1], g, out=field[k, y0:y1, x0:x1])
-    if background:
-        field[25] = 1.0 - field[:25].max(axis=0)
-    count = np.zeros((26, h, w), np.float32)
+    if background and t["bkg"]:
+        field[P] = 1.0 - field[:P].max(axis=0)
+    count = np.zeros((npairs, h, w), np.float32)
     for sk in skeletons:
-        for q in range(26):
-            a, b = sk[BODY25_PAIRS[2 * q]], sk[BODY25_PAIRS[2 * q + 1]]
+        for q in range(npairs):
+            a, b = sk[t["pairs"][2 * q]], sk[t["pairs"][2 * q + 1]]
             v = b - a
             length = float(np.hypot(*v))
             if length < 1e-6:
@@ -74,21 +132,23 @@ def render_field(skeletons, h, w, sigma, paf_width, background=True):
             along = px * u[0] + py * u[1]
             across = np.abs(px * u[1] - py * u[0])
             m = (along >= 0) & (along <= length) & (across <= paf_width)
-            cx = 26 + BODY25_MAP_IDX[2 * q]
-            cy = 26 + BODY25_MAP_IDX[2 * q + 1]
+            cx = base + t["map_idx"][2 * q]
+            cy = base + t["map_idx"][2 * q + 1]
             field[cx, y0:y1, x0:x1][m] += u[0]
             field[cy, y0:y1, x0:x1][m] += u[1]
             count[q, y0:y1, x0:x1][m] += 1
-    for q in range(26):
+    for q in range(npairs):
         c = np.maximum(count[q], 1)
-        field[26 + BODY25_MAP_IDX[2 * q]] /= c
-        field[26 + BODY25_MAP_IDX[2 * q + 1]] /= c
+        field[base + t["map_idx"][2 * q]] /= c
+        field[base + t["map_idx"][2 * q + 1]] /= c
     return field
 
 
-def overlay(n_people, h, w, seed):
+def overlay(n_people, h, w, seed, table=None):
     """Net-output-resolution overlay: sigma 1 px Gaussians, 1 px PAF strips."""
-    return render_field(people(n_people, h, w, seed), h, w, sigma=1.0, paf_width=1.0)
+    t = table or BODY25_TABLE
+    return render_field(people_model(t, n_people, h, w, seed), h, w, sigma=1.0, paf_width=1.0,
+                        table=t)
 
 
 def fnv1a(name):

@@ -48,6 +48,11 @@ def lib():
         L.orc_connect_from_scores.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _f, _f, _i]
         L.orc_connect_gpu_semantics.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _f, _f,
                                                 _i]
+        _u32p = np.ctypeslib.ndpointer(np.uint32, flags="C_CONTIGUOUS")
+        L.orc_connect_gpu_tables.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _u32p, _i, _i,
+                                             _f, _f, _i]
+        L.orc_pair_scores.argtypes = [_f32p, _f32p, _f32p, _i, _u32p, _u32p, _u32p, _i, _i, _i, _f,
+                                      _f, _f]
         L.orc_conv2d.argtypes = [_f32p, _f32p, _f32p, _f32p, _i, _i, _i, _i, _i, _i, _i, _i]
         L.orc_prelu.argtypes = [_f32p, _f32p, _i, _i, _i]
         L.orc_relu.argtypes = [_f32p, ctypes.c_long]
@@ -68,6 +73,8 @@ def ref_lib():
         R = ctypes.CDLL(path, mode=os.RTLD_LAZY)  # OpenCV-only symbols stay unresolved
         R.ref_connect_cpu.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _i, _f, _f, _i,
                                       _f, _f, _f, _i]
+        R.ref_connect_gpu_assembly.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _f, _f,
+                                               _i]
         _REF = R
     return _REF
 
@@ -144,6 +151,59 @@ def connect_from_scores(pair_scores, peaks, gpu_semantics=False, **params):
            p["min_subset_cnt"], p["min_subset_score"], p["scale"], int(p["maximize_positives"]))
     n = min(n, p["max_people"])
     return kp[:n].copy(), ks[:n].copy()
+
+
+def pose_tables():
+    """Pose tables of every PoseModel as the reference computes them (tests/golden/pose_tables.json,
+    written by tools/gen_pose_tables.py from the reference's poseParameters.cpp)."""
+    import json
+    with open(os.path.join(_HERE, "..", "tests", "golden", "pose_tables.json")) as f:
+        return json.load(f)
+
+
+def connect_gpu_semantics(pair_scores, peaks, table, use_reference=False, **params):
+    """connectBodyPartsGpu host assembly for any model (table: a pose_tables() entry).  With
+    use_reference the reference's own pafVectorIntoPeopleVector / removePeople... run (None when
+    the input would reach getKeypointsRoi, which needs OpenCV)."""
+    p = _connect_args(params)
+    pair_scores = np.ascontiguousarray(pair_scores, np.float32)
+    peaks = np.ascontiguousarray(peaks, np.float32)
+    nparts = peaks.shape[0]
+    kp = np.zeros((p["max_people"], nparts, 3), np.float32)
+    ks = np.zeros(p["max_people"], np.float32)
+    if use_reference:
+        n = ref_lib().ref_connect_gpu_assembly(kp, ks, p["max_people"], pair_scores, peaks,
+                                               table["id"], peaks.shape[1] - 1, p["min_subset_cnt"],
+                                               p["min_subset_score"], p["scale"],
+                                               int(p["maximize_positives"]))
+        if n == -2:
+            return None
+    else:
+        pairs = np.asarray(table["pairs"], np.uint32)
+        n = lib().orc_connect_gpu_tables(kp, ks, p["max_people"], pair_scores, peaks, nparts,
+                                         len(pairs) // 2, pairs, peaks.shape[1] - 1,
+                                         p["min_subset_cnt"], p["min_subset_score"], p["scale"],
+                                         int(p["maximize_positives"]))
+    n = min(n, p["max_people"])
+    return kp[:n].copy(), ks[:n].copy()
+
+
+def pair_scores_table(heat, peaks, table, inter_th=0.05, inter_min_above=0.95, nms_th=0.05):
+    """Dense [npairs, maxPeaks, maxPeaks] getScoreAB table for any model (PAF channel of pair q:
+    parts + bkg + map_idx)."""
+    heat = np.ascontiguousarray(heat, np.float32)
+    peaks = np.ascontiguousarray(peaks, np.float32)
+    pairs = np.asarray(table["pairs"], np.uint32)
+    npairs = len(pairs) // 2
+    base = table["parts"] + (1 if table["bkg"] else 0)
+    mi = np.asarray(table["map_idx"], np.uint32)
+    mapx = np.ascontiguousarray(base + mi[0:2 * npairs:2], np.uint32)
+    mapy = np.ascontiguousarray(base + mi[1:2 * npairs:2], np.uint32)
+    mp = peaks.shape[1] - 1
+    out = np.zeros((npairs, mp, mp), np.float32)
+    lib().orc_pair_scores(out, heat, peaks, npairs, pairs, mapx, mapy, heat.shape[2],
+                          heat.shape[1], mp, inter_th, inter_min_above, nms_th)
+    return out
 
 
 def paf_score(a, b, mapx, mapy, inter_th=0.05, inter_min_above=0.95, nms_th=0.05):

@@ -453,4 +453,36 @@ int orc_connect_gpu_semantics(float* kp, float* ks, int max_people, const float*
     return write_people(kp, ks, max_people, people, valid, peaks, md.parts, md.pairs, scale);
 }
 
+int orc_connect_gpu_tables(float* kp, float* ks, int max_people, const float* pair_scores,
+                           const float* peaks, int parts, int npairs, const unsigned* pairs,
+                           int max_peaks, int min_cnt, float min_score, float scale, int maxpos)
+{
+    const Model md{parts, npairs, pairs, nullptr};
+    auto people = people_global_sort(peaks, md, max_peaks, pair_scores);
+    std::vector<int> valid;
+    int n = 0;
+    select_people(valid, n, people, md.parts, min_cnt, min_score, maxpos != 0, peaks);
+    return write_people(kp, ks, max_people, people, valid, peaks, md.parts, md.pairs, scale);
+}
+
+void orc_pair_scores(float* out, const float* heat, const float* peaks, int npairs,
+                     const unsigned* pairs, const unsigned* mapx, const unsigned* mapy, int W,
+                     int H, int max_peaks, float inter_th, float inter_min_above, float nms_th)
+{
+    const long area = (long)W * H;
+    const int stride = 3 * (max_peaks + 1);
+    for (int q = 0; q < npairs; ++q) {
+        const float* a0 = peaks + pairs[2 * q] * stride;
+        const float* b0 = peaks + pairs[2 * q + 1] * stride;
+        const int na = round_pos(a0[0]), nb = round_pos(b0[0]);
+        float* o = out + (long)q * max_peaks * max_peaks;
+        for (int i = 0; i < max_peaks * max_peaks; ++i) o[i] = 0.f;
+        for (int i = 0; i < na; ++i)
+            for (int j = 0; j < nb; ++j)
+                o[i * max_peaks + j] = score_ab(a0 + (i + 1) * 3, b0 + (j + 1) * 3,
+                                                heat + mapx[q] * area, heat + mapy[q] * area, W, H,
+                                                inter_th, inter_min_above, nms_th);
+    }
+}
+
 }  // extern "C"

@@ -76,6 +76,17 @@ int orc_connect_gpu_semantics(float* out_keypoints, float* out_scores, int max_p
                               const float* pair_scores, const float* peaks, int pose_model,
                               int max_peaks, int min_subset_cnt, float min_subset_score,
                               float scale_factor, int maximize_positives);
+/* same, for any model given its tables (BODY_135 and the other models the CPU path rejects);
+ * pairs: 2*npairs part indices (getPosePartPairs) */
+int orc_connect_gpu_tables(float* out_keypoints, float* out_scores, int max_people,
+                           const float* pair_scores, const float* peaks, int parts, int npairs,
+                           const unsigned* pairs, int max_peaks, int min_subset_cnt,
+                           float min_subset_score, float scale_factor, int maximize_positives);
+/* dense pair scores [npairs][max_peaks][max_peaks] via getScoreAB (0 where no peak); mapx/mapy:
+ * absolute heat channel of each pair's x/y PAF */
+void orc_pair_scores(float* out, const float* heat, const float* peaks, int npairs,
+                     const unsigned* pairs, const unsigned* mapx, const unsigned* mapy, int W,
+                     int H, int max_peaks, float inter_th, float inter_min_above, float nms_th);
 /* pose tables (poseParameters.cpp:253-256,413-419) */
 int orc_pose_num_parts(int pose_model);
 int orc_pose_num_pairs(int pose_model);

@@ -19,10 +19,14 @@
 // peopleVectorToPeopleArray, which this driver does not call; getKeypointsRoi only for >=135
 // parts).  The final people -> array step (bodyPartConnectorBase.cpp:886-934) is a 10-line
 // copy-out done here on the returned std::vector.
+#include <algorithm>
 #include <cstring>
+#include <functional>
+#include <tuple>
 #include <vector>
 #include <openpose/net/bodyPartConnectorBase.hpp>
 #include <openpose/pose/poseParameters.hpp>
+#include <openpose/utilities/fastMath.hpp>
 
 extern "C" int ref_connect_cpu(float* kp, float* ks, int max_people, const float* heat,
                                const float* peaks, int pose_model, int W, int H, int max_peaks,
@@ -57,4 +61,105 @@ extern "C" int ref_connect_cpu(float* kp, float* ks, int max_people, const float
         ks[o] = pr.second * inv;
     }
     return (int)valid.size();
+}
+
+// Pose tables of model `pose_model` as the reference computes them (poseParameters.cpp): writes
+// up to `cap` pair entries and map entries; returns the number of pair entries (2 per pair), or
+// -1 when a buffer is too small.  params: [0] parts, [1] bkg, [2] map entries, [3] NMS threshold,
+// [4] inter threshold, [5] NMS threshold (maximizePositives), [6] inter threshold (maxpos).
+extern "C" int ref_pose_table(int pose_model, unsigned* pairs, unsigned* map, int cap, float* params)
+{
+    const auto model = (op::PoseModel)pose_model;
+    const auto& p = op::getPosePartPairs(model);
+    const auto& m = op::getPoseMapIndex(model);
+    if ((int)p.size() > cap || (int)m.size() > cap) return -1;
+    std::memcpy(pairs, p.data(), p.size() * sizeof(unsigned));
+    std::memcpy(map, m.data(), m.size() * sizeof(unsigned));
+    params[0] = (float)op::getPoseNumberBodyParts(model);
+    params[1] = op::addBkgChannel(model) ? 1.f : 0.f;
+    params[2] = (float)m.size();
+    params[3] = op::getPoseDefaultNmsThreshold(model, false);
+    params[4] = op::getPoseDefaultConnectInterThreshold(model, false);
+    params[5] = op::getPoseDefaultNmsThreshold(model, true);
+    params[6] = op::getPoseDefaultConnectInterThreshold(model, true);
+    return (int)p.size();
+}
+
+// connectBodyPartsGpu's host half (bodyPartConnectorBase.cu:147-250) on host pair scores
+// [npairs][max_peaks][max_peaks]: the reference's pafVectorIntoPeopleVector,
+// removePeopleBelowThresholdsAndFillFaces and the people -> array copy-out.  pafPtrIntoVector takes
+// an op::Array (OpenCV-dependent array.cpp, not built), so its loop -- collect (total, paf, q, i, j)
+// for score > 1e-6 with total = paf + 0.1 sA + 0.1 sB, sort descending -- is restated here.
+// Returns -2 when the call would reach getKeypointsRoi (keypoint.cpp, not built): a >= 135-part
+// model with face-only fragments next to valid people; callers skip such inputs.
+extern "C" int ref_connect_gpu_assembly(float* kp, float* ks, int max_people,
+                                        const float* pair_scores, const float* peaks,
+                                        int pose_model, int max_peaks, int min_cnt,
+                                        float min_score, float scale, int maxpos)
+{
+    const auto model = (op::PoseModel)pose_model;
+    const auto& pairs = op::getPosePartPairs(model);
+    const auto nparts = op::getPoseNumberBodyParts(model);
+    const auto npairs = (unsigned)(pairs.size() / 2);
+    const int off = 3 * (max_peaks + 1);
+    std::vector<std::tuple<float, float, int, int, int>> conn;
+    for (unsigned q = 0; q < npairs; ++q) {
+        const int pa = (int)pairs[2 * q], pb = (int)pairs[2 * q + 1];
+        const int na = op::positiveIntRound(peaks[pa * off]);
+        const int nb = op::positiveIntRound(peaks[pb * off]);
+        for (int i = 0; i < na; ++i)
+            for (int j = 0; j < nb; ++j) {
+                const float s = pair_scores[((size_t)q * max_peaks + i) * max_peaks + j];
+                if (s > 1e-6)
+                    conn.emplace_back(s + 0.1f * peaks[pa * off + (i + 1) * 3 + 2] +
+                                          0.1f * peaks[pb * off + (j + 1) * 3 + 2],
+                                      s, (int)q, i + 1, j + 1);
+            }
+    }
+    std::sort(conn.begin(), conn.end(), std::greater<std::tuple<double, double, int, int, int>>());
+    auto people = op::pafVectorIntoPeopleVector<float>(conn, peaks, max_peaks, pairs, nparts);
+    if (nparts >= 135) {   // would removePeople... call getKeypointsRoi? (its counting, :740-798)
+        auto disc = [](int& c, const std::vector<int>& r, int a, int b, int minimum) {
+            int k = 0;
+            for (int i = a; i < b; ++i) k += r[i] > 0;
+            if (k > minimum) c += minimum - k;
+        };
+        std::function<bool(bool)> reaches = [&](bool mp) {
+            int valid = 0, face_valid = 0, face_invalid = 0;
+            for (const auto& p : people) {
+                int c = p.first.back();
+                const int before = c;
+                disc(c, p.first, 65, 135, 1);
+                if (c == 1) { ++face_invalid; continue; }
+                if (c != before) ++face_valid;
+                disc(c, p.first, 45, 65, 1);
+                disc(c, p.first, 25, 45, 1);
+                if (!mp) {
+                    const int b2 = c;
+                    disc(c, p.first, 19, 25, 0);
+                    if (c != b2 && c <= 4) continue;
+                }
+                if (c >= min_cnt && (p.second / c) >= min_score) ++valid;
+            }
+            if (valid > 0) return face_invalid > 0 && face_valid > 0;
+            return !mp && reaches(true);
+        };
+        if (reaches(maxpos != 0)) return -2;
+    }
+    std::vector<int> keep;
+    int npeople = 0;
+    op::removePeopleBelowThresholdsAndFillFaces<float>(keep, npeople, people, nparts, min_cnt,
+                                                       min_score, maxpos != 0, peaks);
+    const float inv = 1 / float(nparts + npairs);
+    for (int o = 0; o < (int)keep.size() && o < max_people; ++o) {
+        const auto& pr = people[keep[o]];
+        for (unsigned k = 0; k < nparts; ++k) {
+            float* d = kp + ((size_t)o * nparts + k) * 3;
+            const int s = pr.first[k];
+            if (s > 0) { d[0] = peaks[s - 2] * scale; d[1] = peaks[s - 1] * scale; d[2] = peaks[s]; }
+            else { d[0] = d[1] = d[2] = 0.f; }
+        }
+        ks[o] = pr.second * inv;
+    }
+    return (int)keep.size();
 }

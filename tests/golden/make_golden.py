@@ -62,6 +62,84 @@ def make_connector():
                             field_sha=sha(f), peaks=pk, keypoints=kp, scores=ks)
 
 
+# connectBodyPartsGpu host assembly (GPU semantics), any model: (name, model, kind, n, seed, h, w,
+# maximize_positives).  kind "people": synthetic field -> oracle NMS -> oracle pair scores;
+# "random": random peaks and random pair scores (many merges and fragments).  BODY_135 cases blank
+# the face parts ("_noface"): with face-only fragments next to valid people the reference calls
+# getKeypointsRoi (utilities/keypoint.cpp, needs OpenCV: not built), so the face-fragment merge is
+# checked oracle-vs-product only (tests/test_connector_gpu.py, parity unpinned).
+GPU_CONNECTOR_CASES = [
+    ("b25_p5", 0, "people", 5, 111, 368, 656, False),
+    ("b25_p20", 0, "people", 20, 112, 368, 656, False),
+    ("b25_random", 0, "random", 0, 113, 368, 656, False),
+    ("b135_p3", 14, "people_noface", 3, 114, 184, 328, False),
+    ("b135_p8", 14, "people_noface", 8, 115, 368, 656, False),
+    ("b135_p8_maxpos", 14, "people_noface", 8, 116, 368, 656, True),
+    ("b135_random", 14, "random_noface", 0, 117, 184, 328, False),
+    ("b25b_p6", 13, "people", 6, 118, 184, 328, False),
+]
+
+
+def gpu_connector_inputs(table, kind, n, seed, h, w):
+    """(peaks [parts,128,3], dense pair scores [npairs,127,127]) of one GPU-connector case.
+    kind "people_noface": BODY_135 people whose face heat maps are blanked (no face peaks)."""
+    if kind.startswith("people"):
+        t = table
+        sk = synth.people_model(t, n, h, w, seed)
+        sc = h / 368.0
+        f = synth.render_field(sk, h, w, sigma=max(1.0, 7.0 * sc), paf_width=max(1.0, 6.0 * sc),
+                               table=t)
+        if kind == "people_noface":
+            f[65:t["parts"]] = 0
+        scale = 1.959128
+        off = np.float32(0.5 / scale)
+        pk = oracle.nms(f, 0.05, 128, (off, off), channels=t["parts"])
+        return pk, oracle.pair_scores_table(f, pk, t)
+    rng = np.random.default_rng(seed)
+    P, npairs = table["parts"], len(table["pairs"]) // 2
+    pk = np.zeros((P, 128, 3), np.float32)
+    for k in range(P):
+        c = 0 if (kind == "random_noface" and k >= 65) else int(rng.integers(0, 5))
+        pk[k, 0, 0] = c
+        pk[k, 1:c + 1, 0] = rng.uniform(0, w, c)
+        pk[k, 1:c + 1, 1] = rng.uniform(0, h, c)
+        pk[k, 1:c + 1, 2] = rng.uniform(0.05, 1.0, c)
+    ps = np.zeros((npairs, 127, 127), np.float32)
+    for q in range(npairs):
+        na, nb = int(pk[table["pairs"][2 * q], 0, 0]), int(pk[table["pairs"][2 * q + 1], 0, 0])
+        v = rng.uniform(-0.5, 1.0, (na, nb)).astype(np.float32)
+        ps[q, :na, :nb] = np.where(v > 0.2, v, 0)
+    return pk, ps
+
+
+def sparse_scores(ps):
+    q, i, j = np.nonzero(ps)
+    return np.stack([q, i, j], 1).astype(np.int16), ps[q, i, j].astype(np.float32)
+
+
+def dense_scores(idx, val, npairs):
+    ps = np.zeros((npairs, 127, 127), np.float32)
+    ps[idx[:, 0], idx[:, 1], idx[:, 2]] = val
+    return ps
+
+
+def make_connector_gpu():
+    assert oracle.ref_lib() is not None, "needs /root/reference (oracle/_ref)"
+    tables = oracle.pose_tables()
+    for name, model, kind, n, seed, h, w, maxpos in GPU_CONNECTOR_CASES:
+        t = tables[model]
+        pk, ps = gpu_connector_inputs(t, kind, n, seed, h, w)
+        res = oracle.connect_gpu_semantics(ps, pk, t, use_reference=True, scale=1.959128,
+                                           maximize_positives=maxpos)
+        assert res is not None, name + ": reaches getKeypointsRoi (needs OpenCV); pick another seed"
+        idx, val = sparse_scores(ps)
+        np.savez_compressed(os.path.join(HERE, "gpuconn_%s.npz" % name), model=model, kind=kind,
+                            n_people=n, seed=seed, h=h, w=w, maximize_positives=maxpos,
+                            scale=1.959128, peaks=pk, score_idx=idx, score_val=val,
+                            npairs=len(t["pairs"]) // 2, keypoints=res[0], scores=res[1])
+        print(name, "peaks", int(pk[:, 0, 0].sum()), "scores", len(val), "people", len(res[1]))
+
+
 def make_nms():
     cases = {"people": people_field(5, 92, 164, 201),
              "noise": noise_field(78, 40, 56, 202, levels=5, density=0.8),
@@ -91,7 +169,12 @@ def make_cnn():
 
 
 if __name__ == "__main__":
+    if len(sys.argv) > 1:
+        for name in sys.argv[1:]:
+            globals()["make_" + name]()
+        sys.exit(0)
     make_connector()
+    make_connector_gpu()
     make_nms()
     make_resize()
     make_cnn()

@@ -18,6 +18,7 @@ import oracle
 from oracle import body25
 from openpose_amd import synth
 from openpose_amd.api import Net, PoseExtractor
+from openpose_amd.pose_tables import BODY_135, CONNECT_GPU
 from tests.golden.make_golden import connector_field
 
 pytestmark = pytest.mark.gpu
@@ -156,3 +157,63 @@ def test_pose_submit_collect_pipeline(ctx):
             np.testing.assert_array_equal(kp, r[k][0])
             np.testing.assert_array_equal(ks, r[k][1])
     assert pipe.pending() == 0
+
+
+GPU_CONN = sorted(glob.glob(os.path.join(GOLDEN, "gpuconn_*.npz")))
+
+
+@pytest.mark.parametrize("path", GPU_CONN, ids=lambda p: os.path.basename(p))
+def test_gpu_connector_gpu_semantics_matches_reference_fixture(ctx, path):
+    """connectBodyPartsGpu semantics (any model): GPU NMS + GPU PAF integrals + global-sort
+    assembly reproduce the reference's own outputs (random-score fixtures: CPU tests only)."""
+    g = np.load(path, allow_pickle=False)
+    kind = str(g["kind"])
+    if not kind.startswith("people"):
+        pytest.skip("random pair scores have no heat map")
+    t = oracle.pose_tables()[int(g["model"])]
+    h, w = int(g["h"]), int(g["w"])
+    sk = synth.people_model(t, int(g["n_people"]), h, w, int(g["seed"]))
+    sc = h / 368.0
+    f = synth.render_field(sk, h, w, sigma=max(1.0, 7.0 * sc), paf_width=max(1.0, 6.0 * sc), table=t)
+    if kind == "people_noface":
+        f[65:t["parts"]] = 0
+    scale = float(g["scale"])
+    off = float(np.float32(0.5 / scale))
+    peaks = torch.zeros((1, t["parts"], 128, 3), device="cuda")
+    heat = _dev(f[None])
+    ctx.nms(peaks, heat, 0.05, (off, off))
+    np.testing.assert_array_equal(peaks.cpu().numpy()[0], g["peaks"])
+    kp, ks = ctx.connect_body_parts(heat, peaks, pose_model=int(g["model"]), scale=scale,
+                                    maximize_positives=bool(g["maximize_positives"]),
+                                    semantics=CONNECT_GPU)
+    np.testing.assert_array_equal(kp, g["keypoints"])
+    np.testing.assert_array_equal(ks, g["scores"])
+
+
+@pytest.mark.parametrize("model,people", [(BODY_135, 20), (0, 5)])
+def test_pose_injection_gpu_semantics(ctx, model, people):
+    """BODY_135 through the poseNetOutput injection path -- 439 x 46 x 82
+    net output, 20 synthetic people, GPU-path connector -- bit-exact against the oracle chain
+    (resize -> NMS -> getScoreAB table -> global-sort assembly); BODY_25 with the same semantics."""
+    t = oracle.pose_tables()[model]
+    C = t["parts"] + int(t["bkg"]) + len(t["map_idx"])
+    fields = np.stack([synth.overlay(people, 46, 82, seed=1500 + k, table=t) +
+                       np.random.default_rng(k).normal(0, 0.01, (C, 46, 82)).astype(np.float32)
+                       for k in range(2)]).astype(np.float32)
+    pose = PoseExtractor(ctx, None, pose_model=model, semantics=CONNECT_GPU)
+    net_out = _dev(fields)
+    pose.forward_net_output(net_out, (656, 368), (1280, 720))
+    s = pose.scale_net_to_output()
+    off = float(np.float32(0.5 / np.float64(s)))
+    gpu_peaks = pose.peaks_numpy()
+    assert gpu_peaks.shape == (2, t["parts"], 128, 3)
+    for k in range(2):
+        heat = oracle.resize_merge([fields[k]], 368, 656)
+        peaks = oracle.nms(heat, 0.05, 128, (off, off), channels=t["parts"])
+        np.testing.assert_array_equal(gpu_peaks[k], peaks)
+        ps = oracle.pair_scores_table(heat, peaks, t)
+        rk, rs = oracle.connect_gpu_semantics(ps, peaks, t, scale=s)
+        kp, ks = pose.keypoints(k)
+        assert len(kp) >= 1
+        np.testing.assert_array_equal(kp, rk)
+        np.testing.assert_array_equal(ks, rs)
