@@ -209,6 +209,14 @@ int opk_pose_submit(opk_pose* pose, const float* frames_dev, int n, int net_h, i
 int opk_pose_submit_net_output(opk_pose* pose, const float* net_output_dev, int n, int out_h,
                                int out_w, int net_h, int net_w, int producer_w, int producer_h);
 int opk_pose_collect(opk_pose* pose, int* frames);
+/* Multi-scale (--scale_number > 1; poseExtractorCaffe.cpp:240-245 runs the net once per scale,
+ * resizeAndMergeCpu averages the x8 resizes of every scale's output, resizeAndMergeBase.cpp:55-106):
+ * frames_dev[i] = [n][3][net_hw[2i]][net_hw[2i+1]] net input of scale i (the reference's
+ * inputNetData[i]); scale 0 sets the heat-map size and scaleNetToOutput.  1..8 scales. */
+int opk_pose_submit_multi(opk_pose* pose, const float* const* frames_dev, const int* net_hw,
+                          int num_scales, int n, int producer_w, int producer_h);
+int opk_pose_forward_multi(opk_pose* pose, const float* const* frames_dev, const int* net_hw,
+                           int num_scales, int n, int producer_w, int producer_h);
 int opk_pose_pending(opk_pose* pose);   /* batches in flight, -1 for NULL */
 /* optional additive overlay on the net output before resize (synthetic-people workloads):
  * [n][78][out_h][out_w] device fp32, NULL to disable */

@@ -62,6 +62,8 @@ _SIGS = {
     "opk_pose_submit": (_i, [_p, _p, _i, _i, _i, _i, _i]),
     "opk_pose_submit_net_output": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i]),
     "opk_pose_collect": (_i, [_p, _ip]),
+    "opk_pose_submit_multi": (_i, [_p, _c.POINTER(_p), _ip, _i, _i, _i, _i]),
+    "opk_pose_forward_multi": (_i, [_p, _c.POINTER(_p), _ip, _i, _i, _i, _i]),
     "opk_pose_pending": (_i, [_p]),
     "opk_pose_num_people": (_i, [_p, _i]),
     "opk_pose_keypoints": (_i, [_p, _i, _p, _p, _i]),

@@ -275,6 +275,21 @@ class PoseExtractor:
         check(self.L.opk_pose_forward(self.h, _ptr(frames), n, h, w, producer_size[0],
                                       producer_size[1]))
 
+    def _multi(self, fn, frames, producer_size):
+        n = frames[0].shape[0]
+        ptrs = (ctypes.c_void_p * len(frames))(*[f.data_ptr() for f in frames])
+        for f in frames:
+            assert f.is_cuda and f.is_contiguous() and f.shape[0] == n
+        hw = (ctypes.c_int * (2 * len(frames)))(*[v for f in frames for v in f.shape[2:]])
+        check(fn(self.h, ptrs, hw, len(frames), n, producer_size[0], producer_size[1]))
+
+    def forward_multi(self, frames, producer_size):
+        """Multi-scale: frames = list of [n,3,h_i,w_i] net inputs, scale 0 first."""
+        self._multi(self.L.opk_pose_forward_multi, frames, producer_size)
+
+    def submit_multi(self, frames, producer_size):
+        self._multi(self.L.opk_pose_submit_multi, frames, producer_size)
+
     def forward_net_output(self, net_output, net_size, producer_size):
         """net_output: [n, heat_channels, h, w] CUDA tensor (or (ptr, shape)); net_size = (w, h)."""
         if isinstance(net_output, tuple):

@@ -184,6 +184,26 @@ int opk_pose_submit(opk_pose* p, const float* frames, int n, int net_h, int net_
     });
 }
 
+int opk_pose_submit_multi(opk_pose* p, const float* const* frames, const int* net_hw, int nscales,
+                          int n, int pw, int ph)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->submit_multi(frames, net_hw, nscales, n, pw, ph);
+    });
+}
+
+int opk_pose_forward_multi(opk_pose* p, const float* const* frames, const int* net_hw,
+                           int nscales, int n, int pw, int ph)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        OPK_CHECK_ARG(p->pose->pending() == 0, "batches in flight: collect them first");
+        p->pose->submit_multi(frames, net_hw, nscales, n, pw, ph);
+        p->pose->collect();
+    });
+}
+
 int opk_pose_submit_net_output(opk_pose* p, const float* out, int n, int oh, int ow, int net_h,
                                int net_w, int pw, int ph)
 {

@@ -278,7 +278,8 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
     OPK_HIP(hipMemcpyAsync(ds, sl.data(), sl.size() * 4, hipMemcpyHostToDevice, ctx_->stream));
     OPK_HIP(hipStreamSynchronize(ctx_->stream));
     c.loaded = true;
-    n_ = 0;   // re-derive launch arguments
+    shapes_.clear();   // re-derive launch arguments
+    cur_ = nullptr;
 }
 
 bool NetHip::ready() const
@@ -302,8 +303,18 @@ double NetHip::flops_per_frame(int h, int w) const
     return f;
 }
 
-void NetHip::reshape(int n, int h, int w)
+NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
 {
+    for (auto& sp : shapes_)
+        if (sp->n == n && sp->h == h && sp->w == w) return sp.get();
+    if ((int)shapes_.size() >= kMaxShapes) shapes_.erase(shapes_.begin());
+    shapes_.push_back(std::make_unique<ShapePlan>());
+    ShapePlan& S = *shapes_.back();
+    S.n = n;
+    S.h = h;
+    S.w = w;
+    std::vector<int>& lh_ = S.lh;
+    std::vector<int>& lw_ = S.lw;
     lh_.assign(nlevels_, 0);
     lw_.assign(nlevels_, 0);
     lh_[0] = h;
@@ -312,18 +323,17 @@ void NetHip::reshape(int n, int h, int w)
         lh_[l] = (lh_[l - 1] - 2 + 1) / 2 + 1;
         lw_[l] = (lw_[l - 1] - 2 + 1) / 2 + 1;
     }
-    mem_.clear();
-    std::vector<uint16_t*>& ptr = base_;
+    std::vector<uint16_t*>& ptr = S.base;
     ptr.assign(bufs_.size(), nullptr);
     {
         const char* e = std::getenv("OPK_CONV1_FUSED");   // dev A/B switch: 0 disables the fusion
-        fused1_active_ = fuse1_.a >= 0 && !conv_v1_ && !(e && e[0] == '0') &&
-                         conv1_fused_supported(h, w, 64, 64);
+        S.fused1 = fuse1_.a >= 0 && !conv_v1_ && !(e && e[0] == '0') &&
+                   conv1_fused_supported(h, w, 64, 64);
     }
     for (size_t i = 0; i < bufs_.size(); ++i) {
-        mem_.push_back(std::make_unique<DevBuf>());
+        S.mem.push_back(std::make_unique<DevBuf>());
         if ((int)i == image_buf_ && !conv_v1_) continue;   // conv_image reads the NCHW input itself
-        if (fused1_active_ && ((int)i == fuse1_.abuf || (int)i == fuse1_.bbuf))
+        if (S.fused1 && ((int)i == fuse1_.abuf || (int)i == fuse1_.bbuf))
             continue;   // conv1_1 / conv1_2 outputs live only inside conv1_fused_kernel
         // zeroed guards: the kernels read up to W+3 positions before the first frame and up to
         // kConvGuardTail positions after the last one (conv.h)
@@ -332,18 +342,20 @@ void NetHip::reshape(int n, int h, int w)
         const size_t pos = head + (size_t)n * (lh_[L] + 2) * (lw_[L] + 2) + kConvGuardTail;
         const size_t bytes = pos * bufs_[i].cs * 2;
         OPK_CHECK_ARG(pos * bufs_[i].cs < (size_t)1 << 31, "activation buffer exceeds 2^31 elements");
-        uint16_t* raw = static_cast<uint16_t*>(mem_.back()->get(bytes));
+        uint16_t* raw = static_cast<uint16_t*>(S.mem.back()->get(bytes));
         OPK_HIP(hipMemsetAsync(raw, 0, bytes, ctx_->stream));
         ptr[i] = raw + head * bufs_[i].cs;
     }
     const char* e3 = std::getenv("OPK_CONV3");   // dev A/B switch: OPK_CONV3=0 disables the halo kernel
     const bool allow3 = !conv_v1_ && !(e3 && e3[0] == '0');
     const size_t out_bytes = (size_t)n * out_c_ * lh_[out_level_] * lw_[out_level_] * 4;
-    out32_ = static_cast<float*>(out_mem_.get(out_bytes));
+    S.out32 = static_cast<float*>(S.out_mem.get(out_bytes));
     void* sink = sink_.get(kConv3SinkBytes);
-    for (auto& c : convs_) {
-        ConvArgs& a = c.args;
-        a = ConvArgs{};
+    S.args.assign(convs_.size(), ConvArgs{});
+    S.use3.assign(convs_.size(), 0);
+    for (size_t ci = 0; ci < convs_.size(); ++ci) {
+        const ConvPlan& c = convs_[ci];
+        ConvArgs& a = S.args[ci];
         const int H = lh_[c.level], W = lw_[c.level], Wp = W + 2;
         a.in = ptr[c.in.buf];
         a.in_cs = bufs_[c.in.buf].cs;
@@ -355,15 +367,16 @@ void NetHip::reshape(int n, int h, int w)
         else
             a.tapoff[0] = Wp + 1;
         a.ksteps = c.ksteps;
-        c.use3 = allow3 && !c.from_image && c.w3.ptr != nullptr;
-        if (c.use3) {
+        const bool use3 = allow3 && !c.from_image && c.w3.ptr != nullptr;
+        S.use3[ci] = use3;
+        if (use3) {
             const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, c.info.k);
             a.sw = s3.sw;
             a.nstrips = s3.nstrips;
             a.sink = sink;
             a.cus = cus_;
         }
-        a.w = static_cast<const uint16_t*>(c.use3 ? c.w3.ptr : c.w.ptr);
+        a.w = static_cast<const uint16_t*>(use3 ? c.w3.ptr : c.w.ptr);
         a.bias = static_cast<const float*>(c.bias.ptr);
         a.slope = static_cast<const float*>(c.slope.ptr);
         a.act = c.info.act;
@@ -380,14 +393,12 @@ void NetHip::reshape(int n, int h, int w)
         }
         if (c.out32_coff >= 0) {
             OPK_CHECK_ARG(c.level == out_level_, c.info.name + ": output at another resolution");
-            a.out32 = out32_;
+            a.out32 = S.out32;
             a.out32_c = out_c_;
             a.out32_coff = c.out32_coff;
         }
     }
-    n_ = n;
-    h_ = h;
-    w_ = w;
+    return &S;
 }
 
 void NetHip::forward(const float* input, int n, int h, int w)
@@ -395,11 +406,14 @@ void NetHip::forward(const float* input, int n, int h, int w)
     OPK_CHECK_ARG(input && n > 0 && h > 0 && w > 0, "empty input");
     OPK_CHECK_ARG(ready(), "weights not loaded for every convolution");
     ctx_->bind();
-    if (n != n_ || h != h_ || w != w_) reshape(n, h, w);
-    const std::vector<uint16_t*>& ptr = base_;
+    ShapePlan& S = *shape_plan(n, h, w);
+    cur_ = &S;
+    const std::vector<uint16_t*>& ptr = S.base;
+    const std::vector<int>& lh_ = S.lh;
+    const std::vector<int>& lw_ = S.lw;
     if (conv_v1_) launch_im2col3(ptr[image_buf_], input, n, h, w, ctx_->stream);
     size_t first = 0;
-    if (fused1_active_) {
+    if (S.fused1) {
         const ConvPlan& a = convs_[fuse1_.a];
         const ConvPlan& b = convs_[fuse1_.b];
         const PoolPlan& p = pools_[fuse1_.p];
@@ -428,10 +442,11 @@ void NetHip::forward(const float* input, int n, int h, int w)
         const Step& s = steps_[si];
         if (s.conv) {
             const ConvPlan& c = convs_[s.idx];
-            if (conv_v1_) launch_conv(c.args, c.bn > 128 ? 128 : c.bn, ctx_->stream);
-            else if (c.from_image) launch_conv_image(c.args, input, ctx_->stream);
-            else if (c.use3) launch_conv3(c.args, ctx_->stream);
-            else launch_conv2(c.args, c.bn, ctx_->stream);
+            const ConvArgs& a = S.args[s.idx];
+            if (conv_v1_) launch_conv(a, c.bn > 128 ? 128 : c.bn, ctx_->stream);
+            else if (c.from_image) launch_conv_image(a, input, ctx_->stream);
+            else if (S.use3[s.idx]) launch_conv3(a, ctx_->stream);
+            else launch_conv2(a, c.bn, ctx_->stream);
         } else {
             const PoolPlan& p = pools_[s.idx];
             const int L = p.level_in;

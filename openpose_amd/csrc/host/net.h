@@ -23,13 +23,18 @@ public:
     void set_conv(const std::string& name, const float* w, const float* b, const float* slope);
     bool ready() const;
 
-    // input: device NCHW fp32 [n][3][h][w]
+    // input: device NCHW fp32 [n][3][h][w].  Every input shape gets its own plan (activation
+    // buffers with zeroed guards, launch arguments, net output), kept across forwards, so the
+    // scales of a multi-scale pass alternate without re-planning and their outputs coexist.
     void forward(const float* input, int n, int h, int w);
-    float* output() const { return out32_; }
+    // net output of the last forward ([n][out_channels][out_h][out_w] fp32, stays valid until
+    // set_conv or until more than kMaxShapes other shapes have been planned)
+    float* output() const { return cur_ ? cur_->out32 : nullptr; }
     int out_channels() const { return out_c_; }
-    int out_h() const { return lh_.empty() ? 0 : lh_[out_level_]; }
-    int out_w() const { return lw_.empty() ? 0 : lw_[out_level_]; }
-    int frames() const { return n_; }
+    int out_h() const { return cur_ ? cur_->lh[out_level_] : 0; }
+    int out_w() const { return cur_ ? cur_->lw[out_level_] : 0; }
+    int frames() const { return cur_ ? cur_->n : 0; }
+    static constexpr int kMaxShapes = 8;
     double flops_per_frame(int h, int w) const;   // useful (unpadded) conv FLOPs
 
 private:
@@ -46,15 +51,26 @@ private:
         int out32_coff = -1;
         DevBuf w, bias, slope;
         DevBuf w3;            // halo-kernel weight layout (3x3 convs)
-        bool use3 = false;    // launch conv3 (decided per input shape)
         bool loaded = false;
-        ConvArgs args{};
     };
     struct PoolPlan { int in_buf, out_buf, level_in, channels; };
     struct Step { bool conv; int idx; };
 
+    // shape-dependent state of one input shape
+    struct ShapePlan {
+        int n = 0, h = 0, w = 0;
+        std::vector<int> lh, lw;
+        std::vector<std::unique_ptr<DevBuf>> mem;
+        std::vector<uint16_t*> base;   // first position of each buffer (past its head guard)
+        DevBuf out_mem;
+        float* out32 = nullptr;
+        bool fused1 = false;           // conv1_fused_kernel runs for this shape
+        std::vector<ConvArgs> args;    // per conv
+        std::vector<char> use3;        // per conv: launch conv3
+    };
+
     void plan(const std::vector<LayerDesc>& layers);
-    void reshape(int n, int h, int w);
+    ShapePlan* shape_plan(int n, int h, int w);
 
     Context* ctx_;
     std::string output_blob_;
@@ -69,17 +85,11 @@ private:
     bool conv_v1_ = false;
     struct Fuse1 { int a = -1, b = -1, p = -1, abuf = -1, bbuf = -1; };
     Fuse1 fuse1_;                 // conv1_1 -> conv1_2 -> pool1 (conv1_fused.hip) when planned
-    bool fused1_active_ = false;  // ... and the input shape allows it
     int cus_ = 256;               // compute units (persistent-kernel grid)
 
-    // shape-dependent state
-    int n_ = 0, h_ = 0, w_ = 0;
-    std::vector<int> lh_, lw_;
-    std::vector<std::unique_ptr<DevBuf>> mem_;
-    std::vector<uint16_t*> base_;   // first position of each buffer (past its head guard)
-    DevBuf out_mem_;
+    std::vector<std::unique_ptr<ShapePlan>> shapes_;   // oldest first
+    ShapePlan* cur_ = nullptr;    // shape of the last forward
     DevBuf sink_;                 // persistent conv3: target of masked-off stores
-    float* out32_ = nullptr;
 };
 
 }  // namespace opk

@@ -119,31 +119,64 @@ void PoseHip::submit(const float* frames, int n, int net_h, int net_w, int prod_
                       prod_h);
 }
 
+void PoseHip::submit_multi(const float* const* frames, const int* net_hw, int nscales, int n,
+                           int prod_w, int prod_h)
+{
+    OPK_CHECK_ARG(net_ != nullptr, "no network: multi-scale needs the net");
+    OPK_CHECK_ARG(frames && net_hw && nscales >= 1 && nscales <= kMaxResizeSources,
+                  "1..8 scales");
+    OPK_CHECK_ARG(count_ < 2, "two batches already in flight: collect first");
+    // one net pass per scale (poseExtractorCaffe.cpp:240-245); every input shape keeps its own
+    // plan and output buffer in NetHip, so the outputs coexist until the merge reads them
+    std::vector<NetOutput> outs(nscales);
+    for (int i = 0; i < nscales; ++i) {
+        OPK_CHECK_ARG(frames[i] != nullptr, "NULL scale input");
+        net_->forward(frames[i], n, net_hw[2 * i], net_hw[2 * i + 1]);
+        outs[i] = NetOutput{net_->output(), net_->out_h(), net_->out_w()};
+    }
+    submit_outputs(outs.data(), nscales, n, net_hw[0], net_hw[1], prod_w, prod_h);
+}
+
 void PoseHip::submit_net_output(const float* net_out, int n, int oh, int ow, int net_h,
                                 int net_w, int prod_w, int prod_h)
 {
+    const NetOutput o{net_out, oh, ow};
+    submit_outputs(&o, 1, n, net_h, net_w, prod_w, prod_h);
+}
+
+void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_h, int net_w,
+                             int prod_w, int prod_h)
+{
     const PoseModelInfo& m = pose_model(model_);
     const int C = m.heat_channels();
-    OPK_CHECK_ARG(net_out && n > 0 && oh > 0 && ow > 0, "empty net output");
+    OPK_CHECK_ARG(n > 0 && nscales >= 1 && nscales <= kMaxResizeSources, "bad batch");
+    for (int i = 0; i < nscales; ++i)
+        OPK_CHECK_ARG(outs[i].ptr && outs[i].h > 0 && outs[i].w > 0, "empty net output");
     OPK_CHECK_ARG(count_ < 2, "two batches already in flight: collect first");
     ctx_->bind();
     hipStream_t s = ctx_->stream;
     Slot& sl = slots_[(head_ + count_) & 1];
-    const size_t out_elems = (size_t)n * C * oh * ow;
-    if (overlay_) launch_add_inplace(const_cast<float*>(net_out), overlay_, out_elems, s);
+    if (overlay_) {   // synthetic people on the first scale's output
+        const size_t out_elems = (size_t)n * C * outs[0].h * outs[0].w;
+        launch_add_inplace(const_cast<float*>(outs[0].ptr), overlay_, out_elems, s);
+    }
 
-    // 1. resize x8 (ResizeAndMergeCaffe::Reshape: (h*8 - 1)*1 + 1), evaluated lazily: NMS and
-    //    the PAF scorer compute the resized values they touch with resize.hip's arithmetic
-    //    (bit-identical), so the 75 MB/frame heat-map stack is only written if requested
-    const int H = oh * 8, W = ow * 8;
-    const auto& t = ctx_->tables(oh, ow, H, W);
+    // 1. resize x8 of the first scale's size (ResizeAndMergeCaffe::Reshape: (h*8 - 1)*1 + 1) and
+    //    average of the scales (resizeAndMergeBase.cpp:55-106), evaluated lazily: NMS and the PAF
+    //    scorer compute the merged values they touch with resize.hip's arithmetic (bit-identical),
+    //    so the 75 MB/frame heat-map stack is only written if requested
+    const int H = outs[0].h * 8, W = outs[0].w * 8;
     HeatMap heat{};
     heat.channels = C;
     heat.h = H;
     heat.w = W;
-    heat.nsrc = 1;
-    heat.inv_n = 1.f;
-    heat.src[0] = ResizeSource{net_out, oh, ow, t.yofs, t.ycoef, t.xofs, t.xcoef};
+    heat.nsrc = nscales;
+    heat.inv_n = (float)(1. / (double)nscales);
+    for (int i = 0; i < nscales; ++i) {
+        const auto& t = ctx_->tables(outs[i].h, outs[i].w, H, W);
+        heat.src[i] = ResizeSource{outs[i].ptr, outs[i].h, outs[i].w, t.yofs, t.ycoef, t.xofs,
+                                   t.xcoef};
+    }
 
     // 2. scale net -> output (poseExtractorCaffe.cpp:281-310), net output size == net input size
     const double sp = resize_scale_factor(prod_w, prod_h, net_w, net_h);

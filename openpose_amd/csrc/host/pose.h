@@ -32,6 +32,10 @@ public:
     void submit(const float* frames, int n, int net_h, int net_w, int prod_w, int prod_h);
     void submit_net_output(const float* net_out, int n, int out_h, int out_w, int net_h,
                            int net_w, int prod_w, int prod_h);
+    // multi-scale (poseExtractorCaffe.cpp:240-245, resizeAndMergeBase.cpp:55-106): frames[i] is
+    // the [n][3][net_hw[2i]][net_hw[2i+1]] net input of scale i; scale 0 sets the heat-map size
+    void submit_multi(const float* const* frames, const int* net_hw, int nscales, int n,
+                      int prod_w, int prod_h);
     int collect();                       // frames of the collected batch
     int pending() const { return count_; }
 
@@ -60,6 +64,12 @@ private:
         float scale = 1.f;
         HeatMap heat{};
     };
+    struct NetOutput {
+        const float* ptr;
+        int h, w;
+    };
+    void submit_outputs(const NetOutput* outs, int nscales, int n, int net_h, int net_w,
+                        int prod_w, int prod_h);
     size_t record_floats() const;        // per frame: 1 + every candidate pair of the model
 
     Context* ctx_;

@@ -217,3 +217,42 @@ def test_pose_injection_gpu_semantics(ctx, model, people):
         assert len(kp) >= 1
         np.testing.assert_array_equal(kp, rk)
         np.testing.assert_array_equal(ks, rs)
+
+
+def test_multiscale_config4_bitexact(ctx):
+    """four scales (nets 656x368, 480x272, 320x176, 160x80) through
+    opk_pose_forward_multi: the merged heat maps (resizeAndMergeCpu average of the x8 cubic
+    resizes), peaks and people are bit-identical to the oracle chain fed with the same per-scale
+    net outputs."""
+    sizes = [(368, 656), (272, 480), (176, 320), (80, 160)]
+    graph = body25.layers()
+    params = synth.he_weights(graph, seed=21, out_scale=0.02)
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(params)
+    rng = np.random.default_rng(22)
+    xs = [rng.uniform(-0.5, 0.5, (2, 3, h, w)).astype(np.float32) for h, w in sizes]
+    outs = []
+    for x in xs:
+        net.forward(_dev(x))
+        outs.append(net.output_numpy())
+    assert [o.shape[2:] for o in outs] == [(46, 82), (34, 60), (22, 40), (10, 20)]
+    ov = np.stack([synth.overlay(4, 46, 82, seed=2300 + k) for k in range(2)]).astype(np.float32)
+    pose = PoseExtractor(ctx, net)
+    ovd = _dev(ov)
+    pose.set_overlay(ovd)
+    pose.forward_multi([_dev(x) for x in xs], (1280, 720))
+    s = pose.scale_net_to_output()
+    assert abs(s - 1.959128) < 1e-5
+    off = float(np.float32(0.5 / np.float64(s)))
+    gpu_heat = pose.heatmaps_numpy()
+    gpu_peaks = pose.peaks_numpy()
+    for k in range(2):
+        heat = oracle.resize_merge([outs[0][k] + ov[k]] + [o[k] for o in outs[1:]], 368, 656)
+        np.testing.assert_array_equal(gpu_heat[k], heat)
+        peaks = oracle.nms(heat, 0.05, 128, (off, off))
+        np.testing.assert_array_equal(gpu_peaks[k], peaks)
+        rk, rs = oracle.connect(heat, peaks, scale=s)
+        kp, ks = pose.keypoints(k)
+        assert len(kp) >= 1
+        np.testing.assert_array_equal(kp, rk)
+        np.testing.assert_array_equal(ks, rs)
