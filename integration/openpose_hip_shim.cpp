@@ -125,20 +125,26 @@ namespace op
             const auto numberBodyParts = (int)getPoseNumberBodyParts(poseModel);
             const auto channels = numberBodyParts + (addBkgChannel(poseModel) ? 1 : 0)
                                 + (int)getPoseMapIndex(poseModel).size();
+            // the CPU path's assembly (the parity target) where the reference's CPU connector
+            // exists; connectBodyPartsGpu's own global-sort assembly for the other models (BODY_135...)
+            const bool cpuModel = numberBodyParts == 25 || numberBodyParts == 18 || numberBodyParts == 15;
+            const int semantics = cpuModel ? OPK_CONNECT_CPU : OPK_CONNECT_GPU;
             int people = 0;
-            // first pass sizes the output (at most one person per peak of the first pair part)
-            std::vector<float> keypoints((size_t)(maxPeaks * 4 + 8) * numberBodyParts * 3);
-            std::vector<float> scores(maxPeaks * 4 + 8);
-            const int capacity = (int)scores.size();
-            check(opk_connect_body_parts(
-                      threadContext(), keypoints.data(), scores.data(), capacity, &people,
-                      (const float*)heatMapGpuPtr, (const float*)peaksGpuPtr, (int)poseModel, channels,
-                      heatMapSize.y, heatMapSize.x, maxPeaks, (float)interMinAboveThreshold,
-                      (float)interThreshold, minSubsetCnt, (float)minSubsetScore, (float)defaultNmsThreshold,
-                      (float)scaleFactor, maximizePositives ? 1 : 0),
-                  __LINE__, __FUNCTION__);
-            if (people > capacity)
-                error("more people than the connector's output capacity", __LINE__, __FUNCTION__, __FILE__);
+            std::vector<float> keypoints, scores;
+            for (int capacity = maxPeaks * 4 + 8;; capacity = people)
+            {
+                keypoints.resize((size_t)capacity * numberBodyParts * 3);
+                scores.resize(capacity);
+                check(opk_connect_body_parts_semantics(
+                          threadContext(), keypoints.data(), scores.data(), capacity, &people,
+                          (const float*)heatMapGpuPtr, (const float*)peaksGpuPtr, (int)poseModel, channels,
+                          heatMapSize.y, heatMapSize.x, maxPeaks, (float)interMinAboveThreshold,
+                          (float)interThreshold, minSubsetCnt, (float)minSubsetScore,
+                          (float)defaultNmsThreshold, (float)scaleFactor, maximizePositives ? 1 : 0, semantics),
+                      __LINE__, __FUNCTION__);
+                if (people <= capacity)
+                    break;   // otherwise: more people than rows, run again with room for all
+            }
             // peopleVectorToPeopleArray semantics (bodyPartConnectorBase.cpp:895-907)
             if (people > 0)
             {
