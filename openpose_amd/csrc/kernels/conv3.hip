@@ -477,7 +477,8 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
         boff[j] = rb * 32 + (phys ^ (((rb >> 2) & 1) << 1)) * 8;
     }
     // halo rows as 32-bit byte offsets from the position before the image (map() >= -1; buffers
-    // hold < 2^31 elements): one VGPR each, SGPR base + VGPR offset addressing
+    // hold < 2^31 elements): one VGPR each, SGPR base + VGPR offset addressing (measured faster on
+    // the BODY_25 layers than 64-bit per-lane addresses)
     const char* abase = reinterpret_cast<const char*>(a.in + a.in_coff - a.in_cs);
     uint32_t aoff[AIW];
 #define OPK3P_AROW(mt_)                                                                       \
@@ -537,13 +538,18 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
             vm_wait_rt64(younger);
             __builtin_amdgcn_s_barrier();
             if (u == 0 && it == 0) OPK3_STAMP(1);
-            if (u + 2 < U) {
-                const int c2 = (u + 2) / 3;
-                OPK3P_ISSUE(c2, (u + 2) - 3 * c2, (gc + c2) & 1, (u + 2) % 3);
-            } else if (has_next) {
-                if (u + 2 == U) OPK3P_AROW(mn);
-                OPK3P_ISSUE(0, u + 2 - U, (gc + cpt) & 1, (u + 2) % 3);
-            }
+            if (u == 0 && it == 1) OPK3_STAMP(3);
+#define OPK3P_PREFETCH()                                                                      \
+    do {                                                                                      \
+        if (u + 2 < U) {                                                                      \
+            const int c2 = (u + 2) / 3;                                                       \
+            OPK3P_ISSUE(c2, (u + 2) - 3 * c2, (gc + c2) & 1, (u + 2) % 3);                    \
+        } else if (has_next) {                                                                \
+            if (u + 2 == U) OPK3P_AROW(mn);                                                   \
+            OPK3P_ISSUE(0, u + 2 - U, (gc + cpt) & 1, (u + 2) % 3);                           \
+        }                                                                                     \
+    } while (0)
+            OPK3P_PREFETCH();
             const uint4* As = lds + ((gc + c) & 1) * ASLOT;
             const uint4* Bs = lds + 2 * ASLOT + (u % 3) * BSLOT;
 #pragma unroll
@@ -563,7 +569,9 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
             }
         }
+#undef OPK3P_PREFETCH
         if (it == 0) OPK3_STAMP(2);
+        if (it == 1) OPK3_STAMP(4);
 
         // ---- epilogue: one 8-byte store per (fragment, destination), border lanes to the sink ----
         long prow[MF];
@@ -708,9 +716,9 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
             const unsigned G = (unsigned)(per_n * nn);
             OPK_CHECK_ARG(G <= 1024, "persistent grid exceeds the sink");
             if (s.bn == 96)
-                hipLaunchKernelGGL(conv3p_kernel<96>, dim3(G), dim3(1024), 0, stream, a);
+                hipLaunchKernelGGL((conv3p_kernel<96>), dim3(G), dim3(1024), 0, stream, a);
             else
-                hipLaunchKernelGGL(conv3p_kernel<128>, dim3(G), dim3(1024), 0, stream, a);
+                hipLaunchKernelGGL((conv3p_kernel<128>), dim3(G), dim3(1024), 0, stream, a);
             OPK_LAUNCH_CHECK();
             return;
         }

@@ -3,6 +3,7 @@ the BODY_25 graph (product builtin == oracle restatement == the reference protot
 import ctypes
 import os
 import re
+import shutil
 import subprocess
 
 import pytest
@@ -40,8 +41,11 @@ def test_library_loads_and_reports_errors():
     assert rc == 1 and b"NULL" in L.opk_last_error()
 
 
-def test_gpu_kernels_are_gfx950_code_objects():
-    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", _lib.LIB_PATH],
+def test_gpu_kernels_are_gfx950_code_objects(tmp_path):
+    # llvm-objdump --offloading extracts the bundles next to its input: run it on a copy
+    lib = tmp_path / "libopk_hip.so"
+    shutil.copy(_lib.LIB_PATH, lib)
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", str(lib)],
                          capture_output=True, text=True)
     text = out.stdout + out.stderr
     assert "gfx950" in text

@@ -78,6 +78,12 @@ int main(int argc, char** argv)
     a.dst_cs[0] = cout;
     a.dst_coff[0] = 0;
 
+    void* dsink;
+    CK(hipMalloc(&dsink, kConv3SinkBytes));
+    a.sink = dsink;
+    int cus = 0;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    a.cus = cus;
     const Conv3Shape s3 = conv3_shape(frames, H, W, cout, 3);
     a.sw = s3.sw;
     a.nstrips = s3.nstrips;
@@ -105,29 +111,39 @@ int main(int argc, char** argv)
 
     std::vector<unsigned long long> h((size_t)nblk * 8);
     CK(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
-    // stamps: 0 start, 1 first DMA landed, 2 K loop done, 5 end; 6/7 = s_memrealtime (100 MHz)
-    const int ks[4][2] = {{0, 1}, {1, 2}, {2, 5}, {0, 5}};
-    const char* names[4] = {"prologue", "K loop", "epilogue", "block"};
+    // stamps: 0 start, 1 first DMA landed, 2 K loop done, 5 end; 6/7 = s_memrealtime (100 MHz);
+    // persistent kernel (conv3p): 3 second tile's first unit, 4 second tile's K loop done
+    const int ks[6][2] = {{0, 1}, {1, 2}, {2, 5}, {0, 5}, {2, 3}, {3, 4}};
+    const char* names[6] = {"prologue", "K loop", "epilogue", "block", "tile gap", "K loop 2"};
     double ratio = 0;
-    for (int b = 0; b < nblk; ++b)
+    int nr = 0;
+    for (int b = 0; b < nblk; ++b) {
+        if (h[b * 8 + 5] == 0) continue;   // blocks of a persistent grid beyond G never ran
         ratio += (double)(h[b * 8 + 5] - h[b * 8 + 0]) / (double)(h[b * 8 + 7] - h[b * 8 + 6]);
-    ratio /= nblk;
+        ++nr;
+    }
+    ratio /= nr;
     const double mhz = ratio * 100.0;
     std::printf("  s_memtime clock ~ %.0f MHz (vs s_memrealtime)\n", mhz);
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < 6; ++k) {
         double sum = 0, mn = 1e30, mx = 0;
+        int nb = 0;
         for (int b = 0; b < nblk; ++b) {
+            if (h[b * 8 + 5] == 0 || (k >= 4 && h[b * 8 + 4] == 0)) continue;   // no such stamp
+            ++nb;
             const double d = (double)(h[b * 8 + ks[k][1]] - h[b * 8 + ks[k][0]]);
             sum += d;
             mn = std::min(mn, d);
             mx = std::max(mx, d);
         }
-        std::printf("  %-9s mean %8.0f cyc = %7.2f us  (min %8.0f max %8.0f)\n", names[k], sum / nblk,
-                    sum / nblk / mhz, mn, mx);
+        if (nb == 0) continue;
+        std::printf("  %-9s mean %8.0f cyc = %7.2f us  (min %8.0f max %8.0f, %d blocks)\n", names[k],
+                    sum / nb, sum / nb / mhz, mn, mx, nb);
     }
     // wall span of the launch seen by the realtime clock
     unsigned long long t0 = ~0ull, t1 = 0;
     for (int b = 0; b < nblk; ++b) {
+        if (h[b * 8 + 5] == 0) continue;
         t0 = std::min(t0, h[b * 8 + 6]);
         t1 = std::max(t1, h[b * 8 + 7]);
     }
