@@ -2,14 +2,15 @@
 """bench.py -- OpenPose BODY_25 hot path on MI355X: frames/sec, whole node.
 
 Workload (BASELINE.json configs[1], one GPU; configs[2] when launched with --gpus N under
-torch.distributed.run): BODY_25 at net_resolution -1x368 on synthetic 1280x720 frames, i.e. net input
-656x368 (ScaleAndSizeExtractor, scaleAndSizeExtractor.cpp:57-66).  One step = one batch of frames
-per GPU through the whole hot path of PoseExtractorCaffe::forwardPass:
-    CNN forward (114 convs, MFMA fp16 / fp32 accumulate) -> + people overlay -> resize x8 (78 maps)
-    -> NMS (25 parts) -> PAF line integrals -> host people assembly -> keypoints per frame.
-Inputs are resident in HBM before timing: net-input frames (uniform [-0.5, 0.5), the range of the
-reference's /256-0.5 normalisation) and per-frame 5-person overlays (synthetic weights carry no
-meaning, so a deterministic people field is added to the net output -- its cost is counted).
+torch.distributed.run): BODY_25 at net_resolution -1x368 on synthetic 1280x720 BGR uint8 frames.
+One step = one batch of frames per GPU through the reference's whole per-frame path
+(ScaleAndSizeExtractor -> CvMatToOpInput -> PoseExtractorCaffe::forwardPass):
+    warpAffine 1280x720 -> 656x368 + normalisation -> CNN forward (114 convs, MFMA fp16 / fp32
+    accumulate) -> + people overlay -> resize x8 (78 maps) -> NMS (25 parts) -> PAF line integrals
+    -> host people assembly -> keypoints per frame.
+Inputs are resident in HBM before timing: uint8 frames (uniform random pixels) and per-frame
+5-person overlays (synthetic weights carry no meaning, so a deterministic people field is added to
+the net output -- its cost is counted).
 
 Frames shard across ranks with no collective in the data path (frame-parallel replicas, weak
 scaling); the only cross-rank traffic is the barrier and the max-reduce of the timer.
@@ -47,8 +48,9 @@ def parse():
 
 
 def cpu_baseline(args, params, frames_np, overlays_np):
-    """fp32 CPU restatement (oracle/) of the same pipeline on the same frames: CNN (im2col + SGEMM,
-    OpenMP), OpenCV-semantics cubic resize, nmsCpu, connectBodyPartsCpu."""
+    """fp32 CPU restatement (oracle/) of the same pipeline on the same uint8 frames: warpAffine +
+    normalisation, CNN (im2col + SGEMM, OpenMP), OpenCV-semantics cubic resize, nmsCpu,
+    connectBodyPartsCpu."""
     import oracle
     from oracle import body25
     graph = body25.layers()
@@ -56,7 +58,8 @@ def cpu_baseline(args, params, frames_np, overlays_np):
     done = 0
     people = 0
     while True:
-        x = frames_np[done % len(frames_np)][None]
+        scales, [(nw, nh)] = oracle.scale_and_size(PRODUCER)
+        x = oracle.cvmat_to_input(frames_np[done % len(frames_np)], scales[0], nw, nh)[None]
         out = body25.forward(x, params, graph=graph, nthreads=args.cpu_threads)[0]
         out = out + overlays_np[done % len(overlays_np)]
         heat = oracle.resize_merge([out], NET_H, NET_W)
@@ -69,8 +72,9 @@ def cpu_baseline(args, params, frames_np, overlays_np):
         if el >= args.cpu_seconds:
             break
     return {"value": done / el, "unit": "frames/s", "cores": args.cpu_threads, "kind": "port",
-            "sample": "%d frame(s) of the full pipeline at 656x368 (CNN fp32 + resize + NMS + "
-                      "connector), oracle/ CPU restatement, %.1f s, %d people found"
+            "sample": "%d frame(s) of the full pipeline on 1280x720 frames (warpAffine + CNN fp32 "
+                      "at 656x368 + resize + NMS + connector), oracle/ CPU restatement, %.1f s, "
+                      "%d people found"
                       % (done, el, people)}
 
 
@@ -109,7 +113,10 @@ def main():
 
     B = args.batch
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
-    frames = [torch.rand((B, 3, NET_H, NET_W), generator=gen, device="cuda") - 0.5 for _ in range(2)]
+    W_IN, H_IN = PRODUCER
+    frames = [torch.randint(0, 256, (B, H_IN, W_IN, 3), generator=gen, device="cuda",
+                            dtype=torch.uint8) for _ in range(2)]
+    pose.set_input((-1, NET_H))   # --net_resolution -1x368 -> 656x368 for 1280x720
     ov_np = np.stack([synth.overlay(args.people, NET_H // 8, NET_W // 8, seed=1000 * rank + f)
                       for f in range(B)])
     overlay = torch.from_numpy(ov_np).cuda()
@@ -119,14 +126,8 @@ def main():
 
     # Two-stage pipeline (opk_pose_submit / opk_pose_collect): the device work of batch i+1 is
     # enqueued before the host assembly of batch i, which then overlaps it.
-    def step(i, ev=None):
-        x = frames[i % 2]
-        if ev is not None:
-            ev[0].record()
-        p, shape = net.forward(x)
-        if ev is not None:
-            ev[1].record()
-        pose.submit_net_output((p, shape), (NET_W, NET_H), PRODUCER)
+    def step(i):
+        pose.submit_frames(frames[i % 2])
         if pose.pending() > 1:
             pose.collect()
 
@@ -139,24 +140,30 @@ def main():
     drain()
     torch.cuda.synchronize()
     people = [pose.num_people(f) for f in range(B)]
-    net.forward(frames[0])
+    pose.forward_frames(frames[0])
     out_std = float(net.output_numpy()[:2].std())
+    net_in = pose.net_input_numpy()
+    assert net_in.shape == (B, 3, NET_H, NET_W)
 
-    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in range(args.steps)]
+    # CNN forward time: HIP events recorded by the library around every forward, on the
+    # context stream the conv kernels run on (opk_net_set_timing)
+    net.set_timing(True)
     if world > 1:
         import torch.distributed as dist
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i, events[i])
+        step(i)
     drain()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    net_ms = float(np.mean([a.elapsed_time(b) for a, b in events]))
+    nfw, fw_ms = net.read_timing()
+    net.set_timing(False)
+    assert nfw == args.steps, nfw
+    net_ms = fw_ms / nfw
     if world > 1:
         t = torch.tensor([elapsed, net_ms], device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -177,15 +184,16 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp16",
-        "data": "synthetic",
+        "data": "synthetic uint8 BGR 1280x720 frames (uniform random), random-init weights",
         "config": {
             "workload": "BODY_25 net_resolution -1x368 (net input 656x368) on synthetic 1280x720 "
-                        "frames, %d-person overlay per frame; CNN+resize+NMS+PAF+assembly" % args.people,
+                        "uint8 frames, %d-person overlay per frame; warpAffine+CNN+resize+NMS+PAF+"
+                        "assembly" % args.people,
             "frames_per_step_per_gpu": B,
             "net_input": [NET_H, NET_W],
             "heatmaps": [78, NET_H, NET_W],
             "parallelism": "frame-parallel replicas x%d" % world,
-            "compute": "conv fp16 x fp16 -> fp32 MFMA; resize/NMS/PAF fp32",
+            "compute": "warp u8 fixed-point; conv fp16 x fp16 -> fp32 MFMA; resize/NMS/PAF fp32",
             "people_per_frame_found": people[:4],
             "net_output_std_before_overlay": round(out_std, 5),
         },
@@ -204,7 +212,7 @@ def main():
         },
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        frames_np = frames[0][:2].cpu().numpy()
+        frames_np = frames[0][:2].cpu().numpy()   # uint8 [2][720][1280][3]
         result["cpu_baseline"] = cpu_baseline(args, params, frames_np, ov_np[:2])
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -150,6 +150,23 @@ int opk_pose_model_info(int pose_model, int* parts, int* bkg, int* npairs, int* 
 int opk_pose_default_thresholds(int pose_model, int maximize_positives, float* nms_threshold,
                                 float* inter_threshold);
 
+/* ---- Frame -> net input.
+ * opk_scale_and_size replaces op::ScaleAndSizeExtractor::extract
+ *      (include/openpose/core/scaleAndSizeExtractor.hpp:17-18, scaleAndSizeExtractor.cpp:37-105):
+ *      net_w or net_h <= 0 derives that side from the frame's aspect ratio (-1x368), bounded at
+ *      16:9 times dynamic_behavior when it is > 0 (--net_resolution_dynamic); scales[i] =
+ *      scaleInputToNetInputs, net_sizes[2i], [2i+1] = netInputSizes (w, h), i < scale_number.
+ * opk_cvmat_to_input replaces op::CvMatToOpInput::createArray for one scale
+ *      (include/openpose/core/cvMatToOpInput.hpp:17-19, cvMatToOpInput.cpp:63-98), for a batch:
+ *      frames_dev = n BGR uint8 frames [height][step bytes] (step 0 = width*3), input_dev =
+ *      [n][3][net_h][net_w] fp32: cv::warpAffine(diag(scale)) with OpenCV's fixed-point 8-bit
+ *      arithmetic (INTER_LINEAR for scale <= 1, INTER_CUBIC above; zero border), then
+ *      u/256 - 0.5 when normalize == 1 (uCharCvMatToFloatPtr, openCv.cpp:57-150). */
+int opk_scale_and_size(int in_w, int in_h, int net_w, int net_h, float dynamic_behavior,
+                       int scale_number, double scale_gap, double* scales, int* net_sizes);
+int opk_cvmat_to_input(opk_ctx* ctx, float* input_dev, const uint8_t* frames_dev, int n, int width,
+                       int height, size_t step, double scale, int net_w, int net_h, int normalize);
+
 /* ---- Net: replaces op::Net / op::NetCaffe (include/openpose/net/net.hpp:8-18,
  *      netCaffe.hpp:12-13).  prototxt: a Caffe prototxt path, or "builtin:BODY_25".
  *      caffemodel: path or NULL (then weights must be supplied with opk_net_set_conv). */
@@ -167,6 +184,11 @@ int opk_net_set_conv(opk_net* net, const char* name, const float* weights_host,
 int opk_net_forward(opk_net* net, const float* input_dev, int n, int h, int w);
 /* useful (unpadded) convolution FLOPs of one frame of h x w (2 * MACs, all conv layers) */
 int opk_net_flops_per_frame(opk_net* net, int h, int w, double* flops);
+/* Forward timing (measurement hook, no reference counterpart): while enabled every forward is
+ * bracketed by HIP events on the context stream; read waits for them and returns the number of
+ * forwards since the last read and their summed device time in milliseconds. */
+int opk_net_set_timing(opk_net* net, int enable);
+int opk_net_read_timing(opk_net* net, int* forwards, double* total_ms);
 /* device pointer + NCHW shape of the last forward's net_output blob */
 int opk_net_output(opk_net* net, float** output_dev, int shape[4]);
 
@@ -217,6 +239,21 @@ int opk_pose_submit_multi(opk_pose* pose, const float* const* frames_dev, const 
                           int num_scales, int n, int producer_w, int producer_h);
 int opk_pose_forward_multi(opk_pose* pose, const float* const* frames_dev, const int* net_hw,
                            int num_scales, int n, int producer_w, int producer_h);
+/* Raw frames: the whole per-frame path of the reference's Wrapper workers
+ * (WScaleAndSizeExtractor -> WCvMatToOpInput -> WPoseExtractorNet, wrapperAuxiliary.hpp):
+ * frames_dev = n BGR uint8 frames [height][step bytes] on device (step 0 = width*3), prepared
+ * on the GPU for every scale of opk_pose_set_input (default: -1x368, dynamic 1, one scale, gap
+ * 0.25 -- the reference's flag defaults), then one net pass per scale and the merged
+ * post-processing.  Keypoints are in frame pixels (scaleNetToOutput for a frame-sized output). */
+int opk_pose_set_input(opk_pose* pose, int net_w, int net_h, float dynamic_behavior,
+                       int scale_number, double scale_gap);
+int opk_pose_submit_frames(opk_pose* pose, const uint8_t* frames_dev, int n, int width,
+                           int height, size_t step);
+int opk_pose_forward_frames(opk_pose* pose, const uint8_t* frames_dev, int n, int width,
+                            int height, size_t step);
+/* net input of scale i prepared by the last opk_pose_submit_frames ([n][3][net_h][net_w]) */
+int opk_pose_net_input(opk_pose* pose, int scale, const float** input_dev, int* net_w,
+                       int* net_h);
 int opk_pose_pending(opk_pose* pose);   /* batches in flight, -1 for NULL */
 /* optional additive overlay on the net output before resize (synthetic-people workloads):
  * [n][78][out_h][out_w] device fp32, NULL to disable */

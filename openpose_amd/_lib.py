@@ -70,6 +70,14 @@ _SIGS = {
     "opk_pose_heatmaps": (_i, [_p, _c.POINTER(_p), _ip]),
     "opk_pose_peaks": (_i, [_p, _c.POINTER(_p), _ip]),
     "opk_pose_scale_net_to_output": (_f, [_p]),
+    "opk_net_set_timing": (_i, [_p, _i]),
+    "opk_net_read_timing": (_i, [_p, _ip, _c.POINTER(_d)]),
+    "opk_scale_and_size": (_i, [_i, _i, _i, _i, _f, _i, _d, _c.POINTER(_d), _ip]),
+    "opk_cvmat_to_input": (_i, [_p, _p, _p, _i, _i, _i, _c.c_size_t, _d, _i, _i, _i]),
+    "opk_pose_set_input": (_i, [_p, _i, _i, _f, _i, _d]),
+    "opk_pose_submit_frames": (_i, [_p, _p, _i, _i, _i, _c.c_size_t]),
+    "opk_pose_forward_frames": (_i, [_p, _p, _i, _i, _i, _c.c_size_t]),
+    "opk_pose_net_input": (_i, [_p, _i, _c.POINTER(_p), _ip, _ip]),
 }
 
 _LIB = None

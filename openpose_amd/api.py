@@ -90,6 +90,16 @@ class Context:
         check(self.L.opk_resize_and_merge(self.h, _ptr(target), ptrs, n, int4(target.shape), sizes,
                                           None))
 
+    def cvmat_to_input(self, net_input, frames, scale, normalize=1):
+        """op::CvMatToOpInput for one scale: frames [n, h, w, 3] uint8 BGR (CUDA) ->
+        net_input [n, 3, net_h, net_w] float32 (CUDA)."""
+        n, h, w, c = frames.shape
+        assert c == 3 and frames.dtype == torch.uint8
+        assert net_input.shape[0] == n and net_input.shape[1] == 3
+        check(self.L.opk_cvmat_to_input(self.h, _ptr(net_input), _ptr(frames), n, w, h, w * 3,
+                                        float(scale), net_input.shape[3], net_input.shape[2],
+                                        normalize))
+
     def nms(self, peaks, heat, threshold=NMS_THRESHOLD, offset=(0.0, 0.0)):
         """peaks [N,parts,maxPeaks+1,3]; heat [N,C,H,W] (nmsGpu)."""
         check(self.L.opk_nms(self.h, _ptr(peaks), None, _ptr(heat), threshold, int4(peaks.shape),
@@ -120,6 +130,18 @@ class Context:
             nms_th, scale, int(maximize_positives), semantics))
         k = min(n.value, max_people)
         return kp[:k].copy(), ks[:k].copy()
+
+
+def scale_and_size(input_size, net_resolution=(-1, 368), dynamic_behavior=1.0, scale_number=1,
+                   scale_gap=0.25):
+    """op::ScaleAndSizeExtractor::extract: ([scaleInputToNetInputs], [(net_w, net_h)])."""
+    L = _lib.load()
+    scales = (ctypes.c_double * scale_number)()
+    sizes = (ctypes.c_int * (2 * scale_number))()
+    check(L.opk_scale_and_size(input_size[0], input_size[1], net_resolution[0], net_resolution[1],
+                               float(dynamic_behavior), scale_number, float(scale_gap), scales,
+                               sizes))
+    return list(scales), [(sizes[2 * i], sizes[2 * i + 1]) for i in range(scale_number)]
 
 
 def pose_model_info(pose_model):
@@ -218,6 +240,15 @@ class Net:
         check(self.L.opk_net_forward(self.h, _ptr(x), n, h, w))
         return self.output()
 
+    def set_timing(self, on=True):
+        check(self.L.opk_net_set_timing(self.h, int(on)))
+
+    def read_timing(self):
+        """(forwards, summed device ms) since the last read (HIP events on the context stream)."""
+        n, ms = ctypes.c_int(), ctypes.c_double()
+        check(self.L.opk_net_read_timing(self.h, ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
     def flops_per_frame(self, h, w):
         f = ctypes.c_double()
         check(self.L.opk_net_flops_per_frame(self.h, h, w, ctypes.byref(f)))
@@ -289,6 +320,35 @@ class PoseExtractor:
 
     def submit_multi(self, frames, producer_size):
         self._multi(self.L.opk_pose_submit_multi, frames, producer_size)
+
+    def set_input(self, net_resolution=(-1, 368), dynamic_behavior=1.0, scale_number=1,
+                  scale_gap=0.25):
+        """--net_resolution, --net_resolution_dynamic, --scale_number, --scale_gap."""
+        check(self.L.opk_pose_set_input(self.h, net_resolution[0], net_resolution[1],
+                                        float(dynamic_behavior), scale_number, float(scale_gap)))
+
+    def _frames(self, fn, frames):
+        n, h, w, c = frames.shape
+        assert c == 3 and frames.dtype == torch.uint8
+        check(fn(self.h, _ptr(frames), n, w, h, w * 3))
+        self._frames_n = n
+
+    def forward_frames(self, frames):
+        """Raw BGR uint8 frames [n, h, w, 3] (CUDA): GPU preprocessing + net + post-processing."""
+        self._frames(self.L.opk_pose_forward_frames, frames)
+
+    def submit_frames(self, frames):
+        self._frames(self.L.opk_pose_submit_frames, frames)
+
+    def net_input_numpy(self, scale=0):
+        p = ctypes.c_void_p()
+        w, h = ctypes.c_int(), ctypes.c_int()
+        check(self.L.opk_pose_net_input(self.h, scale, ctypes.byref(p), ctypes.byref(w),
+                                        ctypes.byref(h)))
+        n = self._frames_n
+        out = np.empty((n, 3, h.value, w.value), np.float32)
+        check(self.L.opk_memcpy_d2h(self.ctx.h, out.ctypes.data_as(ctypes.c_void_p), p, out.nbytes))
+        return out
 
     def forward_net_output(self, net_output, net_size, producer_size):
         """net_output: [n, heat_channels, h, w] CUDA tensor (or (ptr, shape)); net_size = (w, h)."""

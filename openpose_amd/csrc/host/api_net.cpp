@@ -6,6 +6,7 @@
 
 #include "../../../include/opk.h"
 #include "net.h"
+#include "input.h"
 #include "pose.h"
 
 namespace opk {
@@ -264,6 +265,79 @@ int opk_pose_peaks(opk_pose* p, float** peaks, int shape[4])
     return guarded_net([&] {
         OPK_CHECK_ARG(p && peaks && shape, "NULL argument");
         *peaks = p->pose->peaks(shape);
+    });
+}
+
+int opk_net_set_timing(opk_net* net, int enable)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net, "NULL net");
+        net->net->set_timing(enable != 0);
+    });
+}
+
+int opk_net_read_timing(opk_net* net, int* forwards, double* total_ms)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net, "NULL net");
+        net->net->read_timing(forwards, total_ms);
+    });
+}
+
+int opk_scale_and_size(int in_w, int in_h, int net_w, int net_h, float dynamic_behavior,
+                       int scale_number, double scale_gap, double* scales, int* net_sizes)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(scales && net_sizes, "NULL output");
+        opk::scale_and_size(in_w, in_h, net_w, net_h, dynamic_behavior, scale_number, scale_gap,
+                            scales, net_sizes);
+    });
+}
+
+int opk_cvmat_to_input(opk_ctx* ctx, float* input_dev, const uint8_t* frames_dev, int n, int width,
+                       int height, size_t step, double scale, int net_w, int net_h, int normalize)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ctx, "NULL context");
+        OPK_CHECK_ARG(normalize == 0 || normalize == 1,
+                      "normalize: 0 (none) or 1 (VGG); DenseNet (2) is not supported");
+        opk::cvmat_to_input(ctx, input_dev, frames_dev, n, width, height, step, scale, net_w, net_h,
+                            normalize);
+    });
+}
+
+int opk_pose_set_input(opk_pose* p, int net_w, int net_h, float dynamic_behavior, int scale_number,
+                       double scale_gap)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->set_input(net_w, net_h, dynamic_behavior, scale_number, scale_gap);
+    });
+}
+
+int opk_pose_submit_frames(opk_pose* p, const uint8_t* frames, int n, int width, int height,
+                           size_t step)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->submit_frames(frames, n, width, height, step);
+    });
+}
+
+int opk_pose_forward_frames(opk_pose* p, const uint8_t* frames, int n, int width, int height,
+                            size_t step)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->forward_frames(frames, n, width, height, step);
+    });
+}
+
+int opk_pose_net_input(opk_pose* p, int scale, const float** input_dev, int* net_w, int* net_h)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p && input_dev, "NULL argument");
+        *input_dev = p->pose->net_input(scale, net_w, net_h);
     });
 }
 

@@ -31,6 +31,14 @@ struct Context {
     std::map<int, std::unique_ptr<PoseDev>> pose_dev;
     const PafPairTable& pose_table(int model);
 
+    // frame -> net input (host/input.cpp): fixed-point weight tables (0 linear, 1 cubic) and the
+    // per-axis tap tables of each (scale, dw, dh)
+    DevBuf warp_weights[2];
+    const short* warp_weight_table(bool cubic);
+    struct WarpAxes { DevBuf buf; const int* x; const int* y; };
+    std::map<std::tuple<uint64_t, int, int>, std::unique_ptr<WarpAxes>> warp_axes;
+    const WarpAxes& warp_axis_tables(double scale, int dw, int dh);
+
     DevBuf scratch_scores;   // dense pair scores for opk_connect_body_parts
     // NMS candidate lists (nms.hip), zeroed when (re)allocated; the kernels keep them zeroed
     DevBuf nms_scratch;

@@ -408,6 +408,23 @@ void NetHip::forward(const float* input, int n, int h, int w)
     ctx_->bind();
     ShapePlan& S = *shape_plan(n, h, w);
     cur_ = &S;
+    if (timing_) {
+        if (free_events_.empty()) {
+            std::pair<hipEvent_t, hipEvent_t> e;
+            OPK_HIP(hipEventCreate(&e.first));
+            OPK_HIP(hipEventCreate(&e.second));
+            free_events_.push_back(e);
+        }
+        events_.push_back(free_events_.back());
+        free_events_.pop_back();
+        OPK_HIP(hipEventRecord(events_.back().first, ctx_->stream));
+    }
+    forward_launches(S, input, n, h, w);
+    if (timing_) OPK_HIP(hipEventRecord(events_.back().second, ctx_->stream));
+}
+
+void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, int w)
+{
     const std::vector<uint16_t*>& ptr = S.base;
     const std::vector<int>& lh_ = S.lh;
     const std::vector<int>& lw_ = S.lw;
@@ -454,6 +471,35 @@ void NetHip::forward(const float* input, int n, int h, int w)
                             bufs_[p.in_buf].cs, lh_[L + 1], lw_[L + 1], ctx_->stream);
         }
     }
+}
+
+NetHip::~NetHip()
+{
+    for (auto* v : {&events_, &free_events_})
+        for (auto& e : *v) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+}
+
+void NetHip::set_timing(bool on)
+{
+    timing_ = on;
+}
+
+void NetHip::read_timing(int* count, double* total_ms)
+{
+    double t = 0;
+    for (auto& e : events_) {
+        OPK_HIP(hipEventSynchronize(e.second));
+        float ms = 0.f;
+        OPK_HIP(hipEventElapsedTime(&ms, e.first, e.second));
+        t += ms;
+        free_events_.push_back(e);
+    }
+    if (count) *count = (int)events_.size();
+    if (total_ms) *total_ms = t;
+    events_.clear();
 }
 
 }  // namespace opk

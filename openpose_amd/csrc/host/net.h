@@ -36,6 +36,12 @@ public:
     int frames() const { return cur_ ? cur_->n : 0; }
     static constexpr int kMaxShapes = 8;
     double flops_per_frame(int h, int w) const;   // useful (unpadded) conv FLOPs
+    ~NetHip();
+
+    // forward timing on the context stream (HIP events around every forward while enabled);
+    // read() waits for the recorded forwards and returns their count and summed milliseconds
+    void set_timing(bool on);
+    void read_timing(int* count, double* total_ms);
 
 private:
     struct Placement { int buf; int coff; };
@@ -70,6 +76,7 @@ private:
     };
 
     void plan(const std::vector<LayerDesc>& layers);
+    void forward_launches(ShapePlan& S, const float* input, int n, int h, int w);
     ShapePlan* shape_plan(int n, int h, int w);
 
     Context* ctx_;
@@ -90,6 +97,9 @@ private:
     std::vector<std::unique_ptr<ShapePlan>> shapes_;   // oldest first
     ShapePlan* cur_ = nullptr;    // shape of the last forward
     DevBuf sink_;                 // persistent conv3: target of masked-off stores
+    bool timing_ = false;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events_;   // recorded forwards
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events_;
 };
 
 }  // namespace opk

@@ -18,6 +18,7 @@
 #include <string>
 
 #include "../../../include/opk.h"
+#include "input.h"
 
 namespace opk {
 
@@ -117,6 +118,61 @@ void PoseHip::submit(const float* frames, int n, int net_h, int net_w, int prod_
     net_->forward(frames, n, net_h, net_w);
     submit_net_output(net_->output(), n, net_->out_h(), net_->out_w(), net_h, net_w, prod_w,
                       prod_h);
+}
+
+void PoseHip::set_input(int net_w, int net_h, float dyn, int scale_number, double scale_gap)
+{
+    OPK_CHECK_ARG(net_w > 0 || net_h > 0,
+                  "Only 1 of the dimensions of net input resolution can be <= 0.");
+    OPK_CHECK_ARG(scale_number >= 1 && scale_number <= kMaxResizeSources, "1..8 scales");
+    OPK_CHECK_ARG(1. - (scale_number - 1) * scale_gap >= 0. && scale_gap >= 0.,
+                  "All scales must be in the range [0, 1], i.e., 0 <= 1-scale_number*scale_gap <= 1");
+    in_net_w_ = net_w;
+    in_net_h_ = net_h;
+    dyn_ = dyn;
+    scale_number_ = scale_number;
+    scale_gap_ = scale_gap;
+}
+
+void PoseHip::submit_frames(const uint8_t* frames, int n, int w, int h, size_t step)
+{
+    OPK_CHECK_ARG(net_ != nullptr, "no network: raw frames need the net");
+    OPK_CHECK_ARG(frames != nullptr && n > 0 && w > 0 && h > 0, "empty frames");
+    OPK_CHECK_ARG(count_ < 2, "two batches already in flight: collect first");
+    OPK_CHECK_ARG(model_ != 6, "BODY_19N (DenseNet normalisation) is not supported");
+    double scales[kMaxResizeSources];
+    scale_and_size(w, h, in_net_w_, in_net_h_, dyn_, scale_number_, scale_gap_, scales, input_hw_);
+    const float* ptrs[kMaxResizeSources];
+    int hw[2 * kMaxResizeSources];
+    for (int i = 0; i < scale_number_; ++i) {
+        const int nw = input_hw_[2 * i], nh = input_hw_[2 * i + 1];
+        float* x = static_cast<float*>(inputs_[i].get((size_t)n * 3 * nh * nw * sizeof(float)));
+        // the net of the previous batch read this buffer earlier on the same stream
+        cvmat_to_input(ctx_, x, frames, n, w, h, step, scales[i], nw, nh, 1);
+        ptrs[i] = x;
+        hw[2 * i] = nh;
+        hw[2 * i + 1] = nw;
+    }
+    inputs_n_ = n;
+    if (scale_number_ == 1)
+        submit(ptrs[0], n, hw[0], hw[1], w, h);
+    else
+        submit_multi(ptrs, hw, scale_number_, n, w, h);
+}
+
+void PoseHip::forward_frames(const uint8_t* frames, int n, int w, int h, size_t step)
+{
+    OPK_CHECK_ARG(count_ == 0, "batches in flight: collect them first");
+    submit_frames(frames, n, w, h, step);
+    collect();
+}
+
+const float* PoseHip::net_input(int i, int* w, int* h) const
+{
+    OPK_CHECK_ARG(i >= 0 && i < scale_number_ && inputs_n_ > 0, "no such scale");
+    if (w) *w = input_hw_[2 * i];
+    if (h) *h = input_hw_[2 * i + 1];
+    return static_cast<const float*>(inputs_[i].ptr);
 }
 
 void PoseHip::submit_multi(const float* const* frames, const int* net_hw, int nscales, int n,

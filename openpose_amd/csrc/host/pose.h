@@ -36,6 +36,14 @@ public:
     // the [n][3][net_hw[2i]][net_hw[2i+1]] net input of scale i; scale 0 sets the heat-map size
     void submit_multi(const float* const* frames, const int* net_hw, int nscales, int n,
                       int prod_w, int prod_h);
+    // raw frames (the reference's full per-frame path: ScaleAndSizeExtractor -> CvMatToOpInput ->
+    // PoseExtractorCaffe): n BGR uint8 frames [h][step bytes] on device, prepared on the GPU for
+    // every scale of set_input(), then the net per scale and the merged post-processing
+    void set_input(int net_w, int net_h, float dyn, int scale_number, double scale_gap);
+    void submit_frames(const uint8_t* frames, int n, int w, int h, size_t step);
+    void forward_frames(const uint8_t* frames, int n, int w, int h, size_t step);
+    // net input of scale i of the last submit_frames ([n][3][h][w] fp32 device; w/h may be NULL)
+    const float* net_input(int i, int* w, int* h) const;
     int collect();                       // frames of the collected batch
     int pending() const { return count_; }
 
@@ -74,6 +82,13 @@ private:
 
     Context* ctx_;
     NetHip* net_;
+    // set_input(): --net_resolution, --net_resolution_dynamic, --scale_number, --scale_gap
+    int in_net_w_ = -1, in_net_h_ = 368, scale_number_ = 1;
+    float dyn_ = 1.f;
+    double scale_gap_ = 0.25;
+    DevBuf inputs_[kMaxResizeSources];
+    int input_hw_[2 * kMaxResizeSources] = {};
+    int inputs_n_ = 0;
     bool maximize_positives_;
     int model_, semantics_;
     double props_[5];

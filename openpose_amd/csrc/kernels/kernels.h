@@ -70,6 +70,14 @@ void launch_paf_scores_compact(float* records, int rec_floats, const HeatMap& he
                                const PafPairTable& t, float inter_th, float inter_min_above,
                                float reject_score, double near_dist, hipStream_t stream);
 
+// ---- frame -> net input (input.hip) -------------------------------------------------------------
+// src: n BGR uint8 frames [sh][src_step bytes], frame stride src_step*sh; dst [n][3][dh][dw] fp32.
+// xtab/ytab: per destination column/row {first source tap, 5-bit fraction index}; wtab: the
+// fixed-point 2-D weight table [32*32][ksize*ksize] (host/input.cpp builds all three)
+void launch_cvmat_to_input(float* dst, const uint8_t* src, int n, int sh, int sw, size_t src_step,
+                           int dh, int dw, const int* xtab, const int* ytab, const short* wtab,
+                           int ksize, int normalize, hipStream_t stream);
+
 // ---- elementwise helpers (misc.hip) -----------------------------------------------------------
 void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stream);
 

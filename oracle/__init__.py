@@ -57,6 +57,13 @@ def lib():
         L.orc_prelu.argtypes = [_f32p, _f32p, _i, _i, _i]
         L.orc_relu.argtypes = [_f32p, ctypes.c_long]
         L.orc_maxpool.argtypes = [_f32p, _f32p, _i, _i, _i, _i, _i, _i, _i, _i]
+        _u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+        L.orc_scale_and_size.argtypes = [_i, _i, _i, _i, _f, _i, ctypes.c_double,
+                                         np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS"),
+                                         _i32p]
+        L.orc_cvmat_to_input.argtypes = [_f32p, _u8p, _i, _i, ctypes.c_double, _i, _i, _i]
+        _i16p = np.ctypeslib.ndpointer(np.int16, flags="C_CONTIGUOUS")
+        L.orc_warp_tab.argtypes = [_i, _i16p]
         _LIB = L
     return _LIB
 
@@ -232,6 +239,35 @@ def pair_scores(heat, peaks, pairs, map_idx, nparts=25, **kw):
 
 
 # ---- Caffe layers -----------------------------------------------------------------------------
+def scale_and_size(input_size, net_resolution=(-1, 368), dynamic_behavior=1.0, scale_number=1,
+                   scale_gap=0.25):
+    """ScaleAndSizeExtractor::extract restated (preprocess.c): (scales, [(w, h)])."""
+    scales = np.zeros(scale_number, np.float64)
+    sizes = np.zeros(2 * scale_number, np.int32)
+    rc = lib().orc_scale_and_size(input_size[0], input_size[1], net_resolution[0],
+                                  net_resolution[1], dynamic_behavior, scale_number, scale_gap,
+                                  scales, sizes)
+    if rc != 0:
+        raise ValueError("invalid scale/size configuration")
+    return list(scales), [(int(sizes[2 * i]), int(sizes[2 * i + 1])) for i in range(scale_number)]
+
+
+def cvmat_to_input(frame, scale, net_w, net_h, normalize=1):
+    """CvMatToOpInput for one BGR uint8 frame [h, w, 3] -> [3, net_h, net_w] float32."""
+    frame = np.ascontiguousarray(frame, np.uint8)
+    out = np.empty((3, net_h, net_w), np.float32)
+    lib().orc_cvmat_to_input(out, frame, frame.shape[1], frame.shape[0], float(scale), net_w,
+                             net_h, normalize)
+    return out
+
+
+def warp_weight_table(cubic):
+    k = 4 if cubic else 2
+    t = np.zeros(1025 * k * k, np.int16)
+    lib().orc_warp_tab(int(cubic), t)
+    return t[:1024 * k * k].reshape(32, 32, k, k)
+
+
 def default_threads():
     """OMP_NUM_THREADS if set (16 on the GPU box: its CPU share), else min(16, cpu_count)."""
     env = os.environ.get("OMP_NUM_THREADS")

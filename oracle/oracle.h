@@ -15,6 +15,8 @@
  *     absent from the image -> reference unbuildable here); restatement + known-answer tests
  *   - resize (orc_resize_cubic/merge)        : parity unpinned (OpenCV cv::resize is a third-party
  *     dependency absent from the image); restatement of OpenCV's generic float INTER_CUBIC path
+ *   - frame -> net input (orc_cvmat_to_input) : parity unpinned (cv::warpAffine is OpenCV);
+ *     restatement of OpenCV 4.2's fixed-point 8-bit warp
  *   - CNN layers (orc_conv2d, ...)           : parity unpinned (Caffe absent); restatement of Caffe
  *     layer semantics, cross-checked against torch CPU fp32 in tests
  *
@@ -92,6 +94,16 @@ int orc_pose_num_parts(int pose_model);
 int orc_pose_num_pairs(int pose_model);
 const unsigned* orc_pose_pairs(int pose_model);
 const unsigned* orc_pose_map_idx(int pose_model);
+
+/* ---- frame -> net input (preprocess.c): ScaleAndSizeExtractor::extract
+ * (scaleAndSizeExtractor.cpp:37-105) and CvMatToOpInput::createArray's CPU branch
+ * (cvMatToOpInput.cpp:63-98: warpAffine + uCharCvMatToFloatPtr).  Parity unpinned (OpenCV). */
+int orc_scale_and_size(int in_w, int in_h, int net_w, int net_h, float dyn, int scale_number,
+                       double scale_gap, double* scales, int* sizes);
+double orc_resize_scale_factor(int iw, int ih, int tw, int th);
+void orc_warp_tab(int cubic, short* itab);
+void orc_cvmat_to_input(float* dst, const uint8_t* src, int sw, int sh, double scale, int dw,
+                        int dh, int normalize);
 
 /* ---- Caffe layer semantics for the BODY_25 prototxt (NCHW fp32, batch n) ------------------ */
 /* Convolution: cross-correlation, zero pad, stride 1, bias (Caffe ConvolutionLayer) */
