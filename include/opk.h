@@ -168,10 +168,18 @@ int opk_cvmat_to_input(opk_ctx* ctx, float* input_dev, const uint8_t* frames_dev
                        int height, size_t step, double scale, int net_w, int net_h, int normalize);
 
 /* ---- Net: replaces op::Net / op::NetCaffe (include/openpose/net/net.hpp:8-18,
- *      netCaffe.hpp:12-13).  prototxt: a Caffe prototxt path, or "builtin:BODY_25".
- *      caffemodel: path or NULL (then weights must be supplied with opk_net_set_conv). */
+ *      netCaffe.hpp:12-13).  prototxt: a Caffe prototxt path, or "builtin:BODY_25". */
 typedef struct opk_net opk_net;
+/* caffemodel (or NULL): trained weights, loaded as caffe::Net::CopyTrainedLayersFrom does
+ * (netCaffe.cpp:163-185): every conv whose name is in the file gets its weights, bias and the
+ * slopes of its PReLU layer, shapes checked; file layers the net lacks are ignored.  Convs not in
+ * the file must be set with opk_net_set_conv before a forward. */
 int opk_net_create(opk_ctx* ctx, const char* prototxt, const char* caffemodel, opk_net** out);
+int opk_net_load_caffemodel(opk_net* net, const char* caffemodel, int* convs_loaded);
+/* Host utility (no device): blob `index` of `layer` in a .caffemodel; shape gets <= 8 dims
+ * (legacy 4-D shapes as stored), data (may be NULL) the float values. */
+int opk_caffemodel_blob(const char* caffemodel, const char* layer, int index, float* data,
+                        size_t capacity, int64_t* shape, int* ndim);
 int opk_net_destroy(opk_net* net);
 int opk_net_num_convs(opk_net* net);
 /* name buffer >= 64 bytes; act: 0 none, 1 ReLU, 2 PReLU */

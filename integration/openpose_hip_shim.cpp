@@ -10,7 +10,10 @@
 //   op::connectBodyPartsGpu<float|double> (include/openpose/net/bodyPartConnectorBase.hpp:17-24,
 //                                          replaces src/openpose/net/bodyPartConnectorBase.cu)
 // and op::NetHip, an op::Net (include/openpose/net/net.hpp:8-18) with NetCaffe's constructor shape
-// (netCaffe.hpp:12-13), for PoseExtractorCaffe::addCaffeNetOnThread (poseExtractorCaffe.cpp:82-86).
+// (netCaffe.hpp:12-13), for PoseExtractorCaffe::addCaffeNetOnThread (poseExtractorCaffe.cpp:82-86),
+// loading the .caffemodel itself; and the members of op::CvMatToOpInput
+// (include/openpose/core/cvMatToOpInput.hpp:9-28, replaces src/openpose/core/cvMatToOpInput.cpp):
+// the frame -> net-input warp and normalisation on the GPU with the CPU branch's numerics.
 // Numerics are the CPU path's; errors come back through op::error, the reference's
 // convention (errorAndLog.cpp:158-233).  See INTEGRATION.md for the build lines.
 #include <memory>
@@ -19,6 +22,7 @@
 #include <vector>
 
 #include <openpose/core/common.hpp>
+#include <openpose/core/cvMatToOpInput.hpp>
 #include <openpose/net/bodyPartConnectorBase.hpp>
 #include <openpose/net/net.hpp>
 #include <openpose/net/nmsBase.hpp>
@@ -259,5 +263,80 @@ namespace op
     std::shared_ptr<Net> makeNetHip(const std::string& proto, const std::string& model, const int gpuId)
     {
         return std::make_shared<NetHip>(proto, model, gpuId);
+    }
+
+    // ---- op::CvMatToOpInput on libopk_hip --------------------------------------------------------
+    // The reference's own members are reused: pInputImageCuda holds the frame, pOutputImageCuda the
+    // net input of one scale (both device buffers of the calling thread's context).
+    CvMatToOpInput::CvMatToOpInput(const PoseModel poseModel, const bool gpuResize) :
+        mPoseModel{poseModel},
+        mGpuResize{gpuResize},   // either way the GPU runs the CPU branch's arithmetic
+        pInputImageCuda{nullptr},
+        pInputImageReorderedCuda{nullptr},
+        pOutputImageCuda{nullptr},
+        pInputMaxSize{0ull},
+        pOutputMaxSize{0ull}
+    {
+        if (mPoseModel == PoseModel::BODY_19N)
+            error("BODY_19N (DenseNet normalisation) is not supported by libopk_hip.", __LINE__,
+                  __FUNCTION__, __FILE__);
+    }
+
+    CvMatToOpInput::~CvMatToOpInput()
+    {
+        opk_ctx* ctx = threadContext();
+        if (pInputImageCuda)
+            opk_free(ctx, pInputImageCuda);
+        if (pOutputImageCuda)
+            opk_free(ctx, pOutputImageCuda);
+    }
+
+    std::vector<Array<float>> CvMatToOpInput::createArray(
+        const Matrix& inputData, const std::vector<double>& scaleInputToNetInputs,
+        const std::vector<Point<int>>& netInputSizes)
+    {
+        // sanity checks of cvMatToOpInput.cpp:68-76
+        if (inputData.empty())
+            error("Wrong input element (empty inputData).", __LINE__, __FUNCTION__, __FILE__);
+        if (inputData.channels() != 3)
+            error("Input images must be 3-channel BGR.", __LINE__, __FUNCTION__, __FILE__);
+        if (scaleInputToNetInputs.size() != netInputSizes.size())
+            error("scaleInputToNetInputs.size() != netInputSizes.size().", __LINE__, __FUNCTION__, __FILE__);
+        opk_ctx* ctx = threadContext();
+        const size_t step = inputData.step1(0);   // bytes per row (uchar)
+        const unsigned long long frameBytes = (unsigned long long)step * inputData.rows();
+        if (pInputMaxSize < frameBytes)
+        {
+            if (pInputImageCuda)
+                opk_free(ctx, pInputImageCuda);
+            void* p = nullptr;
+            check(opk_malloc(ctx, &p, frameBytes), __LINE__, __FUNCTION__);
+            pInputImageCuda = static_cast<unsigned char*>(p);
+            pInputMaxSize = frameBytes;
+        }
+        check(opk_memcpy_h2d(ctx, pInputImageCuda, inputData.dataConst(), frameBytes), __LINE__,
+              __FUNCTION__);
+        std::vector<Array<float>> inputNetData(scaleInputToNetInputs.size());
+        for (auto i = 0u; i < inputNetData.size(); i++)
+        {
+            const auto& size = netInputSizes.at(i);
+            const unsigned long long outBytes = 3ull * size.x * size.y * sizeof(float);
+            if (pOutputMaxSize < outBytes)
+            {
+                if (pOutputImageCuda)
+                    opk_free(ctx, pOutputImageCuda);
+                void* p = nullptr;
+                check(opk_malloc(ctx, &p, outBytes), __LINE__, __FUNCTION__);
+                pOutputImageCuda = static_cast<float*>(p);
+                pOutputMaxSize = outBytes;
+            }
+            check(opk_cvmat_to_input(ctx, pOutputImageCuda, pInputImageCuda, 1, inputData.cols(),
+                                     inputData.rows(), step, scaleInputToNetInputs[i], size.x, size.y, 1),
+                  __LINE__, __FUNCTION__);
+            inputNetData[i].reset({1, 3, size.y, size.x});
+            check(opk_memcpy_d2h(ctx, inputNetData[i].getPtr(), pOutputImageCuda, outBytes), __LINE__,
+                  __FUNCTION__);
+        }
+        return inputNetData;
     }
 }

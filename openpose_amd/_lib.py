@@ -70,6 +70,8 @@ _SIGS = {
     "opk_pose_heatmaps": (_i, [_p, _c.POINTER(_p), _ip]),
     "opk_pose_peaks": (_i, [_p, _c.POINTER(_p), _ip]),
     "opk_pose_scale_net_to_output": (_f, [_p]),
+    "opk_net_load_caffemodel": (_i, [_p, _c.c_char_p, _ip]),
+    "opk_caffemodel_blob": (_i, [_c.c_char_p, _c.c_char_p, _i, _p, _c.c_size_t, _p, _ip]),
     "opk_net_set_timing": (_i, [_p, _i]),
     "opk_net_read_timing": (_i, [_p, _ip, _c.POINTER(_d)]),
     "opk_scale_and_size": (_i, [_i, _i, _i, _i, _f, _i, _d, _c.POINTER(_d), _ip]),

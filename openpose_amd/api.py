@@ -144,6 +144,21 @@ def scale_and_size(input_size, net_resolution=(-1, 368), dynamic_behavior=1.0, s
     return list(scales), [(sizes[2 * i], sizes[2 * i + 1]) for i in range(scale_number)]
 
 
+def caffemodel_blob(path, layer, index):
+    """Host utility: (shape, float32 data) of a blob in a .caffemodel (opk_caffemodel_blob)."""
+    L = _lib.load()
+    shape = (ctypes.c_int64 * 8)()
+    nd = ctypes.c_int()
+    check(L.opk_caffemodel_blob(path.encode(), layer.encode(), index, None, 0, shape,
+                                ctypes.byref(nd)))
+    dims = tuple(shape[i] for i in range(nd.value))
+    out = np.empty(int(np.prod(dims)) if dims else 0, np.float32)
+    check(L.opk_caffemodel_blob(path.encode(), layer.encode(), index,
+                                out.ctypes.data_as(ctypes.c_void_p), out.size, shape,
+                                ctypes.byref(nd)))
+    return dims, out.reshape(dims)
+
+
 def pose_model_info(pose_model):
     """Tables of a PoseModel from libopk_hip: dict(parts, bkg, pairs, map_idx, heat_channels,
     nms_threshold, inter_threshold)."""
@@ -189,11 +204,12 @@ def assemble_people(pair_scores, peaks, pose_model=BODY_25, scale=1.0, max_peopl
 class Net:
     """op::NetCaffe replacement (NetHip): prototxt path or "builtin:BODY_25"."""
 
-    def __init__(self, ctx, prototxt="builtin:BODY_25"):
+    def __init__(self, ctx, prototxt="builtin:BODY_25", caffemodel=None):
         self.ctx = ctx
         self.L = ctx.L
         h = ctypes.c_void_p()
-        check(self.L.opk_net_create(ctx.h, prototxt.encode(), None, ctypes.byref(h)))
+        check(self.L.opk_net_create(ctx.h, prototxt.encode(),
+                                    caffemodel.encode() if caffemodel else None, ctypes.byref(h)))
         self.h = h
         _LIVE["net"].add(self)
 
@@ -239,6 +255,12 @@ class Net:
         n, c, h, w = x.shape
         check(self.L.opk_net_forward(self.h, _ptr(x), n, h, w))
         return self.output()
+
+    def load_caffemodel(self, path):
+        """Trained weights (CopyTrainedLayersFrom semantics); returns the convs loaded."""
+        n = ctypes.c_int()
+        check(self.L.opk_net_load_caffemodel(self.h, path.encode(), ctypes.byref(n)))
+        return n.value
 
     def set_timing(self, on=True):
         check(self.L.opk_net_set_timing(self.h, int(on)))

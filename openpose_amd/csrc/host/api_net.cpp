@@ -6,6 +6,7 @@
 
 #include "../../../include/opk.h"
 #include "net.h"
+#include "caffemodel.h"
 #include "input.h"
 #include "pose.h"
 
@@ -44,14 +45,15 @@ int opk_net_create(opk_ctx* ctx, const char* prototxt, const char* caffemodel, o
 {
     return guarded_net([&] {
         OPK_CHECK_ARG(ctx && prototxt && out, "NULL argument");
-        OPK_CHECK_ARG(caffemodel == nullptr || caffemodel[0] == 0,
-                      "caffemodel loading is not implemented yet: supply weights with "
-                      "opk_net_set_conv");
         const std::string p(prototxt);
         std::vector<opk::LayerDesc> layers =
             p == "builtin:BODY_25" ? opk::builtin_body25() : opk::load_prototxt(p);
-        auto* n = new opk_net{ctx, std::make_unique<opk::NetHip>(ctx, std::move(layers))};
-        *out = n;
+        auto n = std::make_unique<opk_net>(opk_net{ctx, std::make_unique<opk::NetHip>(ctx, std::move(layers))});
+        if (caffemodel && caffemodel[0]) {
+            OPK_CHECK_ARG(ctx->device >= 0, "weights need a device context");
+            n->net->load_caffemodel(caffemodel);
+        }
+        *out = n.release();
     });
 }
 
@@ -265,6 +267,39 @@ int opk_pose_peaks(opk_pose* p, float** peaks, int shape[4])
     return guarded_net([&] {
         OPK_CHECK_ARG(p && peaks && shape, "NULL argument");
         *peaks = p->pose->peaks(shape);
+    });
+}
+
+int opk_net_load_caffemodel(opk_net* net, const char* caffemodel, int* loaded)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net && caffemodel, "NULL argument");
+        OPK_CHECK_ARG(net->ctx->device >= 0, "weights need a device context");
+        const int n = net->net->load_caffemodel(caffemodel);
+        if (loaded) *loaded = n;
+    });
+}
+
+int opk_caffemodel_blob(const char* caffemodel, const char* layer, int index, float* data,
+                        size_t capacity, int64_t* shape, int* ndim)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(caffemodel && layer && ndim, "NULL argument");
+        const auto layers = opk::load_caffemodel(caffemodel);
+        for (const auto& L : layers) {
+            if (L.name != layer) continue;
+            OPK_CHECK_ARG(index >= 0 && index < (int)L.blobs.size(), "no such blob");
+            const auto& b = L.blobs[index];
+            OPK_CHECK_ARG(b.shape.size() <= 8, "blob rank > 8");
+            *ndim = (int)b.shape.size();
+            if (shape) for (size_t i = 0; i < b.shape.size(); ++i) shape[i] = b.shape[i];
+            if (data) {
+                OPK_CHECK_ARG(capacity >= b.data.size(), "capacity too small");
+                std::memcpy(data, b.data.data(), b.data.size() * sizeof(float));
+            }
+            return;
+        }
+        throw opk::Error(1, std::string("layer ") + layer + " has no blobs in " + caffemodel);
     });
 }
 

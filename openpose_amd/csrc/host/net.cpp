@@ -13,6 +13,8 @@
 // Buffers are allocated per input shape (frames x h x w) and kept; borders stay zero.
 #include "net.h"
 
+#include "caffemodel.h"
+
 #include <algorithm>
 #include <cstdlib>
 #include <set>
@@ -74,6 +76,7 @@ void NetHip::plan(const std::vector<LayerDesc>& layers)
                 if ((A.type == "ReLU" || A.type == "PReLU") && A.bottom.size() == 1 &&
                     A.bottom[0] == L.top[0] && A.top.size() == 1 && A.top[0] == L.top[0])
                     c.info.act = A.type == "ReLU" ? 1 : 2;
+                if (c.info.act) c.info.act_layer = A.name;
             }
             if (!c.from_image) convs_reading[L.bottom[0]]++;
             blobs[L.top[0]] = Blob{L.num_output, c.level, (int)convs_.size(), {}};
@@ -471,6 +474,38 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
                             bufs_[p.in_buf].cs, lh_[L + 1], lw_[L + 1], ctx_->stream);
         }
     }
+}
+
+int NetHip::load_caffemodel(const std::string& path)
+{
+    const std::vector<CaffeLayer> layers = opk::load_caffemodel(path);
+    std::map<std::string, const CaffeLayer*> by_name;
+    for (const auto& L : layers) by_name[L.name] = &L;
+    int loaded = 0;
+    for (const ConvInfo& c : info_) {
+        auto it = by_name.find(c.name);
+        if (it == by_name.end()) continue;   // kept as set (Caffe keeps the filler's values)
+        const auto& blobs = it->second->blobs;
+        OPK_CHECK_ARG(blobs.size() == 2, c.name + ": expected weights and bias blobs, got " +
+                                             std::to_string(blobs.size()));
+        const std::vector<int64_t> wshape{c.cout, c.cin, c.k, c.k}, bshape{c.cout};
+        // CopyTrainedLayersFrom's check (net.cpp: "Cannot copy param ... shape mismatch")
+        OPK_CHECK_ARG(blob_shape_is(blobs[0], wshape), "Cannot copy param 0 weights from layer '" +
+                                                           c.name + "'; shape mismatch.");
+        OPK_CHECK_ARG(blob_shape_is(blobs[1], bshape), "Cannot copy param 1 weights from layer '" +
+                                                           c.name + "'; shape mismatch.");
+        const float* slope = nullptr;
+        if (c.act == 2) {
+            auto pt = by_name.find(c.act_layer);
+            OPK_CHECK_ARG(pt != by_name.end() && pt->second->blobs.size() == 1 &&
+                              blob_shape_is(pt->second->blobs[0], bshape),
+                          c.act_layer + ": PReLU slopes missing or of the wrong shape");
+            slope = pt->second->blobs[0].data.data();
+        }
+        set_conv(c.name, blobs[0].data.data(), blobs[1].data.data(), slope);
+        ++loaded;
+    }
+    return loaded;
 }
 
 NetHip::~NetHip()

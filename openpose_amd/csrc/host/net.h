@@ -18,10 +18,15 @@ public:
     struct ConvInfo {
         std::string name;
         int cin, cout, k, act;   // act: 0 none, 1 ReLU, 2 PReLU
+        std::string act_layer;   // the fused ReLU/PReLU layer (holds the PReLU slopes)
     };
     const std::vector<ConvInfo>& convs() const { return info_; }
     void set_conv(const std::string& name, const float* w, const float* b, const float* slope);
     bool ready() const;
+    // caffe::Net::CopyTrainedLayersFrom (netCaffe.cpp:165,185): weights, bias and PReLU slopes of
+    // every conv named in the file (shapes checked as Caffe does); layers the net does not have
+    // are ignored.  Returns the number of convolutions loaded.
+    int load_caffemodel(const std::string& path);
 
     // input: device NCHW fp32 [n][3][h][w].  Every input shape gets its own plan (activation
     // buffers with zeroed guards, launch arguments, net output), kept across forwards, so the

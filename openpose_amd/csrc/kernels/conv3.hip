@@ -152,7 +152,7 @@ void conv3_kernel(const ConvArgs a)
     constexpr int WAVES_N = BN % 64 == 0 ? BN / 64 : 2, WAVES_M = NW / WAVES_N;
     constexpr int WROWS = BM / WAVES_M;            // wave tile WROWS x WN
     constexpr int WN = BN / WAVES_N;
-    static_assert(WROWS % 16 == 0 && WROWS <= 64 && WN % 16 == 0 && WN <= 64, "wave tiles");
+    static_assert(WROWS % 16 == 0 && WROWS <= 128 && WN % 16 == 0 && WN <= 64, "wave tiles");
     static_assert(TAPU == 1 || TAPU == 3, "taps per unit");
     static_assert(KS == 3 || (KS == 1 && TAPU == 1 && HR == BM), "1x1: one tap, halo = tile");
     constexpr int MF = WROWS / 16, NF = WN / 16;
@@ -252,7 +252,8 @@ void conv3_kernel(const ConvArgs a)
             mv[j_] = a.act == 2 ? sl_ : float4_t{neg, neg, neg, neg};                         \
         }                                                                                     \
     } while (0)
-    constexpr bool BIAS_EARLY = MINB == 1 && NW == 8;   // registers to spare across the K loop
+    // registers to spare across the K loop
+    constexpr bool BIAS_EARLY = MINB == 1 && NW == 8 && MF * NF <= 16;
     if constexpr (BIAS_EARLY) OPK3_BIAS();
 
     OPK3_ISSUE(0);
@@ -669,6 +670,8 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
     // +10-17 % on the 92x164 / 184x328 / 512-channel layers, -20 % at one tile per CU)
     const long tiles = ((long)frames * (H + 2) * (W + 2) / 256) * ((cout + s.bn - 1) / s.bn);
     s.nw = 8;
+    // (measured, round 1: 4-wave 256x128 two-per-CU tiles and 8-wave 512x128 tiles of 128x64
+    // wave tiles were both slower than these on every BODY_25 layer)
     if (s.bn != 64 && big16 && tiles >= 3 * 256) {   // 512 x {128,96} tiles, 16 waves
         s.persist = env_int("OPK_CONV3_PERSIST", 1) != 0;
         // the persistent kernel keeps bias/slopes in LDS: 688 halo rows (strips <= 85 columns)
