@@ -141,6 +141,21 @@ int opk_connect_body_parts_semantics(opk_ctx* ctx, float* keypoints_host, float*
                                      float default_nms_threshold, float scale_factor,
                                      int maximize_positives, int semantics);
 
+/* ---- Keypoint post-steps (host arrays [people][parts][3]).
+ * opk_scale_keypoints replaces op::KeypointScaler::scale (src/openpose/core/keypointScaler.cpp:64-95;
+ * getScaleAndOffset :6-45): scale_mode = op::ScaleMode (0 InputResolution = unchanged,
+ * 1 NetOutputResolution, 2 OutputResolution, 3/4 ZeroToOne(FixedAspect), 5/6 PlusMinusOne(...)).
+ * opk_keep_top_n_people replaces op::KeepTopNPeople::keepTopPeople (keepTopNPeople.cpp:16-86,
+ * --number_people_max): people ranked by score * sqrt(keypoint box area) and the top max_people
+ * kept in their original order; *out_people = rows written (people itself when no cut is needed),
+ * out_index_host (may be NULL) = source person of each row. */
+int opk_scale_keypoints(float* keypoints_host, int people, int parts, int scale_mode,
+                        double scale_input_to_output, double scale_net_to_output, int producer_w,
+                        int producer_h);
+int opk_keep_top_n_people(const float* keypoints_host, int people, int parts,
+                          const float* scores_host, int max_people, float* out_keypoints_host,
+                          int* out_index_host, int* out_people);
+
 /* Pose tables (getPoseNumberBodyParts, addBkgChannel, getPosePartPairs, getPoseMapIndex;
  * poseParameters.hpp:17-34).  Any output pointer may be NULL; pairs gets 2*npairs entries,
  * map_idx the model's map-index entries (heat_channels - parts - bkg). */
@@ -279,6 +294,20 @@ int opk_pose_keypoints(opk_pose* pose, int frame, float* keypoints_host, float* 
 int opk_pose_heatmaps(opk_pose* pose, float** heat_dev, int shape[4]);
 int opk_pose_peaks(opk_pose* pose, float** peaks_dev, int shape[4]);
 float opk_pose_scale_net_to_output(opk_pose* pose);
+/* PoseExtractorNet::getHeatMapsCopy (src/openpose/pose/poseExtractorNet.cpp:106-244) for every
+ * frame of the last collected batch: types = OPK_HEATMAP_* bits (copied in the order parts,
+ * background, PAFs, as --heatmaps_add_parts/_bkg/_PAFs), scale_mode = op::ScaleMode
+ * (include/openpose/core/enumClasses.hpp:6-17; --heatmaps_scale: 5 PlusMinusOne, 3 ZeroToOne,
+ * 7 UnsignedChar, 8 NoScale).  dst_dev [n][channels][H][W] device, or NULL to get the shape. */
+#define OPK_HEATMAP_PARTS 1
+#define OPK_HEATMAP_BACKGROUND 2
+#define OPK_HEATMAP_PAFS 4
+int opk_pose_heatmaps_copy(opk_pose* pose, int types, int scale_mode, float* dst_dev,
+                           int shape[4]);
+/* PoseExtractorNet::getCandidatesCopy (poseExtractorNet.cpp:246-282) of one collected frame:
+ * candidates_host [parts][127][3] (x, y in output pixels = net pixels * scaleNetToOutput, score),
+ * counts_host [parts]; either may be NULL. */
+int opk_pose_candidates(opk_pose* pose, int frame, float* candidates_host, int* counts_host);
 
 #ifdef __cplusplus
 }

@@ -74,6 +74,10 @@ _SIGS = {
     "opk_caffemodel_blob": (_i, [_c.c_char_p, _c.c_char_p, _i, _p, _c.c_size_t, _p, _ip]),
     "opk_net_set_timing": (_i, [_p, _i]),
     "opk_net_read_timing": (_i, [_p, _ip, _c.POINTER(_d)]),
+    "opk_pose_heatmaps_copy": (_i, [_p, _i, _i, _p, _ip]),
+    "opk_pose_candidates": (_i, [_p, _i, _p, _ip]),
+    "opk_scale_keypoints": (_i, [_p, _i, _i, _i, _d, _d, _i, _i]),
+    "opk_keep_top_n_people": (_i, [_p, _i, _i, _p, _i, _p, _p, _ip]),
     "opk_scale_and_size": (_i, [_i, _i, _i, _i, _f, _i, _d, _c.POINTER(_d), _ip]),
     "opk_cvmat_to_input": (_i, [_p, _p, _p, _i, _i, _i, _c.c_size_t, _d, _i, _i, _i]),
     "opk_pose_set_input": (_i, [_p, _i, _i, _f, _i, _d]),

@@ -144,6 +144,32 @@ def scale_and_size(input_size, net_resolution=(-1, 368), dynamic_behavior=1.0, s
     return list(scales), [(sizes[2 * i], sizes[2 * i + 1]) for i in range(scale_number)]
 
 
+def scale_keypoints(keypoints, scale_mode, scale_input_to_output=1.0, scale_net_to_output=1.0,
+                    producer_size=(1, 1)):
+    """op::KeypointScaler::scale on a copy of keypoints [people, parts, 3]."""
+    kp = np.ascontiguousarray(keypoints, np.float32).copy()
+    check(_lib.load().opk_scale_keypoints(kp.ctypes.data_as(ctypes.c_void_p), kp.shape[0],
+                                          kp.shape[1], scale_mode, float(scale_input_to_output),
+                                          float(scale_net_to_output), producer_size[0],
+                                          producer_size[1]))
+    return kp
+
+
+def keep_top_n_people(keypoints, scores, max_people):
+    """op::KeepTopNPeople::keepTopPeople: (kept keypoints, source index of each kept row)."""
+    kp = np.ascontiguousarray(keypoints, np.float32)
+    sc = np.ascontiguousarray(scores, np.float32)
+    rows = max(kp.shape[0], max_people, 1)
+    out = np.zeros((rows,) + kp.shape[1:], np.float32)
+    idx = np.full(rows, -1, np.int32)
+    n = ctypes.c_int()
+    check(_lib.load().opk_keep_top_n_people(kp.ctypes.data_as(ctypes.c_void_p), kp.shape[0],
+                                            kp.shape[1], sc.ctypes.data_as(ctypes.c_void_p),
+                                            max_people, out.ctypes.data_as(ctypes.c_void_p),
+                                            idx.ctypes.data_as(ctypes.c_void_p), ctypes.byref(n)))
+    return out[:n.value], idx[:n.value]
+
+
 def caffemodel_blob(path, layer, index):
     """Host utility: (shape, float32 data) of a blob in a .caffemodel (opk_caffemodel_blob)."""
     L = _lib.load()
@@ -432,6 +458,23 @@ class PoseExtractor:
 
     def heatmaps_numpy(self):
         return self._dev_array(self.L.opk_pose_heatmaps)
+
+    def heatmaps_copy(self, types=7, scale_mode=8):
+        """getHeatMapsCopy for every frame of the last batch: [n, channels, H, W] float32 numpy
+        (types bits: 1 parts, 2 background, 4 PAFs; scale_mode: op::ScaleMode value)."""
+        shape = (ctypes.c_int * 4)()
+        check(self.L.opk_pose_heatmaps_copy(self.h, types, scale_mode, None, shape))
+        dev = torch.empty(tuple(shape), dtype=torch.float32, device="cuda")
+        check(self.L.opk_pose_heatmaps_copy(self.h, types, scale_mode, _ptr(dev), shape))
+        return dev.cpu().numpy()
+
+    def candidates(self, frame):
+        """getCandidatesCopy: list over parts of [count, 3] arrays (x, y output pixels, score)."""
+        out = np.zeros((self.parts, 127, 3), np.float32)
+        counts = np.zeros(self.parts, np.int32)
+        check(self.L.opk_pose_candidates(self.h, frame, out.ctypes.data_as(ctypes.c_void_p),
+                                         counts.ctypes.data_as(ctypes.POINTER(ctypes.c_int))))
+        return [out[p, :counts[p]].copy() for p in range(self.parts)]
 
     def peaks_numpy(self):
         return self._dev_array(self.L.opk_pose_peaks)

@@ -7,6 +7,7 @@
 #include "../../../include/opk.h"
 #include "connector.h"
 #include "context.h"
+#include "output.h"
 
 namespace opk {
 
@@ -318,6 +319,27 @@ int opk_connect_body_parts_semantics(opk_ctx* ctx, float* kp_out, float* ks_out,
         const int w = std::min(n, max_people);
         if (w > 0 && kp_out) std::memcpy(kp_out, kp.data(), sizeof(float) * (size_t)w * m.parts * 3);
         if (w > 0 && ks_out) std::memcpy(ks_out, ks.data(), sizeof(float) * w);
+    });
+}
+
+int opk_scale_keypoints(float* keypoints_host, int people, int parts, int scale_mode,
+                        double scale_input_to_output, double scale_net_to_output, int producer_w,
+                        int producer_h)
+{
+    return guarded([&] {
+        opk::scale_keypoints(keypoints_host, people, parts, scale_mode, scale_input_to_output,
+                             scale_net_to_output, producer_w, producer_h);
+    });
+}
+
+int opk_keep_top_n_people(const float* keypoints_host, int people, int parts,
+                          const float* scores_host, int max_people, float* out_keypoints_host,
+                          int* out_index_host, int* out_people)
+{
+    return guarded([&] {
+        const int n = opk::keep_top_n_people(keypoints_host, people, parts, scores_host, max_people,
+                                             out_keypoints_host, out_index_host);
+        if (out_people) *out_people = n;
     });
 }
 

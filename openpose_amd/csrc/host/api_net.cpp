@@ -376,6 +376,22 @@ int opk_pose_net_input(opk_pose* p, int scale, const float** input_dev, int* net
     });
 }
 
+int opk_pose_heatmaps_copy(opk_pose* p, int types, int scale_mode, float* dst_dev, int shape[4])
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p && shape, "NULL argument");
+        p->pose->heatmaps_copy(types, scale_mode, dst_dev, shape);
+    });
+}
+
+int opk_pose_candidates(opk_pose* p, int frame, float* candidates_host, int* counts_host)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->candidates(frame, candidates_host, counts_host);
+    });
+}
+
 float opk_pose_scale_net_to_output(opk_pose* p) { return p ? p->pose->scale_net_to_output() : 0.f; }
 
 }  // extern "C"

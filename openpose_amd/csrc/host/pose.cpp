@@ -89,6 +89,59 @@ float* PoseHip::heatmaps(int shape[4])
     return static_cast<float*>(heat_.ptr);
 }
 
+void PoseHip::heatmaps_copy(int types, int scale_mode, float* dst, int shape[4])
+{
+    OPK_CHECK_ARG(types > 0 && types < 8, "heat-map types: bits 0 parts, 1 background, 2 PAFs");
+    OPK_CHECK_ARG(scale_mode >= 0 && scale_mode <= 8, "unknown ScaleMode");
+    const PoseModelInfo& m = pose_model(model_);
+    std::vector<int> sel, kind;
+    if (types & 1)
+        for (int c = 0; c < m.parts; ++c) { sel.push_back(c); kind.push_back(0); }
+    if (types & 2) {
+        OPK_CHECK_ARG(m.bkg, "You enabled `--heatmaps_add_bkg` for a model that does not contain one. "
+                             "Please, remove this flag for this model.");
+        sel.push_back(m.parts);
+        kind.push_back(0);
+    }
+    if (types & 4)
+        for (int c = 0; c < 2 * m.npairs(); ++c) {
+            sel.push_back(m.parts + (m.bkg ? 1 : 0) + c);
+            kind.push_back(1);
+        }
+    int hs[4];
+    float* heat = heatmaps(hs);   // materialised once per collected batch
+    shape[0] = hs[0]; shape[1] = (int)sel.size(); shape[2] = hs[2]; shape[3] = hs[3];
+    if (!dst) return;
+    sel.insert(sel.end(), kind.begin(), kind.end());
+    int* dsel = static_cast<int*>(heat_sel_.get(sel.size() * sizeof(int)));
+    OPK_HIP(hipMemcpyAsync(dsel, sel.data(), sel.size() * sizeof(int), hipMemcpyHostToDevice,
+                           ctx_->stream));
+    launch_heat_copy(dst, heat, dsel, shape[1], hs[0], hs[1], (size_t)hs[2] * hs[3], scale_mode,
+                     ctx_->stream);
+    OPK_HIP(hipStreamSynchronize(ctx_->stream));   // `sel` dies at return
+}
+
+void PoseHip::candidates(int frame, float* out, int* counts) const
+{
+    OPK_CHECK_ARG(last_ >= 0, "no collected batch");
+    OPK_CHECK_ARG(frame >= 0 && frame < n_, "bad frame");
+    const PoseModelInfo& m = pose_model(model_);
+    const size_t area = (size_t)(kMaxPeaks + 1) * 3;
+    const float* p = static_cast<const float*>(slots_[last_].hpeaks.ptr) + (size_t)frame * m.parts * area;
+    for (int part = 0; part < m.parts; ++part) {
+        const float* pp = p + part * area;
+        const int count = (int)std::round(pp[0]);
+        if (counts) counts[part] = count;
+        if (!out) continue;
+        for (int c = 0; c < count; ++c) {
+            float* o = out + ((size_t)part * kMaxPeaks + c) * 3;
+            o[0] = pp[3 + 3 * c] * scale_net_to_output_;
+            o[1] = pp[3 + 3 * c + 1] * scale_net_to_output_;
+            o[2] = pp[3 + 3 * c + 2];
+        }
+    }
+}
+
 float* PoseHip::peaks(int shape[4]) const
 {
     OPK_CHECK_ARG(last_ >= 0, "no collected batch");

@@ -57,6 +57,13 @@ public:
     // later batch is in flight (its net forward overwrites the net output)
     float* heatmaps(int shape[4]);
     float* peaks(int shape[4]) const;
+    // PoseExtractorNet::getHeatMapsCopy (poseExtractorNet.cpp:106-244) for every frame of the last
+    // collected batch: types bit 0 parts, bit 1 background, bit 2 PAFs (in that order), scale_mode
+    // an op::ScaleMode value; dst [n][channels of the types][H][W] device (NULL: shape only)
+    void heatmaps_copy(int types, int scale_mode, float* dst, int shape[4]);
+    // PoseExtractorNet::getCandidatesCopy (:246-282): peaks of one frame, x/y * scaleNetToOutput;
+    // out [parts][kMaxPeaks][3], counts [parts]
+    void candidates(int frame, float* out, int* counts) const;
     float scale_net_to_output() const { return scale_net_to_output_; }
     int model() const { return model_; }
 
@@ -102,7 +109,7 @@ private:
     float scale_net_to_output_ = 1.f;
     int n_ = 0, hh_ = 0, hw_ = 0;
     bool heat_valid_ = false;
-    DevBuf heat_;
+    DevBuf heat_, heat_sel_;
     std::vector<int> people_;
     std::vector<std::vector<float>> kp_, ks_;
 };

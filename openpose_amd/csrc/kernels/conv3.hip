@@ -208,7 +208,8 @@ void conv3_kernel(const ConvArgs a)
 #define OPK3_ISSUE(u_)                                                                        \
     do {                                                                                      \
         const int c_ = (u_) / UPC;                                                            \
-        if ((u_) - c_ * UPC == 0) {                                                           \
+        /* dev probe only: 6 = no halo DMA, 7 = no weight DMA after the prologue */           \
+        if ((u_) - c_ * UPC == 0 && (OPK3_ABLATE != 6 || (u_) < 2)) {                        \
             const int as_ = (c_ % NAS) * ASLOT;                                               \
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
                 if (API % NW == 0 || i_ * NW + wave < API)                                    \
@@ -220,7 +221,7 @@ void conv3_kernel(const ConvArgs a)
         const int bs_ = NAS * ASLOT + ((u_) % 3) * BSLOT;                                     \
         const uint16_t* ub_ = wbase + (size_t)(u_) * BROWS * 32;                              \
         _Pragma("unroll") for (int j_ = 0; j_ < (BPI + NW - 1) / NW; ++j_) {                  \
-            if (BPI % NW == 0 || j_ * NW + wave < BPI) {                                      \
+            if ((BPI % NW == 0 || j_ * NW + wave < BPI) && (OPK3_ABLATE != 7 || (u_) < 2)) {  \
                 const int rb_ = (j_ * NW + wave) * 16 + lrow;                                 \
                 const int lp_ = phys ^ (((rb_ >> 2) & 1) << 1);                               \
                 __builtin_amdgcn_global_load_lds(                                             \

@@ -80,5 +80,9 @@ void launch_cvmat_to_input(float* dst, const uint8_t* src, int n, int sh, int sw
 
 // ---- elementwise helpers (misc.hip) -----------------------------------------------------------
 void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stream);
+// getHeatMapsCopy: dst [frames][nsel][hw] from heat [frames][channels][hw]; sel_dev = nsel source
+// channels then nsel kinds (0 part/background, 1 PAF); scale_mode = op::ScaleMode value
+void launch_heat_copy(float* dst, const float* heat, const int* sel_dev, int nsel, int frames,
+                      int channels, size_t hw, int scale_mode, hipStream_t stream);
 
 }  // namespace opk
