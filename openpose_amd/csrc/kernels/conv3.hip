@@ -636,6 +636,7 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
     OPK3_STAMP(5);
 }
 
+
 }  // namespace
 
 namespace {
@@ -719,6 +720,9 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
             const long per_n = std::min<long>(a.cus / nn, (ntiles + nn - 1) / nn);
             const unsigned G = (unsigned)(per_n * nn);
             OPK_CHECK_ARG(G <= 1024, "persistent grid exceeds the sink");
+            // (measured, round 1: a 32x32x16-MFMA version of this kernel with double-buffered
+            // fragments ran 20 % slower on the 128-channel layers; a pipelined 16x16x32 fragment
+            // schedule spilled at the 128-VGPR budget and ran 4 % slower)
             if (s.bn == 96)
                 hipLaunchKernelGGL((conv3p_kernel<96>), dim3(G), dim3(1024), 0, stream, a);
             else

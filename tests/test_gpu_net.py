@@ -122,6 +122,7 @@ def test_conv1_fused_matches_unfused(ctx, hw, acts):
 
 VARIANTS = {"persistent": {}, "w16": {"OPK_CONV3_PERSIST": "0"},
             "w8": {"OPK_CONV3_W16": "0"}, "w8_one_per_cu": {"OPK_CONV3_W16": "0", "OPK_CONV3_SMALL": "0"}}
+ROUNDING_VARIANTS = set()   # variants with another MFMA shape (another fp32 summation order)
 
 
 def test_conv3_tile_variants_bit_identical(ctx):
@@ -159,6 +160,9 @@ def test_conv3_tile_variants_bit_identical(ctx):
         os.unlink(path)
     assert np.isfinite(outs["w8"]).all() and np.abs(outs["w8"]).max() > 0
     for name in VARIANTS:
+        if name in ROUNDING_VARIANTS:   # other MFMA shape: another fp32 summation order
+            assert rel_l2(outs[name], outs["w8"]) < 1e-3, name
+            continue
         np.testing.assert_array_equal(outs[name], outs["w8"], err_msg=name)
     # and the fp32 torch restatement of the same graph agrees within the fp16 tolerance
     ref = torch_forward(graph, params, x)
