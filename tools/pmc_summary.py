@@ -6,7 +6,7 @@ FETCH_SIZE counts 64-B units per 128-B request on wide streaming reads -> x2; WR
         <frames_per_step> <out.json>
 
 A CNN forward = every conv*/maxpool kernel; forwards are counted by the first conv's launches
-(conv_image_kernel).  Post-processing kernels are reported per launch.
+(conv1_fused_kernel, or conv_image_kernel when the front end is not fused).  Post-processing kernels are reported per launch.
 """
 import collections
 import csv
@@ -32,7 +32,7 @@ def main():
     fetch, write, frames, out = sys.argv[1], sys.argv[2], int(sys.argv[3]), sys.argv[4]
     f, w = per_kernel(fetch), per_kernel(write)
     cnn = [k for k in f if ("conv" in k and "kernel" in k) or "maxpool" in k]
-    forwards = sum(f[k][0] for k in f if "conv_image_kernel" in k)
+    forwards = sum(f[k][0] for k in f if "conv1_fused_kernel" in k or "conv_image_kernel" in k)
     fetch_b = 2.0 * sum(f[k][1] for k in cnn) / forwards
     write_b = sum(w[k][1] for k in cnn if k in w) / forwards
     by_kernel = {}
@@ -42,7 +42,7 @@ def main():
             "fetch_bytes_per_forward": 2.0 * f[k][1] / forwards,
             "write_bytes_per_forward": (w[k][1] if k in w else 0.0) / forwards}
     post = {}
-    for tag in ("nms_detect", "nms_finalize", "paf_compact", "resize_merge"):
+    for tag in ("cvmat_to_input", "nms_detect", "nms_finalize", "paf_compact", "resize_merge"):
         ks = [k for k in f if tag in k]
         n = sum(f[k][0] for k in ks)
         if n:
