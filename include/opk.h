@@ -183,7 +183,11 @@ int opk_cvmat_to_input(opk_ctx* ctx, float* input_dev, const uint8_t* frames_dev
                        int height, size_t step, double scale, int net_w, int net_h, int normalize);
 
 /* ---- Net: replaces op::Net / op::NetCaffe (include/openpose/net/net.hpp:8-18,
- *      netCaffe.hpp:12-13).  prototxt: a Caffe prototxt path, or "builtin:BODY_25". */
+ *      netCaffe.hpp:12-13).  prototxt: a Caffe prototxt path, or one of the reference's networks
+ *      generated in the library: "builtin:BODY_25", "builtin:COCO_18", "builtin:MPI_15",
+ *      "builtin:MPI_15_4", "builtin:HAND", "builtin:FACE" (models/.../pose_deploy*.prototxt).
+ *      Supported layers: Convolution 3x3/pad 1, 7x7/pad 3, 1x1; ReLU/PReLU in place after a conv;
+ *      MaxPool 2x2/2; channel Concat; the output blob is a Concat or a conv's top. */
 typedef struct opk_net opk_net;
 /* caffemodel (or NULL): trained weights, loaded as caffe::Net::CopyTrainedLayersFrom does
  * (netCaffe.cpp:163-185): every conv whose name is in the file gets its weights, bias and the

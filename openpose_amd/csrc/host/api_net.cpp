@@ -47,7 +47,7 @@ int opk_net_create(opk_ctx* ctx, const char* prototxt, const char* caffemodel, o
         OPK_CHECK_ARG(ctx && prototxt && out, "NULL argument");
         const std::string p(prototxt);
         std::vector<opk::LayerDesc> layers =
-            p == "builtin:BODY_25" ? opk::builtin_body25() : opk::load_prototxt(p);
+            p.rfind("builtin:", 0) == 0 ? opk::builtin_graph(p) : opk::load_prototxt(p);
         auto n = std::make_unique<opk_net>(opk_net{ctx, std::make_unique<opk::NetHip>(ctx, std::move(layers))});
         if (caffemodel && caffemodel[0]) {
             OPK_CHECK_ARG(ctx->device >= 0, "weights need a device context");

@@ -230,4 +230,140 @@ std::vector<LayerDesc> builtin_body25()
     return L;
 }
 
+namespace {
+struct GraphBuilder {
+    std::vector<LayerDesc> L;
+    void conv(const std::string& name, const std::string& bottom, int cout, int k,
+              const std::string& relu, const std::string& top = "")
+    {
+        LayerDesc d;
+        d.name = name; d.type = "Convolution"; d.bottom = {bottom}; d.top = {top.empty() ? name : top};
+        d.num_output = cout; d.kernel_size = k; d.pad = k / 2;
+        L.push_back(d);
+        if (relu.empty()) return;
+        LayerDesc a;
+        a.type = "ReLU"; a.name = relu; a.bottom = d.top; a.top = d.top;
+        L.push_back(a);
+    }
+    void pool(const std::string& name, const std::string& bottom)
+    {
+        LayerDesc d;
+        d.name = name; d.type = "Pooling"; d.bottom = {bottom}; d.top = {name};
+        d.kernel_size = 2; d.stride = 2;
+        L.push_back(d);
+    }
+    void concat(const std::string& name, const std::vector<std::string>& bottoms,
+                const std::string& top = "")
+    {
+        LayerDesc d;
+        d.name = name; d.type = "Concat"; d.bottom = bottoms; d.top = {top.empty() ? name : top};
+        L.push_back(d);
+    }
+    // VGG-19 front of every CPM net: conv1_1 .. conv4_2 (pool names differ per model)
+    void vgg(const std::string& p1, const std::string& p2, const std::string& p3,
+             const std::string& relu_suffix_style)
+    {
+        auto r = [&](const std::string& c) {
+            return relu_suffix_style == "re" ? c + "_re" : "relu" + c.substr(4);
+        };
+        conv("conv1_1", "image", 64, 3, r("conv1_1"));
+        conv("conv1_2", "conv1_1", 64, 3, r("conv1_2"));
+        pool(p1, "conv1_2");
+        conv("conv2_1", p1, 128, 3, r("conv2_1"));
+        conv("conv2_2", "conv2_1", 128, 3, r("conv2_2"));
+        pool(p2, "conv2_2");
+        conv("conv3_1", p2, 256, 3, r("conv3_1"));
+        conv("conv3_2", "conv3_1", 256, 3, r("conv3_2"));
+        conv("conv3_3", "conv3_2", 256, 3, r("conv3_3"));
+        conv("conv3_4", "conv3_3", 256, 3, r("conv3_4"));
+        pool(p3, "conv3_4");
+        conv("conv4_1", p3, 512, 3, r("conv4_1"));
+        conv("conv4_2", "conv4_1", 512, 3, r("conv4_2"));
+    }
+};
+}  // namespace
+
+std::vector<LayerDesc> builtin_cpm_pose(int pafs, int heat, int stages)
+{
+    // models/pose/{coco,mpi}/pose_deploy_linevec*.prototxt: VGG front, conv4_3_CPM / conv4_4_CPM,
+    // a 3x3 stage 1 and 7x7 stages 2..N, two branches (L1 PAFs, L2 heat maps) interleaved layer by
+    // layer; net_output = concat(L2, L1)
+    GraphBuilder g;
+    g.vgg("pool1_stage1", "pool2_stage1", "pool3_stage1", "relu");
+    g.conv("conv4_3_CPM", "conv4_2", 256, 3, "relu4_3_CPM");
+    g.conv("conv4_4_CPM", "conv4_3_CPM", 128, 3, "relu4_4_CPM");
+    const char* br[2] = {"L1", "L2"};
+    for (int j = 1; j <= 5; ++j)
+        for (const char* b : br) {
+            const std::string nm = "conv5_" + std::to_string(j) + "_CPM_" + b;
+            const std::string in = j == 1 ? "conv4_4_CPM" : "conv5_" + std::to_string(j - 1) + "_CPM_" + b;
+            const int cout = j <= 3 ? 128 : (j == 4 ? 512 : (b[1] == '1' ? pafs : heat));
+            g.conv(nm, in, cout, j <= 3 ? 3 : 1, j == 5 ? "" : "relu5_" + std::to_string(j) + "_CPM_" + b);
+        }
+    std::string l1 = "conv5_5_CPM_L1", l2 = "conv5_5_CPM_L2";
+    for (int s = 2; s <= stages; ++s) {
+        const std::string st = "stage" + std::to_string(s);
+        const std::string cat = "concat_" + st;
+        g.concat(cat, {l1, l2, "conv4_4_CPM"});
+        for (int j = 1; j <= 7; ++j)
+            for (const char* b : br) {
+                const std::string nm = "Mconv" + std::to_string(j) + "_" + st + "_" + b;
+                const std::string in = j == 1 ? cat : "Mconv" + std::to_string(j - 1) + "_" + st + "_" + b;
+                const int cout = j <= 6 ? 128 : (b[1] == '1' ? pafs : heat);
+                g.conv(nm, in, cout, j <= 5 ? 7 : 1,
+                       j == 7 ? "" : "Mrelu" + std::to_string(j) + "_" + st + "_" + b);
+            }
+        l1 = "Mconv7_" + st + "_L1";
+        l2 = "Mconv7_" + st + "_L2";
+    }
+    g.concat("concat_stage7", {l2, l1}, "net_output");
+    return g.L;
+}
+
+std::vector<LayerDesc> builtin_cpm_single(int outputs, bool face)
+{
+    // models/{hand,face}/pose_deploy.prototxt: VGG front to conv5_2, conv5_3_CPM, a 1x1 stage 1,
+    // five 7x7 stages on concat(previous, conv5_3_CPM); the last conv's top is net_output
+    GraphBuilder g;
+    if (face) g.vgg("pool1", "pool2", "pool3", "re");
+    else g.vgg("pool1_stage1", "pool2_stage1", "pool3_stage1", "relu");
+    auto r = [&](const std::string& c, const std::string& hand_name) {
+        return face ? c + "_re" : hand_name;
+    };
+    g.conv("conv4_3", "conv4_2", 512, 3, r("conv4_3", "relu4_3"));
+    g.conv("conv4_4", "conv4_3", 512, 3, r("conv4_4", "relu4_4"));
+    g.conv("conv5_1", "conv4_4", 512, 3, r("conv5_1", "relu5_1"));
+    g.conv("conv5_2", "conv5_1", 512, 3, r("conv5_2", "relu5_2"));
+    g.conv("conv5_3_CPM", "conv5_2", 128, 3, r("conv5_3_CPM", "relu5_4_stage1_3"));
+    g.conv("conv6_1_CPM", "conv5_3_CPM", 512, 1, r("conv6_1_CPM", "relu6_4_stage1_1"));
+    g.conv("conv6_2_CPM", "conv6_1_CPM", outputs, 1, "");
+    std::string prev = "conv6_2_CPM";
+    for (int s = 2; s <= 6; ++s) {
+        const std::string st = "stage" + std::to_string(s);
+        const std::string cat = face ? "features_in_stage_" + std::to_string(s) : "concat_" + st;
+        g.concat(cat, {prev, "conv5_3_CPM"});
+        for (int j = 1; j <= 7; ++j) {
+            const std::string nm = "Mconv" + std::to_string(j) + "_" + st;
+            const std::string in = j == 1 ? cat : "Mconv" + std::to_string(j - 1) + "_" + st;
+            const std::string relu = j == 7 ? "" : r(nm, "Mrelu1_" + std::to_string(j + 1) + "_" + st + "_" + std::to_string(j));
+            g.conv(nm, in, j <= 6 ? 128 : outputs, j <= 5 ? 7 : 1, relu,
+                   (j == 7 && s == 6) ? "net_output" : "");
+        }
+        prev = "Mconv7_" + st;
+    }
+    return g.L;
+}
+
+std::vector<LayerDesc> builtin_graph(const std::string& name)
+{
+    if (name == "builtin:BODY_25") return builtin_body25();
+    if (name == "builtin:COCO_18") return builtin_cpm_pose(38, 19, 6);
+    if (name == "builtin:MPI_15") return builtin_cpm_pose(28, 16, 6);
+    if (name == "builtin:MPI_15_4") return builtin_cpm_pose(28, 16, 4);
+    if (name == "builtin:HAND") return builtin_cpm_single(22, false);
+    if (name == "builtin:FACE") return builtin_cpm_single(71, true);
+    throw Error(1, "unknown builtin graph " + name +
+                       " (BODY_25, COCO_18, MPI_15, MPI_15_4, HAND, FACE)");
+}
+
 }  // namespace opk

@@ -38,6 +38,7 @@ NetHip::NetHip(Context* ctx, std::vector<LayerDesc> layers, const std::string& o
     const char* v = std::getenv("OPK_CONV_V1");   // A/B switch to the v1 kernel (dev only)
     conv_v1_ = v && v[0] == '1';
     plan(layers);
+    conv_v1_ = conv_v1_ && border_ == 1;   // the v1 kernels know 1-pixel borders only
     if (ctx_->device >= 0) {
         ctx_->bind();
         OPK_HIP(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, ctx_->device));
@@ -61,8 +62,10 @@ void NetHip::plan(const std::vector<LayerDesc>& layers)
             auto it = blobs.find(L.bottom[0]);
             OPK_CHECK_ARG(it != blobs.end(), L.name + ": unknown bottom " + L.bottom[0]);
             OPK_CHECK_ARG(L.stride == 1, L.name + ": only stride 1 convolutions");
-            OPK_CHECK_ARG((L.kernel_size == 3 && L.pad == 1) || (L.kernel_size == 1 && L.pad == 0),
-                          L.name + ": only 3x3/pad1 and 1x1/pad0 convolutions");
+            OPK_CHECK_ARG((L.kernel_size == 3 && L.pad == 1) || (L.kernel_size == 1 && L.pad == 0) ||
+                              (L.kernel_size == 7 && L.pad == 3),
+                          L.name + ": only 3x3/pad 1, 7x7/pad 3 and 1x1/pad 0 convolutions");
+            border_ = std::max(border_, L.kernel_size / 2);
             ConvPlan c;
             c.info = ConvInfo{L.name, it->second.ch, L.num_output, L.kernel_size, 0};
             c.in_blob = L.bottom[0];
@@ -115,7 +118,16 @@ void NetHip::plan(const std::vector<LayerDesc>& layers)
             throw Error(4, "layer type " + L.type + " (" + L.name + ") not supported by NetHip");
         }
     }
-    OPK_CHECK_ARG(out_concat != nullptr, "output blob " + output_blob_ + " not produced by a Concat");
+    // the output blob is a Concat of convs (the pose nets) or one conv's top (hand / face nets)
+    if (!out_concat) {
+        auto it = blobs.find(output_blob_);
+        OPK_CHECK_ARG(it != blobs.end() && it->second.conv >= 0,
+                      "output blob " + output_blob_ + " not produced by a Concat or a Convolution");
+        ConvPlan& c = convs_[it->second.conv];
+        c.out32_coff = 0;
+        out_level_ = it->second.level;
+        out_c_ = it->second.ch;
+    }
 
     // pass 2: concat buffers and placements
     for (const auto& L : layers) {
@@ -182,7 +194,7 @@ void NetHip::plan(const std::vector<LayerDesc>& layers)
         } else {
             const Blob& B = blobs[c.in_blob];
             c.cin_pad = round_up(B.ch, 32);
-            c.ntaps = c.info.k == 3 ? 9 : 1;
+            c.ntaps = c.info.k * c.info.k;
             bool found = false;
             for (const auto& p : B.places)
                 if (p.coff % 8 == 0 && p.coff + c.cin_pad <= bufs_[p.buf].cs) {
@@ -231,9 +243,12 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
     OPK_CHECK_ARG(c.info.act != 2 || slope, name + ": PReLU slopes required");
     const int K = c.ksteps * kConvBK;
     const int cin = c.info.cin, k = c.info.k;
-    std::vector<uint16_t> packed((size_t)c.cout_pad * K, 0);
+    // the v1/v2 kernels (dev fallbacks) take 1x1 / 3x3 convolutions on 1-pixel borders only
+    const bool legacy = k != 7 && border_ == 1;
+    const bool need_packed = legacy || c.from_image;   // conv_image reads this layout too
+    std::vector<uint16_t> packed(need_packed ? (size_t)c.cout_pad * K : 0, 0);
     auto f2h = [](float v) { _Float16 h = (_Float16)v; return __builtin_bit_cast(uint16_t, h); };
-    for (int co = 0; co < c.info.cout; ++co) {
+    for (int co = 0; co < c.info.cout && need_packed; ++co) {
         uint16_t* dst = packed.data() + (size_t)co * K;
         if (c.from_image) {   // K index (ky*3 + kx)*3 + ci, matching launch_im2col3
             for (int ci = 0; ci < 3; ++ci)
@@ -251,7 +266,7 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
     // conv3.hip layout: [cout_pad/BN][cin_pad/32][ky][kx][n BN][ci 32]
     std::vector<uint16_t> packed3;
     if (!c.from_image) {
-        const int BN = conv3_shape(1, 1, 1, c.info.cout, k).bn;   // BN depends on cout only
+        const int BN = conv3_shape(1, 1, 1, c.info.cout, k, border_).bn;   // BN depends on cout only
         const int nb = (c.info.cout + BN - 1) / BN, cpt = c.cin_pad / 32, kt = k * k;
         packed3.assign((size_t)nb * cpt * kt * BN * 32, 0);
         for (int co = 0; co < c.info.cout; ++co)
@@ -273,10 +288,13 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
         OPK_HIP(hipMemcpyAsync(dw3, packed3.data(), packed3.size() * 2, hipMemcpyHostToDevice,
                                ctx_->stream));
     }
-    void* dw = c.w.get(packed.size() * 2);
     void* db = c.bias.get(bias.size() * 4);
     void* ds = c.slope.get(sl.size() * 4);
-    OPK_HIP(hipMemcpyAsync(dw, packed.data(), packed.size() * 2, hipMemcpyHostToDevice, ctx_->stream));
+    if (!packed.empty()) {
+        void* dw = c.w.get(packed.size() * 2);
+        OPK_HIP(hipMemcpyAsync(dw, packed.data(), packed.size() * 2, hipMemcpyHostToDevice,
+                               ctx_->stream));
+    }
     OPK_HIP(hipMemcpyAsync(db, bias.data(), bias.size() * 4, hipMemcpyHostToDevice, ctx_->stream));
     OPK_HIP(hipMemcpyAsync(ds, sl.data(), sl.size() * 4, hipMemcpyHostToDevice, ctx_->stream));
     OPK_HIP(hipStreamSynchronize(ctx_->stream));
@@ -330,7 +348,7 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
     ptr.assign(bufs_.size(), nullptr);
     {
         const char* e = std::getenv("OPK_CONV1_FUSED");   // dev A/B switch: 0 disables the fusion
-        S.fused1 = fuse1_.a >= 0 && !conv_v1_ && !(e && e[0] == '0') &&
+        S.fused1 = fuse1_.a >= 0 && !conv_v1_ && !(e && e[0] == '0') && border_ == 1 &&
                    conv1_fused_supported(h, w, 64, 64);
     }
     for (size_t i = 0; i < bufs_.size(); ++i) {
@@ -340,9 +358,9 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
             continue;   // conv1_1 / conv1_2 outputs live only inside conv1_fused_kernel
         // zeroed guards: the kernels read up to W+3 positions before the first frame and up to
         // kConvGuardTail positions after the last one (conv.h)
-        const int L = bufs_[i].level;
-        const size_t head = (size_t)lw_[L] + 2 + 64;
-        const size_t pos = head + (size_t)n * (lh_[L] + 2) * (lw_[L] + 2) + kConvGuardTail;
+        const int L = bufs_[i].level, B = border_;
+        const size_t head = (size_t)B * (lw_[L] + 2 * B) + B + 64;
+        const size_t pos = head + (size_t)n * (lh_[L] + 2 * B) * (lw_[L] + 2 * B) + kConvGuardTail;
         const size_t bytes = pos * bufs_[i].cs * 2;
         OPK_CHECK_ARG(pos * bufs_[i].cs < (size_t)1 << 31, "activation buffer exceeds 2^31 elements");
         uint16_t* raw = static_cast<uint16_t*>(S.mem.back()->get(bytes));
@@ -350,7 +368,7 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
         ptr[i] = raw + head * bufs_[i].cs;
     }
     const char* e3 = std::getenv("OPK_CONV3");   // dev A/B switch: OPK_CONV3=0 disables the halo kernel
-    const bool allow3 = !conv_v1_ && !(e3 && e3[0] == '0');
+    const bool allow3 = (!conv_v1_ && !(e3 && e3[0] == '0')) || border_ != 1;
     const size_t out_bytes = (size_t)n * out_c_ * lh_[out_level_] * lw_[out_level_] * 4;
     S.out32 = static_cast<float*>(S.out_mem.get(out_bytes));
     void* sink = sink_.get(kConv3SinkBytes);
@@ -359,7 +377,7 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
     for (size_t ci = 0; ci < convs_.size(); ++ci) {
         const ConvPlan& c = convs_[ci];
         ConvArgs& a = S.args[ci];
-        const int H = lh_[c.level], W = lw_[c.level], Wp = W + 2;
+        const int H = lh_[c.level], W = lw_[c.level], Wp = W + 2 * border_;
         a.in = ptr[c.in.buf];
         a.in_cs = bufs_[c.in.buf].cs;
         a.in_coff = c.in.coff;
@@ -367,13 +385,16 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
         a.ntaps = c.ntaps;
         if (c.ntaps == 9)
             for (int t = 0; t < 9; ++t) a.tapoff[t] = (t / 3) * Wp + (t % 3);
-        else
+        else if (c.ntaps == 1)
             a.tapoff[0] = Wp + 1;
+        a.border = border_;
         a.ksteps = c.ksteps;
         const bool use3 = allow3 && !c.from_image && c.w3.ptr != nullptr;
         S.use3[ci] = use3;
+        OPK_CHECK_ARG(use3 || c.from_image || (c.info.k != 7 && border_ == 1),
+                      c.info.name + ": 7x7 / wide-border convolutions run on the conv3 kernels only");
         if (use3) {
-            const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, c.info.k);
+            const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, c.info.k, border_);
             a.sw = s3.sw;
             a.nstrips = s3.nstrips;
             a.sink = sink;
@@ -471,7 +492,7 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
             const PoolPlan& p = pools_[s.idx];
             const int L = p.level_in;
             launch_maxpool2(ptr[p.out_buf], ptr[p.in_buf], n, lh_[L], lw_[L],
-                            bufs_[p.in_buf].cs, lh_[L + 1], lw_[L + 1], ctx_->stream);
+                            bufs_[p.in_buf].cs, lh_[L + 1], lw_[L + 1], ctx_->stream, border_);
         }
     }
 }

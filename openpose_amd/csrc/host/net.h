@@ -41,6 +41,7 @@ public:
     int frames() const { return cur_ ? cur_->n : 0; }
     static constexpr int kMaxShapes = 8;
     double flops_per_frame(int h, int w) const;   // useful (unpadded) conv FLOPs
+    int border() const { return border_; }
     ~NetHip();
 
     // forward timing on the context stream (HIP events around every forward while enabled);
@@ -98,6 +99,7 @@ private:
     struct Fuse1 { int a = -1, b = -1, p = -1, abuf = -1, bbuf = -1; };
     Fuse1 fuse1_;                 // conv1_1 -> conv1_2 -> pool1 (conv1_fused.hip) when planned
     int cus_ = 256;               // compute units (persistent-kernel grid)
+    int border_ = 1;              // zero border of every padded image (widest conv pad, >= 1)
 
     std::vector<std::unique_ptr<ShapePlan>> shapes_;   // oldest first
     ShapePlan* cur_ = nullptr;    // shape of the last forward

@@ -39,6 +39,7 @@ struct ConvArgs {
     float rcp[3];         // conv3 only, set by launch_conv3: 1/((H+2)(sw+2)), 1/(sw+2), 1/nstrips
     void* sink;           // conv3 persistent variant: >= kConv3SinkBytes of scratch (masked stores)
     int cus;              // conv3 persistent variant: compute units (grid size); 0 disables it
+    int border;           // zero border of the padded images (conv3 / conv_image; 0 means 1)
 };
 
 // v1 (conv.hip): 256 lanes, 128 x bn tile, register-staged; bn: 32, 64, 96 or 128
@@ -53,13 +54,14 @@ void launch_conv2(const ConvArgs& a, int bn, hipStream_t stream);
 constexpr int kConvGuardTail = 1024;   // positions
 constexpr size_t kConv3SinkBytes = (size_t)1024 * 1024 * 8;   // 1024 lanes x 1024 workgroups x 8 B
 struct Conv3Shape {
-    int ks;                       // 3 or 1
+    int ks;                       // 7, 3 or 1
+    int border;                   // zero border of the net's padded images
     int bm, bn, hr, tapu, minb;   // tile, halo rows, taps per K unit, workgroups per CU
     int nw;                       // waves per workgroup
     int sw, nstrips;
     bool persist;                 // 16-wave tiles: persistent kernel (conv3p) when the launch allows
 };
-Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks);
+Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border = 1);
 void launch_conv3(const ConvArgs& a, hipStream_t stream);
 
 // NCHW fp32 [frames][3][H][W] -> padded NHWC fp16 [frames][H+2][W+2][32] holding, at each pixel,
@@ -92,6 +94,6 @@ void launch_conv1_fused(const Conv1FusedArgs& a, int workgroups, hipStream_t str
 
 // 2x2 stride-2 max pool with Caffe ceil sizing, padded NHWC fp16 -> padded NHWC fp16.
 void launch_maxpool2(uint16_t* out, const uint16_t* in, int frames, int H, int W, int C, int OH,
-                     int OW, hipStream_t stream);
+                     int OW, hipStream_t stream, int border = 1);
 
 }  // namespace opk

@@ -226,7 +226,7 @@ __device__ __forceinline__ uint32_t hmax2(uint32_t a, uint32_t b)
 __global__ __launch_bounds__(256) void maxpool2_kernel(uint16_t* __restrict__ out,
                                                        const uint16_t* __restrict__ in,
                                                        int frames, int H, int W, int C, int OH,
-                                                       int OW)
+                                                       int OW, int B)
 {
     const int c8 = C / 8;
     const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -242,7 +242,7 @@ __global__ __launch_bounds__(256) void maxpool2_kernel(uint16_t* __restrict__ ou
     bool first = true;
     for (int y = y0; y < y1; ++y)
         for (int x = x0; x < x1; ++x) {
-            const size_t pos = ((size_t)f * (H + 2) + y + 1) * (W + 2) + x + 1;
+            const size_t pos = ((size_t)f * (H + 2 * B) + y + B) * (W + 2 * B) + x + B;
             const uint4 v = *reinterpret_cast<const uint4*>(in + pos * C + g * 8);
             if (first) { m = v; first = false; }
             else {
@@ -252,7 +252,7 @@ __global__ __launch_bounds__(256) void maxpool2_kernel(uint16_t* __restrict__ ou
                 m.w = hmax2(m.w, v.w);
             }
         }
-    const size_t opos = ((size_t)f * (OH + 2) + oy + 1) * (OW + 2) + ox + 1;
+    const size_t opos = ((size_t)f * (OH + 2 * B) + oy + B) * (OW + 2 * B) + ox + B;
     *reinterpret_cast<uint4*>(out + opos * C + g * 8) = m;
 }
 
@@ -286,12 +286,13 @@ void launch_im2col3(uint16_t* out, const float* in, int frames, int H, int W, hi
 }
 
 void launch_maxpool2(uint16_t* out, const uint16_t* in, int frames, int H, int W, int C, int OH,
-                     int OW, hipStream_t stream)
+                     int OW, hipStream_t stream, int border)
 {
+    OPK_CHECK_ARG(border >= 1, "border >= 1");
     OPK_CHECK_ARG(C % 8 == 0, "pool channels must be a multiple of 8");
     const size_t total = (size_t)frames * OH * OW * (C / 8);
     hipLaunchKernelGGL(maxpool2_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
-                       out, in, frames, H, W, C, OH, OW);
+                       out, in, frames, H, W, C, OH, OW, border);
     OPK_LAUNCH_CHECK();
 }
 

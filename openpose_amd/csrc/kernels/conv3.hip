@@ -110,14 +110,22 @@ __device__ __forceinline__ int fdiv(int n, int d, float rd)
 }
 
 // virtual-image geometry (see the header comment)
+// B = the zero border of every activation buffer of the net (1 for BODY_25; the pad of its widest
+// convolution in general, 3 for the 7x7 stages of COCO / MPI / face / hand)
 struct Strips {
-    int H, Wp, sw, VW, nstrips, fposV, total;
+    int H, B, Hp, Wp, sw, VW, nstrips, fposV, total;
     float rf, rv, rs;   // reciprocals of fposV, VW, nstrips
     __device__ Strips(const ConvArgs& a)
-        : H(a.H), Wp(a.W + 2), sw(a.sw), VW(a.sw + 2), nstrips(a.nstrips),
-          fposV((a.H + 2) * (a.sw + 2)), total(a.frames * a.nstrips * (a.H + 2) * (a.sw + 2)),
+        : H(a.H), B(a.border), Hp(a.H + 2 * a.border), Wp(a.W + 2 * a.border), sw(a.sw),
+          VW(a.sw + 2 * a.border), nstrips(a.nstrips), fposV((a.H + 2 * a.border) * (a.sw + 2 * a.border)),
+          total(a.frames * a.nstrips * (a.H + 2 * a.border) * (a.sw + 2 * a.border)),
           rf(a.rcp[0]), rv(a.rcp[1]), rs(a.rcp[2])
     {
+    }
+    // virtual position (yy, xx) of strip s is an output pixel of the image
+    __device__ bool interior(int yy, int xx, int s, int W) const
+    {
+        return yy >= B && yy < H + B && xx >= B && xx < sw + B && s * sw + xx - B < W;
     }
     // padded-image position of virtual position v (any v; outside the image -> -1, a zeroed guard)
     template <bool FAST = true>
@@ -136,7 +144,7 @@ struct Strips {
         xx = rem - yy * VW;
         f = FAST ? fdiv(vf, nstrips, rs) : vf / nstrips;
         s = vf - f * nstrips;
-        return (long)(f * (H + 2) + yy) * Wp + s * sw + xx;
+        return (long)(f * Hp + yy) * Wp + s * sw + xx;
     }
 };
 
@@ -154,7 +162,8 @@ void conv3_kernel(const ConvArgs a)
     constexpr int WN = BN / WAVES_N;
     static_assert(WROWS % 16 == 0 && WROWS <= 128 && WN % 16 == 0 && WN <= 64, "wave tiles");
     static_assert(TAPU == 1 || TAPU == 3, "taps per unit");
-    static_assert(KS == 3 || (KS == 1 && TAPU == 1 && HR == BM), "1x1: one tap, halo = tile");
+    static_assert(KS == 3 || (KS == 7 && TAPU == 1) || (KS == 1 && TAPU == 1 && HR == BM),
+                  "3x3, 7x7 (single-tap units) or 1x1 (one tap, halo = tile)");
     constexpr int MF = WROWS / 16, NF = WN / 16;
     constexpr int KT = KS * KS;                   // taps
     constexpr int UPC = KT / TAPU;                // units per 32-channel chunk
@@ -197,7 +206,7 @@ void conv3_kernel(const ConvArgs a)
         const int lp = phys ^ (((hr >> 2) & 1) << 1);
         int yy, xx, s;
         int f;
-        const long pos = g.template map<false>(p0 - (KS == 3 ? g.VW + 1 : 0) + hr, f, yy, xx, s);
+        const long pos = g.template map<false>(p0 - (KS / 2) * (g.VW + 1) + hr, f, yy, xx, s);
         arow[i] = a.in + a.in_coff + pos * a.in_cs + lp * 8;
     }
     // this wave issues halo instructions i*8 + wave < API and B instructions j*8 + wave < BPI
@@ -276,10 +285,10 @@ void conv3_kernel(const ConvArgs a)
         const uint4* Bs = lds + NAS * ASLOT + (u % 3) * BSLOT;
 #pragma unroll
         for (int k = 0; k < TAPU; ++k) {
-            const int tap = t * TAPU + k;         // ky*3 + kx
-            const int ky = tap / 3, kx = tap - 3 * (tap / 3);
+            const int tap = t * TAPU + k;         // ky*KS + kx
+            const int ky = tap / KS, kx = tap - KS * (tap / KS);
             half8_t fa[MF], fb[NF];
-            const int hoff = KS == 3 ? ky * g.VW + kx : 0;
+            const int hoff = ky * g.VW + kx;
 #if OPK3_ABLATE == 4   // dev probe only: no fragment reads (register operands)
 #pragma unroll
             for (int i = 0; i < MF; ++i) fa[i] = (half8_t)(_Float16)(hoff + i);
@@ -319,14 +328,14 @@ void conv3_kernel(const ConvArgs a)
     {   // fragment i is 16 virtual positions after fragment i-1: step the coordinates
         int f, yy, xx, s;
         prow[0] = g.map(pbase, f, yy, xx, s);
-        pok[0] = yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
+        pok[0] = g.interior(yy, xx, s, a.W);
 #pragma unroll
         for (int i = 1; i < MF; ++i) {
             if (g.VW > 16) {
                 xx += 16;
                 if (xx >= g.VW) {
                     xx -= g.VW;
-                    if (++yy == a.H + 2) {
+                    if (++yy == g.Hp) {
                         yy = 0;
                         if (++s == g.nstrips) {
                             s = 0;
@@ -335,12 +344,12 @@ void conv3_kernel(const ConvArgs a)
                     }
                 }
                 const bool in = pbase + i * 16 < g.total;
-                prow[i] = in ? (long)(f * (a.H + 2) + yy) * g.Wp + s * g.sw + xx : -1;
-                pok[i] = in && yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
+                prow[i] = in ? (long)(f * g.Hp + yy) * g.Wp + s * g.sw + xx : -1;
+                pok[i] = in && g.interior(yy, xx, s, a.W);
             } else {
                 int f2, yy2, xx2, s2;
                 prow[i] = g.map(pbase + i * 16, f2, yy2, xx2, s2);
-                pok[i] = yy2 >= 1 && yy2 <= a.H && xx2 >= 1 && xx2 <= g.sw && s2 * g.sw + xx2 <= a.W;
+                pok[i] = g.interior(yy2, xx2, s2, a.W);
             }
         }
     }
@@ -380,8 +389,8 @@ void conv3_kernel(const ConvArgs a)
             if (a.out32) {   // fp32 NCHW net output (the activations before fp16)
                 int f, yy, xx, sx;
                 (void)g.map(pbase + i * 16, f, yy, xx, sx);
-                float* o = a.out32 + (((size_t)f * a.out32_c + a.out32_coff + ch) * a.H + yy - 1) *
-                                         a.W + sx * g.sw + xx - 1;
+                float* o = a.out32 + (((size_t)f * a.out32_c + a.out32_coff + ch) * a.H + yy - g.B) *
+                                         a.W + sx * g.sw + xx - g.B;
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
                     if (ch + r < a.cout) o[(size_t)r * a.H * a.W] = v[r];
@@ -583,13 +592,13 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
             asm volatile("" : "+v"(pbase));
             int f, yy, xx, s;
             prow[0] = g.map(pbase, f, yy, xx, s);
-            pok[0] = yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
+            pok[0] = g.interior(yy, xx, s, a.W);
 #pragma unroll
             for (int i = 1; i < MF; ++i) {   // VW > 16 (host): step 16 positions
                 xx += 16;
                 if (xx >= g.VW) {
                     xx -= g.VW;
-                    if (++yy == a.H + 2) {
+                    if (++yy == g.Hp) {
                         yy = 0;
                         if (++s == g.nstrips) {
                             s = 0;
@@ -598,8 +607,8 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
                     }
                 }
                 const bool in = pbase + i * 16 < g.total;
-                prow[i] = in ? (long)(f * (a.H + 2) + yy) * g.Wp + s * g.sw + xx : 0;
-                pok[i] = in && yy >= 1 && yy <= a.H && xx >= 1 && xx <= g.sw && s * g.sw + xx <= a.W;
+                prow[i] = in ? (long)(f * g.Hp + yy) * g.Wp + s * g.sw + xx : 0;
+                pok[i] = in && g.interior(yy, xx, s, a.W);
             }
         }
         const int chl = n0 + wn * WN + 4 * q;
@@ -647,15 +656,18 @@ int env_int(const char* name, int dflt)
 }
 }  // namespace
 
-Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
+Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border)
 {
     // dev A/B switches (read per call so tests can compare variants in one process):
     // OPK_CONV3_SMALL=0 -> no two-per-CU tiles, OPK_CONV3_W16=0 -> no 16-wave tiles,
     // OPK_CONV3_PERSIST=0 -> 16-wave tiles without the persistent kernel
     const bool small = env_int("OPK_CONV3_SMALL", 1) != 0;
     const int big16 = env_int("OPK_CONV3_W16", 1);
+    OPK_CHECK_ARG(ks == 1 || ks == 3 || ks == 7, "conv3: 1x1, 3x3 or 7x7");
+    OPK_CHECK_ARG(border >= 1 && border >= ks / 2, "conv3: the zero border must cover the pad");
     Conv3Shape s;
     s.ks = ks;
+    s.border = border;
     s.persist = false;
     s.bn = cout <= 64 ? 64 : (cout <= 96 ? 96 : 128);
     if (ks == 1) {   // no halo: small LDS (three tile slots), two workgroups per CU
@@ -668,24 +680,33 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
         s.sw = W;
         return s;
     }
-    // two workgroups per CU pay off once every CU gets at least two 256-position tiles (measured:
-    // +10-17 % on the 92x164 / 184x328 / 512-channel layers, -20 % at one tile per CU)
-    const long tiles = ((long)frames * (H + 2) * (W + 2) / 256) * ((cout + s.bn - 1) / s.bn);
     s.nw = 8;
-    // (measured, round 1: 4-wave 256x128 two-per-CU tiles and 8-wave 512x128 tiles of 128x64
-    // wave tiles were both slower than these on every BODY_25 layer)
-    if (s.bn != 64 && big16 && tiles >= 3 * 256) {   // 512 x {128,96} tiles, 16 waves
-        s.persist = env_int("OPK_CONV3_PERSIST", 1) != 0;
-        // the persistent kernel keeps bias/slopes in LDS: 688 halo rows (strips <= 85 columns)
-        s.bm = 512; s.hr = s.persist ? kP_HR : 704; s.tapu = 3; s.minb = 1; s.nw = 16;
-    } else if (small && tiles >= 2 * 256) {   // <= 80 KB of LDS
-        s.bm = 256; s.hr = 448; s.tapu = 1; s.minb = 2;
-    } else if (s.bn != 64) {
-        s.bm = 256; s.hr = 512; s.tapu = 3; s.minb = 1;
+    if (ks == 7) {   // 7x7 (COCO / MPI / face / hand stages): single-tap units, 1024-row halo
+        s.bm = 256; s.hr = 1024; s.tapu = 1; s.minb = 1;
     } else {
-        s.bm = 512; s.hr = 768; s.tapu = 3; s.minb = 1;
+        // two workgroups per CU pay off once every CU gets at least two 256-position tiles
+        // (measured: +10-17 % on the 92x164 / 184x328 / 512-channel layers, -20 % at one tile per
+        // CU)
+        const long tiles = ((long)frames * (H + 2 * border) * (W + 2 * border) / 256) *
+                           ((cout + s.bn - 1) / s.bn);
+        // (measured, round 1: 4-wave 256x128 two-per-CU tiles and 8-wave 512x128 tiles of 128x64
+        // wave tiles were both slower than these on every BODY_25 layer)
+        if (s.bn != 64 && big16 && tiles >= 3 * 256) {   // 512 x {128,96} tiles, 16 waves
+            s.persist = env_int("OPK_CONV3_PERSIST", 1) != 0;
+            // the persistent kernel keeps bias/slopes in LDS: 688 halo rows
+            s.bm = 512; s.hr = s.persist ? kP_HR : 704; s.tapu = 3; s.minb = 1; s.nw = 16;
+        } else if (small && tiles >= 2 * 256) {   // <= 80 KB of LDS
+            s.bm = 256; s.hr = 448; s.tapu = 1; s.minb = 2;
+        } else if (s.bn != 64) {
+            s.bm = 256; s.hr = 512; s.tapu = 3; s.minb = 1;
+        } else {
+            s.bm = 512; s.hr = 768; s.tapu = 3; s.minb = 1;
+        }
     }
-    const int max_strip = (s.hr - s.bm - 2) / 2 - 2;   // halo: BM + 2 * (sw + 2) + 2 rows
+    // halo: BM + (ks - 1) * (VW + 1) rows, VW = sw + 2 * border
+    const int max_vw = (s.hr - s.bm - (ks - 1)) / (ks - 1);
+    const int max_strip = max_vw - 2 * border;
+    OPK_CHECK_ARG(max_strip >= 8, "conv3: border too wide for the halo");
     s.nstrips = (W + max_strip - 1) / max_strip;
     s.sw = (W + s.nstrips - 1) / s.nstrips;
     return s;
@@ -694,26 +715,30 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks)
 void launch_conv3(const ConvArgs& args, hipStream_t stream)
 {
     ConvArgs a = args;   // + the reciprocals of the strip geometry (Strips::map, kernel arguments)
-    a.rcp[0] = (float)(1.0 / ((double)(a.H + 2) * (a.sw + 2)));
-    a.rcp[1] = (float)(1.0 / (double)(a.sw + 2));
+    if (a.border <= 0) a.border = 1;
+    const int B = a.border;
+    a.rcp[0] = (float)(1.0 / ((double)(a.H + 2 * B) * (a.sw + 2 * B)));
+    a.rcp[1] = (float)(1.0 / (double)(a.sw + 2 * B));
     a.rcp[2] = (float)(1.0 / (double)(a.nstrips > 0 ? a.nstrips : 1));
-    const int ks = a.ntaps == 9 ? 3 : 1;
-    OPK_CHECK_ARG((a.ntaps == 9 || a.ntaps == 1) && a.cin_pad % 32 == 0 && a.cin_pad > 0,
-                  "3x3 or 1x1, cin_pad % 32 == 0");
+    const int ks = a.ntaps == 49 ? 7 : (a.ntaps == 9 ? 3 : 1);
+    OPK_CHECK_ARG((a.ntaps == 49 || a.ntaps == 9 || a.ntaps == 1) && a.cin_pad % 32 == 0 &&
+                      a.cin_pad > 0,
+                  "7x7, 3x3 or 1x1, cin_pad % 32 == 0");
     OPK_CHECK_ARG(a.in_cs % 8 == 0 && a.in_coff % 8 == 0, "input slice must be 16-byte aligned");
     OPK_CHECK_ARG(a.in_coff + a.cin_pad <= a.in_cs, "input slice exceeds the buffer");
     OPK_CHECK_ARG(a.M > 0 && a.cout > 0 && a.ndst <= kConvMaxDst, "bad sizes");
-    const Conv3Shape s = conv3_shape(a.frames, a.H, a.W, a.cout, ks);
+    const Conv3Shape s = conv3_shape(a.frames, a.H, a.W, a.cout, ks, B);
     OPK_CHECK_ARG(a.sw == s.sw && a.nstrips == s.nstrips, "strip geometry differs from conv3_shape");
-    OPK_CHECK_ARG(ks == 1 || s.bm + 2 * (s.sw + 2) + 2 <= s.hr, "strip too wide for the halo");
-    const long total = (long)a.frames * s.nstrips * (a.H + 2) * (s.sw + 2);
-    OPK_CHECK_ARG(total + s.bm + 2L * (s.sw + 2) < (1L << 24), "too many positions per launch");
+    const int VW = s.sw + 2 * B;
+    OPK_CHECK_ARG(ks == 1 || s.bm + (ks - 1) * (VW + 1) <= s.hr, "strip too wide for the halo");
+    const long total = (long)a.frames * s.nstrips * (a.H + 2 * B) * VW;
+    OPK_CHECK_ARG(total + s.bm + (long)(ks - 1) * (VW + 1) < (1L << 24), "too many positions per launch");
     const int nn = (a.cout + s.bn - 1) / s.bn;
     const long ntiles = ((total + s.bm - 1) / s.bm) * nn;
     dim3 grid((unsigned)ntiles);
     // measured: +3-10 % on the single-n-block layers, 3-8 % slower with 2-4 n-blocks (kept 16-wave)
     if (s.nw == 16 && s.persist && nn == 1 && a.sink && a.cus >= nn && a.cout % s.bn == 0 && !a.out32 &&
-        s.sw + 2 > 16) {
+        VW > 16) {
         bool aligned = true;
         for (int d = 0; d < a.ndst; ++d) aligned = aligned && ((a.dst_coff[d] | a.dst_cs[d]) & 3) == 0;
         if (aligned) {   // one workgroup per CU, n-blocks spread evenly over the grid
@@ -734,7 +759,11 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
 #define OPK3_LAUNCH(BM_, BN_, HR_, TAPU_, MINB_, KS_)                                          \
     hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, MINB_, KS_>), grid, dim3(512), 0,   \
                        stream, a)
-    if (ks == 1) {
+    if (ks == 7) {
+        if (s.bn == 64) OPK3_LAUNCH(256, 64, 1024, 1, 1, 7);
+        else if (s.bn == 96) OPK3_LAUNCH(256, 96, 1024, 1, 1, 7);
+        else OPK3_LAUNCH(256, 128, 1024, 1, 1, 7);
+    } else if (ks == 1) {
         if (s.bn == 64) OPK3_LAUNCH(256, 64, 256, 1, 2, 1);
         else if (s.bn == 96) OPK3_LAUNCH(256, 96, 256, 1, 2, 1);
         else OPK3_LAUNCH(256, 128, 256, 1, 2, 1);

@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
 {
     __shared__ float tile[3 * (TH + 2) * LW];
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int H = a.H, W = a.W;
+    const int H = a.H, W = a.W, B = a.border > 0 ? a.border : 1;
     const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
     int b = blockIdx.x;
     const int tx = b % tiles_x;
@@ -83,7 +83,7 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
     if (y >= H) return;
     uint16_t* dbase[kConvMaxDst];
     for (int d = 0; d < a.ndst; ++d)
-        dbase[d] = a.dst[d] + ((size_t)f * (H + 2) + y + 1) * (W + 2) * a.dst_cs[d] + a.dst_coff[d];
+        dbase[d] = a.dst[d] + ((size_t)f * (H + 2 * B) + y + B) * (W + 2 * B) * a.dst_cs[d] + a.dst_coff[d];
 #pragma unroll
     for (int grp = 0; grp < TW / 16; ++grp) {
         const int xl = grp * 16 + r16;
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
             const uint32_t lo = (uint32_t)f2h_bits_i(v[0]) | ((uint32_t)f2h_bits_i(v[1]) << 16);
             const uint32_t hi = (uint32_t)f2h_bits_i(v[2]) | ((uint32_t)f2h_bits_i(v[3]) << 16);
             for (int d = 0; d < a.ndst; ++d)
-                *reinterpret_cast<uint2*>(dbase[d] + (size_t)(x + 1) * a.dst_cs[d] + ch) = make_uint2(lo, hi);
+                *reinterpret_cast<uint2*>(dbase[d] + (size_t)(x + B) * a.dst_cs[d] + ch) = make_uint2(lo, hi);
         }
     }
 }

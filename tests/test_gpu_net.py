@@ -29,7 +29,7 @@ def rel_l2(a, b):
 
 def conv(name, bottom, cout, k, act=None):
     out = [dict(name=name, type="Convolution", bottom=[bottom], top=[name], num_output=cout,
-                kernel_size=k, pad=1 if k == 3 else 0)]
+                kernel_size=k, pad=k // 2)]
     if act:
         out.append(dict(name=act + "_" + name, type="ReLU" if act == "relu" else "PReLU",
                         bottom=[name], top=[name]))
@@ -120,6 +120,37 @@ def test_conv1_fused_matches_unfused(ctx, hw, acts):
     np.testing.assert_array_equal(outs[0], outs[1])
 
 
+def cpm_stage_graph(out_is_concat=True):
+    """A COCO / hand-like CPM net in miniature: VGG 3x3 front with a pool, then two refinement
+    stages of 7x7 (pad 3) convs on concat(features, previous stage), 1x1 heads; the whole net
+    gets a 3-pixel zero border."""
+    L = conv("c1", "image", 64, 3, "relu") + conv("c2", "c1", 64, 3, "relu")
+    L.append(dict(name="p1", type="Pooling", bottom=["c2"], top=["p1"], pool="MAX",
+                  kernel_size=2, stride=2))
+    L += conv("c3", "p1", 128, 3, "relu") + conv("feat", "c3", 96, 3, "relu")
+    L += conv("s1a", "feat", 128, 3, "relu") + conv("s1b", "s1a", 64, 1, "relu") + conv("s1", "s1b", 22, 1)
+    L.append(dict(name="cat2", type="Concat", bottom=["s1", "feat"], top=["cat2"]))
+    L += conv("s2a", "cat2", 128, 7, "relu") + conv("s2b", "s2a", 128, 7, "relu")
+    L += conv("s2c", "s2b", 96, 7, "relu") + conv("s2d", "s2c", 128, 1, "relu")
+    if out_is_concat:
+        L += conv("s2", "s2d", 19, 1) + conv("s2p", "s2d", 38, 1)
+        L.append(dict(name="net_output", type="Concat", bottom=["s2", "s2p"], top=["net_output"]))
+    else:   # the hand / face nets: the last conv's top is the output blob
+        L += [dict(name="s2", type="Convolution", bottom=["s2d"], top=["net_output"], num_output=22,
+                   kernel_size=1, pad=0)]
+    return L
+
+
+@pytest.mark.parametrize("concat", [True, False])
+@pytest.mark.parametrize("hw", [(64, 96), (96, 200)])
+def test_7x7_cpm_stages_vs_oracle(ctx, concat, hw):
+    x = np.random.default_rng(21).uniform(-0.5, 0.5, (2, 3) + hw).astype(np.float32)
+    got, ref = run_graph(ctx, cpm_stage_graph(concat), x, seed=5)
+    err = rel_l2(got, ref)
+    print("7x7 CPM %s rel-L2 %.3e" % (hw, err))
+    assert got.shape == ref.shape and err < SMALL_TOL
+
+
 VARIANTS = {"persistent": {}, "w16": {"OPK_CONV3_PERSIST": "0"},
             "w8": {"OPK_CONV3_W16": "0"}, "w8_one_per_cu": {"OPK_CONV3_W16": "0", "OPK_CONV3_SMALL": "0"}}
 ROUNDING_VARIANTS = set()   # variants with another MFMA shape (another fp32 summation order)
@@ -189,3 +220,48 @@ def torch_forward(graph, params, x):
         elif t == "Concat":
             blobs[l["top"][0]] = torch.cat([blobs[b] for b in l["bottom"]], 1)
     return blobs["net_output"].numpy()
+
+
+@pytest.mark.parametrize("name,hw", [("builtin:COCO_18", (64, 96)), ("builtin:MPI_15_4", (48, 80)),
+                                     ("builtin:HAND", (64, 64)), ("builtin:FACE", (48, 64))])
+def test_reference_cpm_nets_vs_oracle(ctx, name, hw):
+    """The reference's other networks (7x7 stages, 3-pixel border, ReLU) against the fp32 oracle
+    on the same seeded weights; graphs from tests/cpm_graphs.py (= the reference prototxts,
+    tests/test_models.py)."""
+    from tests import cpm_graphs
+    graph = prototxt.parse(prototxt.emit(cpm_graphs.GRAPHS[name]()))
+    params = synth.he_weights(graph, seed=9)
+    x = np.random.default_rng(10).uniform(-0.5, 0.5, (2, 3) + hw).astype(np.float32)
+    net = Net(ctx, name)
+    net.set_params(params)
+    net.forward(torch.from_numpy(x).cuda())
+    got = net.output_numpy()
+    net.close()
+    ref = body25.forward(x, params, graph=graph)
+    err = rel_l2(got, ref)
+    print("%s %s rel-L2 %.3e" % (name, hw, err))
+    assert got.shape == ref.shape and err < BODY25_TOL
+
+
+def test_coco_pose_pipeline_runs_on_the_net(ctx):
+    """COCO_18 end to end: frames -> warp -> COCO net -> lazy resize -> NMS -> connector, equal to
+    feeding the same net output through the injection path."""
+    from openpose_amd.api import PoseExtractor
+    from openpose_amd.pose_tables import COCO_18
+    from tests import cpm_graphs
+    graph = prototxt.parse(prototxt.emit(cpm_graphs.GRAPHS["builtin:COCO_18"]()))
+    net = Net(ctx, "builtin:COCO_18")
+    net.set_params(synth.he_weights(graph, seed=2, out_scale=0.02))
+    pose = PoseExtractor(ctx, net, pose_model=COCO_18)
+    pose.set_input((-1, 96))
+    frames = torch.randint(0, 256, (2, 90, 160, 3), dtype=torch.uint8)
+    pose.forward_frames(frames.cuda())
+    got = [pose.keypoints(f) for f in range(2)]
+    out = torch.from_numpy(net.output_numpy()).cuda()
+    ref = PoseExtractor(ctx, None, pose_model=COCO_18)
+    ref.forward_net_output(out, (out.shape[3] * 8, out.shape[2] * 8), (160, 90))
+    for f in range(2):
+        kp, ks = ref.keypoints(f)
+        np.testing.assert_array_equal(got[f][0], kp)
+        np.testing.assert_array_equal(got[f][1], ks)
+    assert pose.peaks_numpy().shape[1] == 18
