@@ -89,7 +89,7 @@ def test_unsupported_layers_are_rejected():
     path = os.path.join(ROOT, "tests", "_bad.prototxt")
     open(path, "w").write(bad)
     try:
-        with pytest.raises(_lib.OpkError, match="3x3/pad1"):
+        with pytest.raises(_lib.OpkError, match="3x3/pad 1, 7x7/pad 3 and 1x1"):
             Net(ctx, path)
     finally:
         os.unlink(path)
