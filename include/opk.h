@@ -313,6 +313,49 @@ int opk_pose_heatmaps_copy(opk_pose* pose, int types, int scale_mode, float* dst
  * counts_host [parts]; either may be NULL. */
 int opk_pose_candidates(opk_pose* pose, int frame, float* candidates_host, int* counts_host);
 
+
+/* ---- face / hand keypoints -------------------------------------------------------------------
+ * op::FaceDetector::detectFaces (include/openpose/face/faceDetector.hpp:10-27,
+ * src/openpose/face/faceDetector.cpp:122-139) and op::HandDetector::detectHands
+ * (include/openpose/hand/handDetector.hpp:13-45, src/openpose/hand/handDetector.cpp:135-160):
+ * rectangles (x, y, width, height) from pose keypoints_host [people][parts][3] of pose_model;
+ * rects_host face [people][4], hand [people][2 (left, right)][4].  A model without the detector's
+ * body parts (e.g. CAR_12) fails with OPK_ERR_UNSUPPORTED, as poseBodyPartMapStringToKey errors. */
+int opk_face_detect(int pose_model, const float* keypoints_host, int people, int parts,
+                    float* rects_host);
+int opk_hand_detect(int pose_model, const float* keypoints_host, int people, int parts,
+                    float* rects_host);
+
+/* op::FaceExtractorCaffe / op::HandExtractorCaffe (include/openpose/face/faceExtractorCaffe.hpp:
+ * 14-45, include/openpose/hand/handExtractorCaffe.hpp:14-52): forwardPass(rectangles, inputData)
+ * + getFaceKeypoints() / getHandKeypoints(), for every rectangle of a set of frames at once.  net:
+ * the face (builtin:FACE, pose_deploy.prototxt of models/face) or hand (builtin:HAND) net;
+ * net_w x net_h = --face_net_resolution / --hand_net_resolution (multiples of 16, default
+ * 368x368). */
+typedef struct opk_extractor opk_extractor;
+#define OPK_EXTRACT_FACE 0
+#define OPK_EXTRACT_HAND 1
+int opk_extractor_create(opk_ctx* ctx, opk_net* net, int kind, int net_w, int net_h,
+                         opk_extractor** out);
+int opk_extractor_destroy(opk_extractor* ex);
+/* hand only: --hand_scale_number / --hand_scale_range (HandExtractorNet, handExtractorNet.cpp) */
+int opk_extractor_set_scales(opk_extractor* ex, int number, float range);
+/* crops per net forward (default 32; batches run in power-of-two sizes) */
+int opk_extractor_set_max_batch(opk_extractor* ex, int max_batch);
+int opk_extractor_parts(opk_extractor* ex);   /* net output channels - 1; -1 for NULL */
+/* frames_dev: BGR uint8 [nframes][height][step] on device (step 0: width*3); rects_host as
+ * opk_face_detect / opk_hand_detect return them; frame_of_host [people] (NULL: frame 0).
+ * keypoints_host: face [people][parts][3], hand [2][people][parts][3] (left hands first), in
+ * frame pixels; zeros where the reference skips the rectangle (face: side <= 40; hand: side <= 1
+ * or area <= 10).  A non-square rectangle fails with OPK_ERR_ARG as the reference errors. */
+int opk_extractor_forward(opk_extractor* ex, const uint8_t* frames_dev, int nframes, int width,
+                          int height, size_t step, const float* rects_host,
+                          const int* frame_of_host, int people, float* keypoints_host);
+/* crops of the last forward (order: hand, person, scale; skipped rectangles have none): the 2x3
+ * inverse map (frame <- crop) and the crop's net input [3][net_h][net_w] on device */
+int opk_extractor_crop_count(opk_extractor* ex);
+int opk_extractor_crop(opk_extractor* ex, int i, double* matrix_host, const float** input_dev);
+
 #ifdef __cplusplus
 }
 #endif

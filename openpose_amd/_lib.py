@@ -78,6 +78,16 @@ _SIGS = {
     "opk_pose_candidates": (_i, [_p, _i, _p, _ip]),
     "opk_scale_keypoints": (_i, [_p, _i, _i, _i, _d, _d, _i, _i]),
     "opk_keep_top_n_people": (_i, [_p, _i, _i, _p, _i, _p, _p, _ip]),
+    "opk_face_detect": (_i, [_i, _p, _i, _i, _p]),
+    "opk_hand_detect": (_i, [_i, _p, _i, _i, _p]),
+    "opk_extractor_create": (_i, [_p, _p, _i, _i, _i, _c.POINTER(_p)]),
+    "opk_extractor_destroy": (_i, [_p]),
+    "opk_extractor_set_scales": (_i, [_p, _i, _f]),
+    "opk_extractor_set_max_batch": (_i, [_p, _i]),
+    "opk_extractor_parts": (_i, [_p]),
+    "opk_extractor_forward": (_i, [_p, _p, _i, _i, _i, _c.c_size_t, _p, _p, _i, _p]),
+    "opk_extractor_crop_count": (_i, [_p]),
+    "opk_extractor_crop": (_i, [_p, _i, _p, _c.POINTER(_p)]),
     "opk_scale_and_size": (_i, [_i, _i, _i, _i, _f, _i, _d, _c.POINTER(_d), _ip]),
     "opk_cvmat_to_input": (_i, [_p, _p, _p, _i, _i, _i, _c.c_size_t, _d, _i, _i, _i]),
     "opk_pose_set_input": (_i, [_p, _i, _i, _f, _i, _d]),

@@ -27,12 +27,13 @@ def _ptr(t):
 
 # Handles still open at interpreter exit (e.g. held by a test traceback) are closed before the HIP
 # runtime's own teardown: poses, then nets, then contexts.
-_LIVE = {"pose": weakref.WeakSet(), "net": weakref.WeakSet(), "ctx": weakref.WeakSet()}
+_LIVE = {"pose": weakref.WeakSet(), "extractor": weakref.WeakSet(), "net": weakref.WeakSet(),
+         "ctx": weakref.WeakSet()}
 
 
 @atexit.register
 def _close_live():
-    for kind in ("pose", "net", "ctx"):
+    for kind in ("pose", "extractor", "net", "ctx"):
         for obj in list(_LIVE[kind]):
             try:
                 obj.close()
@@ -478,3 +479,100 @@ class PoseExtractor:
 
     def peaks_numpy(self):
         return self._dev_array(self.L.opk_pose_peaks)
+
+
+# ---- face / hand keypoints ---------------------------------------------------------------------
+FACE, HAND = 0, 1
+
+
+def _detect(fn, pose_model, keypoints, per_person):
+    kp = np.ascontiguousarray(keypoints, np.float32)
+    people, parts = kp.shape[0], (kp.shape[1] if kp.ndim == 3 else 0)
+    out = np.zeros((people, per_person, 4), np.float32)
+    check(fn(pose_model, kp.ctypes.data_as(ctypes.c_void_p), people, parts,
+             out.ctypes.data_as(ctypes.c_void_p)))
+    return out
+
+
+def detect_faces(pose_keypoints, pose_model=BODY_25):
+    """op::FaceDetector(poseModel).detectFaces: [people, 4] (x, y, width, height)."""
+    return _detect(_lib.load().opk_face_detect, pose_model, pose_keypoints, 1)[:, 0]
+
+
+def detect_hands(pose_keypoints, pose_model=BODY_25):
+    """op::HandDetector(poseModel).detectHands: [people, 2 (left, right), 4]."""
+    return _detect(_lib.load().opk_hand_detect, pose_model, pose_keypoints, 2)
+
+
+class KeypointExtractor:
+    """op::FaceExtractorCaffe / op::HandExtractorCaffe over every rectangle of a set of frames:
+    kind FACE (net builtin:FACE) or HAND (builtin:HAND); net_resolution = (w, h)."""
+
+    def __init__(self, ctx, net, kind, net_resolution=(368, 368)):
+        self.ctx = ctx
+        self.L = ctx.L
+        self.net = net
+        self.kind = kind
+        self.net_resolution = tuple(net_resolution)
+        h = ctypes.c_void_p()
+        check(self.L.opk_extractor_create(ctx.h, net.h, kind, net_resolution[0],
+                                          net_resolution[1], ctypes.byref(h)))
+        self.h = h
+        _LIVE["extractor"].add(self)
+
+    def close(self):
+        if self.h:
+            self.L.opk_extractor_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def parts(self):
+        return self.L.opk_extractor_parts(self.h)
+
+    def set_scales(self, number, rng=0.4):
+        """--hand_scale_number / --hand_scale_range."""
+        check(self.L.opk_extractor_set_scales(self.h, number, float(rng)))
+
+    def set_max_batch(self, b):
+        check(self.L.opk_extractor_set_max_batch(self.h, b))
+
+    def forward(self, frames, rectangles, frame_of=None):
+        """frames: BGR uint8 [n, h, w, 3] CUDA tensor; rectangles [people, 4] (face) or
+        [people, 2, 4] (hand); frame_of [people] or None.  Returns face [people, parts, 3] or
+        hand [2, people, parts, 3] keypoints (numpy)."""
+        n, h, w, c = frames.shape
+        assert c == 3 and frames.dtype == torch.uint8
+        r = np.ascontiguousarray(rectangles, np.float32)
+        people = r.shape[0]
+        hands = 2 if self.kind == HAND else 1
+        out = np.zeros((hands, people, self.parts, 3), np.float32)
+        fo = None
+        if frame_of is not None:
+            fo = np.ascontiguousarray(frame_of, np.int32)
+            assert fo.shape == (people,)
+        check(self.L.opk_extractor_forward(
+            self.h, _ptr(frames), n, w, h, w * 3, r.ctypes.data_as(ctypes.c_void_p),
+            fo.ctypes.data_as(ctypes.c_void_p) if fo is not None else None, people,
+            out.ctypes.data_as(ctypes.c_void_p)))
+        return out[0] if self.kind == FACE else out
+
+    def crops(self):
+        """[(2x3 inverse map, net input [3, h, w] numpy)] of the last forward's crops."""
+        out = []
+        w, h = self.net_resolution
+        for i in range(self.L.opk_extractor_crop_count(self.h)):
+            m = np.zeros(6, np.float64)
+            p = ctypes.c_void_p()
+            check(self.L.opk_extractor_crop(self.h, i, m.ctypes.data_as(ctypes.c_void_p),
+                                            ctypes.byref(p)))
+            x = np.empty((3, h, w), np.float32)
+            check(self.L.opk_memcpy_d2h(self.ctx.h, x.ctypes.data_as(ctypes.c_void_p), p,
+                                        x.nbytes))
+            out.append((m.reshape(2, 3), x))
+        return out

@@ -7,6 +7,7 @@
 #include "../../../include/opk.h"
 #include "net.h"
 #include "caffemodel.h"
+#include "extract.h"
 #include "input.h"
 #include "pose.h"
 
@@ -393,5 +394,93 @@ int opk_pose_candidates(opk_pose* p, int frame, float* candidates_host, int* cou
 }
 
 float opk_pose_scale_net_to_output(opk_pose* p) { return p ? p->pose->scale_net_to_output() : 0.f; }
+
+}  // extern "C"
+
+// ---- face / hand keypoints (op::FaceDetector, op::HandDetector, op::FaceExtractorCaffe,
+//      op::HandExtractorCaffe) ----------------------------------------------------------------
+struct opk_extractor {
+    opk_ctx* ctx;
+    std::unique_ptr<opk::KeypointExtractor> ex;
+};
+
+extern "C" {
+
+int opk_face_detect(int pose_model, const float* keypoints, int people, int parts, float* rects)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(people == 0 || rects, "NULL rectangles");
+        opk::detect_faces(pose_model, keypoints, people, parts, reinterpret_cast<opk::Rect*>(rects));
+    });
+}
+
+int opk_hand_detect(int pose_model, const float* keypoints, int people, int parts, float* rects)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(people == 0 || rects, "NULL rectangles");
+        opk::detect_hands(pose_model, keypoints, people, parts, reinterpret_cast<opk::Rect*>(rects));
+    });
+}
+
+int opk_extractor_create(opk_ctx* ctx, opk_net* net, int kind, int net_w, int net_h,
+                         opk_extractor** out)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ctx && net && out, "NULL argument");
+        OPK_CHECK_ARG(ctx->device >= 0, "extraction needs a device context");
+        *out = new opk_extractor{
+            ctx, std::make_unique<opk::KeypointExtractor>(ctx, net->net.get(), kind, net_w, net_h)};
+    });
+}
+
+int opk_extractor_destroy(opk_extractor* ex)
+{
+    return guarded_net([&] { delete ex; });
+}
+
+int opk_extractor_set_scales(opk_extractor* ex, int number, float range)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ex, "NULL extractor");
+        ex->ex->set_scales(number, range);
+    });
+}
+
+int opk_extractor_set_max_batch(opk_extractor* ex, int max_batch)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ex, "NULL extractor");
+        ex->ex->set_max_batch(max_batch);
+    });
+}
+
+int opk_extractor_parts(opk_extractor* ex) { return ex ? ex->ex->parts() : -1; }
+
+int opk_extractor_forward(opk_extractor* ex, const uint8_t* frames, int nframes, int width,
+                          int height, size_t step, const float* rects, const int* frame_of,
+                          int people, float* keypoints)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ex && (people == 0 || keypoints), "NULL argument");
+        ex->ex->extract(frames, nframes, width, height, step,
+                        reinterpret_cast<const opk::Rect*>(rects), frame_of, people, keypoints);
+    });
+}
+
+int opk_extractor_crop_count(opk_extractor* ex) { return ex ? ex->ex->crops() : -1; }
+
+int opk_extractor_crop(opk_extractor* ex, int i, double* matrix, const float** input_dev)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ex, "NULL extractor");
+        OPK_CHECK_ARG(i >= 0 && i < ex->ex->crops(), "crop index out of range");
+        const auto* k = ex->ex.get();
+        if (matrix) std::memcpy(matrix, k->crop_matrix(i), 6 * sizeof(double));
+        if (input_dev) {
+            // crops are laid out [crops][3][net_h][net_w]
+            *input_dev = k->crop_inputs() + (size_t)i * 3 * k->net_w() * k->net_h();
+        }
+    });
+}
 
 }  // extern "C"

@@ -20,6 +20,7 @@ struct PoseTableRow {
     const int* map;
     int nmap;
     float nms_th, inter_th, nms_th_maxpos, inter_th_maxpos;
+    const int* keys;
 };
 #include "pose_tables.inc"
 }  // namespace
@@ -32,7 +33,8 @@ const PoseModelInfo& pose_model(int id)
             v.push_back(PoseModelInfo{r.id, r.name, r.parts, r.bkg,
                                       std::vector<int>(r.pairs, r.pairs + r.npairs2),
                                       std::vector<int>(r.map, r.map + r.nmap), r.nms_th, r.inter_th,
-                                      r.nms_th_maxpos, r.inter_th_maxpos});
+                                      r.nms_th_maxpos, r.inter_th_maxpos,
+                                      std::vector<int>(r.keys, r.keys + kDetectorKeys)});
         return v;
     }();
     if (id < 0 || id >= (int)models.size())

@@ -13,6 +13,8 @@ struct PoseModelInfo {
     std::vector<int> map_idx;       // getPoseMapIndex  (2 per pair, relative to parts+bkg)
     float nms_th, inter_th;         // getPoseDefaultNmsThreshold / ConnectInterThreshold
     float nms_th_maxpos, inter_th_maxpos;   // ... with maximizePositives
+    // body-part indices the face / hand detectors read (PoseKey below; -1: not in the model)
+    std::vector<int> keys;
     int npairs() const { return (int)pairs.size() / 2; }
     // net output channels: heat maps, background, PAFs (the PAF channels the pairs index)
     int heat_channels() const { return parts + (bkg ? 1 : 0) + (int)map_idx.size(); }
@@ -21,6 +23,9 @@ struct PoseModelInfo {
 };
 
 constexpr int kPoseModels = 15;   // PoseModel::Size (enumClasses.hpp:9-30)
+// indices into PoseModelInfo::keys (faceDetector.cpp:8-15, handDetector.cpp:120-123)
+enum PoseKey { kNeck, kNose, kLEar, kREar, kLEye, kREye, kLWrist, kLElbow, kLShoulder, kRWrist,
+               kRElbow, kRShoulder, kDetectorKeys };
 
 // throws opk::Error(OPK_ERR_UNSUPPORTED) for ids outside [0, kPoseModels)
 const PoseModelInfo& pose_model(int id);

@@ -18,16 +18,20 @@ namespace {
 
 // one workgroup per (frame, destination row); lanes stride the row, every channel plane is written
 // with coalesced 4-byte stores
+// Output image f reads source frame frame_of[f] (f when frame_of is NULL) with the tables at
+// xtab + f * tab_stride, ytab + f * tab_stride (tab_stride 0: one table pair for every image).
 template <int K>
 __global__ __launch_bounds__(256) void cvmat_to_input_kernel(
     float* __restrict__ dst, const uint8_t* __restrict__ src, int sh, int sw, size_t src_step,
     size_t src_frame, int dh, int dw, const int2* __restrict__ xtab, const int2* __restrict__ ytab,
-    const short* __restrict__ wtab, int normalize)
+    const short* __restrict__ wtab, int normalize, const int* __restrict__ frame_of, int tab_stride)
 {
     const int y = blockIdx.x % dh;
     const int f = blockIdx.x / dh;
+    xtab += (size_t)f * tab_stride;
+    ytab += (size_t)f * tab_stride;
     const int2 yt = ytab[y];                      // (first tap row, fraction index)
-    const uint8_t* fsrc = src + (size_t)f * src_frame;
+    const uint8_t* fsrc = src + (size_t)(frame_of ? frame_of[f] : f) * src_frame;
     const size_t plane = (size_t)dh * dw;
     float* out = dst + (size_t)f * 3 * plane + (size_t)y * dw;
     for (int x = threadIdx.x; x < dw; x += blockDim.x) {
@@ -66,7 +70,8 @@ __global__ __launch_bounds__(256) void cvmat_to_input_kernel(
 
 void launch_cvmat_to_input(float* dst, const uint8_t* src, int n, int sh, int sw, size_t src_step,
                            int dh, int dw, const int* xtab, const int* ytab, const short* wtab,
-                           int ksize, int normalize, hipStream_t stream)
+                           int ksize, int normalize, hipStream_t stream, const int* frame_of,
+                           int tab_stride)
 {
     OPK_CHECK_ARG(n > 0 && sh > 0 && sw > 0 && dh > 0 && dw > 0, "empty frame");
     OPK_CHECK_ARG(src_step >= (size_t)sw * 3, "row step shorter than the row");
@@ -79,10 +84,12 @@ void launch_cvmat_to_input(float* dst, const uint8_t* src, int n, int sh, int sw
     const size_t frame = src_step * sh;
     if (ksize == 2)
         hipLaunchKernelGGL(cvmat_to_input_kernel<2>, grid, dim3(threads), 0, stream, dst, src, sh,
-                           sw, src_step, frame, dh, dw, xt, yt, wtab, normalize);
+                           sw, src_step, frame, dh, dw, xt, yt, wtab, normalize, frame_of,
+                           tab_stride);
     else
         hipLaunchKernelGGL(cvmat_to_input_kernel<4>, grid, dim3(threads), 0, stream, dst, src, sh,
-                           sw, src_step, frame, dh, dw, xt, yt, wtab, normalize);
+                           sw, src_step, frame, dh, dw, xt, yt, wtab, normalize, frame_of,
+                           tab_stride);
     OPK_LAUNCH_CHECK();
 }
 

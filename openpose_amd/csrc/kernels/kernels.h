@@ -74,9 +74,17 @@ void launch_paf_scores_compact(float* records, int rec_floats, const HeatMap& he
 // src: n BGR uint8 frames [sh][src_step bytes], frame stride src_step*sh; dst [n][3][dh][dw] fp32.
 // xtab/ytab: per destination column/row {first source tap, 5-bit fraction index}; wtab: the
 // fixed-point 2-D weight table [32*32][ksize*ksize] (host/input.cpp builds all three)
+// frame_of (device, may be NULL): source frame of each output image; tab_stride: distance between
+// the table pairs of consecutive images, in {tap, fraction} entries (0: one shared pair)
 void launch_cvmat_to_input(float* dst, const uint8_t* src, int n, int sh, int sw, size_t src_step,
                            int dh, int dw, const int* xtab, const int* ytab, const short* wtab,
-                           int ksize, int normalize, hipStream_t stream);
+                           int ksize, int normalize, hipStream_t stream,
+                           const int* frame_of = nullptr, int tab_stride = 0);
+
+// ---- crops of face / hand keypoint extraction (crop.hip) -----------------------------------------
+// peaks [crops][parts][3] = (x, y, value) of the maximum of each of the first `parts` channels of
+// `heat` (frames = crops), the first in raster order among equal values (cv::minMaxLoc)
+void launch_heat_argmax(float* peaks, const HeatMap& heat, int crops, int parts, hipStream_t stream);
 
 // ---- elementwise helpers (misc.hip) -----------------------------------------------------------
 void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stream);

@@ -64,6 +64,9 @@ def lib():
         L.orc_cvmat_to_input.argtypes = [_f32p, _u8p, _i, _i, ctypes.c_double, _i, _i, _i]
         _i16p = np.ctypeslib.ndpointer(np.int16, flags="C_CONTIGUOUS")
         L.orc_warp_tab.argtypes = [_i, _i16p]
+        L.orc_warp_affine_inv.argtypes = [_f32p, _u8p, _i, _i,
+                                          np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS"),
+                                          _i, _i, _i]
         _LIB = L
     return _LIB
 
@@ -258,6 +261,16 @@ def cvmat_to_input(frame, scale, net_w, net_h, normalize=1):
     out = np.empty((3, net_h, net_w), np.float32)
     lib().orc_cvmat_to_input(out, frame, frame.shape[1], frame.shape[0], float(scale), net_w,
                              net_h, normalize)
+    return out
+
+
+def warp_affine_inv(frame, M, net_w, net_h, normalize=1):
+    """Face / hand crop: warpAffine(INTER_LINEAR | WARP_INVERSE_MAP) of a BGR uint8 frame [h, w, 3]
+    with the 2x3 matrix M -> [3, net_h, net_w] float32."""
+    frame = np.ascontiguousarray(frame, np.uint8)
+    out = np.empty((3, net_h, net_w), np.float32)
+    lib().orc_warp_affine_inv(out, frame, frame.shape[1], frame.shape[0],
+                              np.ascontiguousarray(M, np.float64).ravel(), net_w, net_h, normalize)
     return out
 
 

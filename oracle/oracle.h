@@ -104,6 +104,10 @@ double orc_resize_scale_factor(int iw, int ih, int tw, int th);
 void orc_warp_tab(int cubic, short* itab);
 void orc_cvmat_to_input(float* dst, const uint8_t* src, int sw, int sh, double scale, int dw,
                         int dh, int normalize);
+/* cv::warpAffine(INTER_LINEAR | WARP_INVERSE_MAP, constant 0) + uCharCvMatToFloatPtr: the face /
+ * hand crops (faceExtractorCaffe.cpp:215-232, handExtractorCaffe.cpp:44-73); M [2][3] */
+void orc_warp_affine_inv(float* dst, const uint8_t* src, int sw, int sh, const double* M, int dw,
+                         int dh, int normalize);
 
 /* ---- Caffe layer semantics for the BODY_25 prototxt (NCHW fp32, batch n) ------------------ */
 /* Convolution: cross-correlation, zero pad, stride 1, bias (Caffe ConvolutionLayer) */

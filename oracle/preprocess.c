@@ -202,3 +202,50 @@ void orc_cvmat_to_input(float* dst, const uint8_t* src, int sw, int sh, double s
         }
     }
 }
+
+/*
+ * cv::warpAffine(src, dst, M, {dw, dh}, INTER_LINEAR | WARP_INVERSE_MAP, BORDER_CONSTANT 0) for a
+ * BGR uint8 image, then uCharCvMatToFloatPtr: the crop of FaceExtractorCaffe::forwardPass
+ * (faceExtractorCaffe.cpp:215-232) and of the hand extractor's cropFrame
+ * (handExtractorCaffe.cpp:44-73).  M is used as given (inverse map), with OpenCV's full per-pixel
+ * arithmetic for any affine M:
+ *   X = (cvRound((M01*y + M02)*1024) + 16 + cvRound(M00*x*1024)) >> 5
+ *   Y = (cvRound((M11*y + M12)*1024) + 16 + cvRound(M10*x*1024)) >> 5
+ * source tap (X >> 5, Y >> 5), weights of entry (Y & 31) * 32 + (X & 31).
+ */
+void orc_warp_affine_inv(float* dst, const uint8_t* src, int sw, int sh, const double* M, int dw,
+                         int dh, int normalize)
+{
+    static short tab[(INTER_TAB * INTER_TAB + 1) * 4];
+    static int ready;
+    if (!ready) {
+        orc_warp_tab(0, tab);
+        ready = 1;
+    }
+    const int rd = AB_SCALE / INTER_TAB / 2;
+    for (int y = 0; y < dh; ++y) {
+        const int X0 = round_d((M[1] * y + M[2]) * AB_SCALE) + rd;
+        const int Y0 = round_d((M[4] * y + M[5]) * AB_SCALE) + rd;
+        for (int x = 0; x < dw; ++x) {
+            const int X = (X0 + round_d(M[0] * x * AB_SCALE)) >> (AB_BITS - INTER_BITS);
+            const int Y = (Y0 + round_d(M[3] * x * AB_SCALE)) >> (AB_BITS - INTER_BITS);
+            const int sx = X >> INTER_BITS, sy = Y >> INTER_BITS;
+            const short* w = tab + ((Y & (INTER_TAB - 1)) * INTER_TAB + (X & (INTER_TAB - 1))) * 4;
+            for (int c = 0; c < 3; ++c) {
+                int sum = 0;
+                for (int ky = 0; ky < 2; ++ky)
+                    for (int kx = 0; kx < 2; ++kx) {
+                        const int yy = sy + ky, xx = sx + kx;
+                        const int v = (yy >= 0 && yy < sh && xx >= 0 && xx < sw)
+                                          ? src[((size_t)yy * sw + xx) * 3 + c] : 0;
+                        sum += v * w[ky * 2 + kx];
+                    }
+                int u = (sum + (1 << 14)) >> 15;
+                u = u < 0 ? 0 : u > 255 ? 255 : u;
+                float f = (float)u;
+                if (normalize) f = f * (1 / 256.f) - 0.5f;
+                dst[((size_t)c * dh + y) * dw + x] = f;
+            }
+        }
+    }
+}

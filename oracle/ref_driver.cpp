@@ -85,6 +85,27 @@ extern "C" int ref_pose_table(int pose_model, unsigned* pairs, unsigned* map, in
     return (int)p.size();
 }
 
+// the body-part indices the face and hand detectors read (faceDetector.cpp:8-15 with
+// poseBodyPartMapStringToKey's name lists; handDetector.cpp:120-123, getPoseKeypoints): Neck,
+// Nose|Head, LEar|Head, REar|Head, LEye|Head, REye|Head, LWrist, LElbow, LShoulder, RWrist,
+// RElbow, RShoulder; -1 where the model has none of the names (the reference errors there)
+extern "C" int ref_pose_keys(int pose_model, int* keys)
+{
+    const auto model = (op::PoseModel)pose_model;
+    const std::vector<std::vector<std::string>> names = {
+        {"Neck"}, {"Nose", "Head"}, {"LEar", "Head"}, {"REar", "Head"}, {"LEye", "Head"},
+        {"REye", "Head"}, {"LWrist"}, {"LElbow"}, {"LShoulder"}, {"RWrist"}, {"RElbow"},
+        {"RShoulder"}};
+    for (size_t i = 0; i < names.size(); ++i) {
+        try {
+            keys[i] = (int)op::poseBodyPartMapStringToKey(model, names[i]);
+        } catch (const std::exception&) {
+            keys[i] = -1;
+        }
+    }
+    return 0;
+}
+
 // connectBodyPartsGpu's host half (bodyPartConnectorBase.cu:147-250) on host pair scores
 // [npairs][max_peaks][max_peaks]: the reference's pafVectorIntoPeopleVector,
 // removePeopleBelowThresholdsAndFillFaces and the people -> array copy-out.  pafPtrIntoVector takes
