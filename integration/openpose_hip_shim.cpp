@@ -13,7 +13,10 @@
 // (netCaffe.hpp:12-13), for PoseExtractorCaffe::addCaffeNetOnThread (poseExtractorCaffe.cpp:82-86),
 // loading the .caffemodel itself; and the members of op::CvMatToOpInput
 // (include/openpose/core/cvMatToOpInput.hpp:9-28, replaces src/openpose/core/cvMatToOpInput.cpp):
-// the frame -> net-input warp and normalisation on the GPU with the CPU branch's numerics.
+// the frame -> net-input warp and normalisation on the GPU with the CPU branch's numerics; and the
+// members of op::FaceExtractorCaffe / op::HandExtractorCaffe (faceExtractorCaffe.hpp:13-45,
+// handExtractorCaffe.hpp:13-58, replace src/openpose/{face,hand}/*ExtractorCaffe.cpp): every
+// rectangle of a frame cropped, run through the face / hand net and reduced on the GPU at once.
 // Numerics are the CPU path's; errors come back through op::error, the reference's
 // convention (errorAndLog.cpp:158-233).  See INTEGRATION.md for the build lines.
 #include <memory>
@@ -23,6 +26,10 @@
 
 #include <openpose/core/common.hpp>
 #include <openpose/core/cvMatToOpInput.hpp>
+#include <openpose/face/faceExtractorCaffe.hpp>
+#include <openpose/face/faceParameters.hpp>
+#include <openpose/hand/handExtractorCaffe.hpp>
+#include <openpose/hand/handParameters.hpp>
 #include <openpose/net/bodyPartConnectorBase.hpp>
 #include <openpose/net/net.hpp>
 #include <openpose/net/nmsBase.hpp>
@@ -338,5 +345,190 @@ namespace op
                   __FUNCTION__);
         }
         return inputNetData;
+    }
+
+    // ---- op::FaceExtractorCaffe / op::HandExtractorCaffe on libopk_hip ----------------------------
+    namespace
+    {
+        // the net, the extractor and the frame buffer of one extractor object (its worker thread)
+        struct KeypointNetHip
+        {
+            std::string proto, model;
+            int gpuId = 0;
+            opk_ctx* ctx = nullptr;
+            opk_net* net = nullptr;
+            opk_extractor* ex = nullptr;
+            void* frame = nullptr;
+            size_t frameBytes = 0;
+
+            ~KeypointNetHip()
+            {
+                if (ex)
+                    opk_extractor_destroy(ex);
+                if (net)
+                    opk_net_destroy(net);
+                if (frame && ctx)
+                    opk_free(ctx, frame);
+            }
+
+            void initialize(const int kind, const Point<int>& netSize)
+            {
+                ctx = threadContext(gpuId);
+                check(opk_net_create(ctx, proto.c_str(), model.c_str(), &net), __LINE__, __FUNCTION__);
+                check(opk_extractor_create(ctx, net, kind, netSize.x, netSize.y, &ex), __LINE__,
+                      __FUNCTION__);
+            }
+
+            // inputData (BGR uint8) -> device, rectangles -> keypoints [hands][people][parts][3]
+            std::vector<float> forward(const Matrix& inputData, const std::vector<float>& rects,
+                                       const int people, const int hands)
+            {
+                if (!ex)
+                    error("netInitializationOnThread() was not called.", __LINE__, __FUNCTION__, __FILE__);
+                if (inputData.empty())
+                    error("Empty cvInputData.", __LINE__, __FUNCTION__, __FILE__);
+                const size_t step = inputData.step1(0);
+                const size_t bytes = step * inputData.rows();
+                if (bytes > frameBytes)
+                {
+                    if (frame)
+                        opk_free(ctx, frame);
+                    frame = nullptr;
+                    check(opk_malloc(ctx, &frame, bytes), __LINE__, __FUNCTION__);
+                    frameBytes = bytes;
+                }
+                check(opk_memcpy_h2d(ctx, frame, inputData.dataConst(), bytes), __LINE__, __FUNCTION__);
+                const int parts = opk_extractor_parts(ex);
+                std::vector<float> keypoints((size_t)hands * people * parts * 3);
+                check(opk_extractor_forward(ex, static_cast<const unsigned char*>(frame), 1,
+                                            inputData.cols(), inputData.rows(), step, rects.data(),
+                                            nullptr, people, keypoints.data()),
+                      __LINE__, __FUNCTION__);
+                return keypoints;
+            }
+        };
+
+        void pushRectangle(std::vector<float>& out, const Rectangle<float>& r)
+        {
+            out.insert(out.end(), {r.x, r.y, r.width, r.height});
+        }
+    }
+
+    struct FaceExtractorCaffe::ImplFaceExtractorCaffe : KeypointNetHip {};
+
+    FaceExtractorCaffe::FaceExtractorCaffe(const Point<int>& netInputSize, const Point<int>& netOutputSize,
+                                           const std::string& modelFolder, const int gpuId,
+                                           const std::vector<HeatMapType>& heatMapTypes,
+                                           const ScaleMode heatMapScaleMode, const bool enableGoogleLogging) :
+        FaceExtractorNet{netInputSize, netOutputSize, heatMapTypes, heatMapScaleMode},
+        upImpl{new ImplFaceExtractorCaffe{}}
+    {
+        (void)enableGoogleLogging;
+        if (!heatMapTypes.empty())
+            error("Face heat maps are not produced by libopk_hip.", __LINE__, __FUNCTION__, __FILE__);
+        upImpl->proto = modelFolder + FACE_PROTOTXT;
+        upImpl->model = modelFolder + FACE_TRAINED_MODEL;
+        upImpl->gpuId = gpuId;
+    }
+
+    FaceExtractorCaffe::~FaceExtractorCaffe()
+    {
+    }
+
+    void FaceExtractorCaffe::netInitializationOnThread()
+    {
+        upImpl->initialize(OPK_EXTRACT_FACE, mNetOutputSize);
+    }
+
+    void FaceExtractorCaffe::forwardPass(const std::vector<Rectangle<float>>& faceRectangles,
+                                         const Matrix& inputData)
+    {
+        try
+        {
+            if (mEnabled && !faceRectangles.empty())
+            {
+                std::vector<float> rects;
+                for (const auto& r : faceRectangles)
+                    pushRectangle(rects, r);
+                const int people = (int)faceRectangles.size();
+                const auto keypoints = upImpl->forward(inputData, rects, people, 1);
+                mFaceKeypoints.reset({people, (int)FACE_NUMBER_PARTS, 3}, 0.f);
+                if (keypoints.size() != mFaceKeypoints.getVolume())
+                    error("The face net does not have 70 parts.", __LINE__, __FUNCTION__, __FILE__);
+                std::copy(keypoints.begin(), keypoints.end(), mFaceKeypoints.getPtr());
+            }
+            else
+                mFaceKeypoints.reset();
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+        }
+    }
+
+    struct HandExtractorCaffe::ImplHandExtractorCaffe : KeypointNetHip {};
+
+    HandExtractorCaffe::HandExtractorCaffe(const Point<int>& netInputSize, const Point<int>& netOutputSize,
+                                           const std::string& modelFolder, const int gpuId,
+                                           const int numberScales, const float rangeScales,
+                                           const std::vector<HeatMapType>& heatMapTypes,
+                                           const ScaleMode heatMapScaleMode, const bool enableGoogleLogging) :
+        HandExtractorNet{netInputSize, netOutputSize, numberScales, rangeScales, heatMapTypes, heatMapScaleMode},
+        upImpl{new ImplHandExtractorCaffe{}}
+    {
+        (void)enableGoogleLogging;
+        if (!heatMapTypes.empty())
+            error("Hand heat maps are not produced by libopk_hip.", __LINE__, __FUNCTION__, __FILE__);
+        upImpl->proto = modelFolder + HAND_PROTOTXT;
+        upImpl->model = modelFolder + HAND_TRAINED_MODEL;
+        upImpl->gpuId = gpuId;
+    }
+
+    HandExtractorCaffe::~HandExtractorCaffe()
+    {
+    }
+
+    void HandExtractorCaffe::netInitializationOnThread()
+    {
+        upImpl->initialize(OPK_EXTRACT_HAND, mNetOutputSize);
+        check(opk_extractor_set_scales(upImpl->ex, mMultiScaleNumberAndRange.first,
+                                       mMultiScaleNumberAndRange.second), __LINE__, __FUNCTION__);
+    }
+
+    void HandExtractorCaffe::forwardPass(const std::vector<std::array<Rectangle<float>, 2>> handRectangles,
+                                         const Matrix& inputData)
+    {
+        try
+        {
+            if (mEnabled && !handRectangles.empty())
+            {
+                std::vector<float> rects;
+                for (const auto& pair : handRectangles)
+                {
+                    pushRectangle(rects, pair[0]);
+                    pushRectangle(rects, pair[1]);
+                }
+                const int people = (int)handRectangles.size();
+                const auto keypoints = upImpl->forward(inputData, rects, people, 2);
+                const size_t half = keypoints.size() / 2;
+                for (auto hand = 0; hand < 2; hand++)
+                {
+                    mHandKeypoints[hand].reset({people, (int)HAND_NUMBER_PARTS, 3}, 0.f);
+                    if (half != mHandKeypoints[hand].getVolume())
+                        error("The hand net does not have 21 parts.", __LINE__, __FUNCTION__, __FILE__);
+                    std::copy(keypoints.begin() + hand * half, keypoints.begin() + (hand + 1) * half,
+                              mHandKeypoints[hand].getPtr());
+                }
+            }
+            else
+            {
+                mHandKeypoints[0].reset();
+                mHandKeypoints[1].reset();
+            }
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+        }
     }
 }
