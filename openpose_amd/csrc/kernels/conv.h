@@ -37,6 +37,7 @@ struct ConvArgs {
     int out32_c, out32_coff;
     int sw, nstrips;      // conv3 only: strip width and count (conv3_shape)
     float rcp[3];         // conv3 only, set by launch_conv3: 1/((H+2)(sw+2)), 1/(sw+2), 1/nstrips
+    int wide;             // conv3 only, set by launch_conv3: 16-byte epilogue stores allowed (dev A/B switch)
     void* sink;           // conv3 persistent variant: >= kConv3SinkBytes of scratch (masked stores)
     int cus;              // conv3 persistent variant: compute units (grid size); 0 disables it
     int border;           // zero border of the padded images (conv3 / conv_image; 0 means 1)
@@ -52,7 +53,7 @@ void launch_conv2(const ConvArgs& a, int bn, hipStream_t stream);
 // Weights packed [cout_pad/BN][cin_pad/32][ky][kx][BN][32] (BN = conv3_shape(...).bn).  Reads padded positions down to -1
 // and the whole row past the last one: buffers carry zeroed guards (kConvGuardTail positions).
 constexpr int kConvGuardTail = 1024;   // positions
-constexpr size_t kConv3SinkBytes = (size_t)1024 * 1024 * 8;   // 1024 lanes x 1024 workgroups x 8 B
+constexpr size_t kConv3SinkBytes = (size_t)1024 * 1024 * 16;   // 1024 lanes x 1024 workgroups x 16 B
 struct Conv3Shape {
     int ks;                       // 7, 3 or 1
     int border;                   // zero border of the net's padded images

@@ -355,6 +355,40 @@ void conv3_kernel(const ConvArgs a)
     }
     const int chl = n0 + wn * WN + 4 * q;   // this lane's first channel (fragment j adds 16 j)
     const bool vec = (a.cout & 3) == 0;
+    // 16-byte stores (see conv3p_kernel): fragment pairs exchanged between lane rows q and q^1 by
+    // v_permlane16_swap, each lane then holds 8 consecutive channels of its position.  Needs whole
+    // 8-channel groups and 16-byte aligned destination slices; OPK_CONV3_WIDE=0 (dev A/B) disables.
+    bool wide = NF % 2 == 0 && (a.cout & 7) == 0 && !a.out32 && a.wide;
+    for (int d = 0; d < a.ndst; ++d) wide = wide && ((a.dst_coff[d] | a.dst_cs[d]) & 7) == 0;
+    if (wide) {
+        const int cw = n0 + wn * WN + 16 * (q & 1) + 8 * (q >> 1);
+#pragma unroll
+        for (int j = 0; j + 1 < NF; j += 2) {
+#pragma unroll
+            for (int i = 0; i < MF; ++i) {
+                uint32_t pk[2][2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float4_t t = acc[i][j + h] + bv[j + h];
+                    const float4_t tm = t * mv[j + h];
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
+                    pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+                    pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                }
+                // every lane takes part in the swap; masked lanes store nothing afterwards
+                const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+                const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+                if (!pok[i] || cw + j * 16 >= a.cout) continue;
+                const uint4 val = make_uint4(sl[0], sh[0], sl[1], sh[1]);
+                for (int d = 0; d < a.ndst; ++d)
+                    *reinterpret_cast<uint4*>(a.dst[d] + a.dst_coff[d] + cw + j * 16 + prow[i] * a.dst_cs[d]) = val;
+            }
+        }
+        OPK3_STAMP(5);
+        return;
+    }
     // fragment column j outer, row i inner: each (i, j) is activated, packed and stored at once
 #pragma unroll
     for (int j = 0; j < NF; ++j) {
@@ -407,8 +441,9 @@ void conv3_kernel(const ConvArgs a)
 // previous tile's epilogue.  Bias/slopes live in LDS for the whole launch.
 //
 // vmcnt counts stores as well as loads on gfx950 and retires in issue order, so the counted waits
-// must know how many stores an epilogue issued: every (fragment, destination) pair issues exactly
-// one 8-byte store (lanes of border positions write to a scratch "sink"), S = MF*NF*ndst.
+// must know how many stores an epilogue issued: every (fragment pair, destination) issues exactly
+// one 16-byte store, plus one 8-byte store per odd last fragment (lanes of border positions write
+// to a scratch "sink"), S = MF*(NF/2 + NF%2)*ndst.
 #define OPK3_VM_CASE(n_) case n_: vm_wait<n_>(); break;
 __device__ __forceinline__ void vm_wait_rt64(int n)
 {
@@ -433,7 +468,15 @@ __device__ __forceinline__ void vm_wait_rt64(int n)
 
 constexpr int kP_BM = 512, kP_HR = 688, kP_NW = 16;
 
-template <int BN>
+// LDS fragment reads with explicit counters (ASMR): the compiler streams one fragment at a time
+// behind s_waitcnt lgkmcnt(0) at the 128-VGPR budget (one LDS round trip per 4 MFMAs per wave);
+// here the next A fragment is always in flight while the current one's MFMAs issue.  The wait is
+// an asm statement that takes the fragments it covers as in/out operands, so every MFMA using
+// them is ordered after it; inside the K loop no other LGKM traffic is outstanding (no SMEM, no
+// compiler-issued LDS access), so the counts are exact.
+#define OPK3_DSR(dst_, addr_, off_)                                                           \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst_) : "v"(addr_), "i"(off_))
+template <int BN, bool ASMR, bool WIDE>
 __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
 {
     constexpr int NW = kP_NW, BM = kP_BM, HR = kP_HR;
@@ -524,7 +567,7 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
                     16, 0, 0);                                                                \
     } while (0)
 
-    const int S = MF * NF * a.ndst;               // store instructions per epilogue and wave
+    const int S = (WIDE ? MF * (NF / 2 + NF % 2) : MF * NF) * a.ndst;   // store instructions per epilogue and wave
     const bool exact = S + ai + bi <= 63;
 
     OPK3P_AROW(m);
@@ -563,6 +606,66 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
             OPK3P_PREFETCH();
             const uint4* As = lds + ((gc + c) & 1) * ASLOT;
             const uint4* Bs = lds + 2 * ASLOT + (u % 3) * BSLOT;
+            if constexpr (ASMR) {
+                static_assert(MF == 4 && NF >= 2 && NF <= 4, "ASMR fragment schedule");
+                // rows i*16 / j*16 / kx*BN keep row bit 2, hence the swizzle: one lane base per
+                // tap and operand, constant offsets (1 KiB per 16 rows)
+                const uint32_t bb = (uint32_t)(uintptr_t)(Bs + swz64(wn * WN + r16, q));
+                const int arow = wm * WROWS + r16 + ky * g.VW;
+                uint32_t ab = (uint32_t)(uintptr_t)(As + swz64(arow, q));
+                half8_t fb[4], fa0, fa1;
+                OPK3_DSR(fb[0], bb, 0);
+                OPK3_DSR(fb[1], bb, 1024);
+                if (NF > 2) OPK3_DSR(fb[2], bb, 2048);
+                if (NF > 3) OPK3_DSR(fb[3], bb, 3072);
+                OPK3_DSR(fa0, ab, 0);
+#pragma unroll
+                for (int kx = 0; kx < 3; ++kx) {
+#pragma unroll
+                    for (int i = 0; i < MF; ++i) {
+                        half8_t& cur = (i & 1) ? fa1 : fa0;
+                        half8_t& nxt = (i & 1) ? fa0 : fa1;
+                        if (i + 1 < MF) {
+                            switch (i) {
+                            case 0: OPK3_DSR(nxt, ab, 1024); break;
+                            case 1: OPK3_DSR(nxt, ab, 2048); break;
+                            default: OPK3_DSR(nxt, ab, 3072); break;
+                            }
+                            // everything but the fragment just issued has landed
+                            if (i == 0)
+                                asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(cur), "+v"(fb[0]), "+v"(fb[1]), "+v"(fb[2]), "+v"(fb[3]));
+                            else
+                                asm volatile("s_waitcnt lgkmcnt(1)" : "+v"(cur));
+                        } else {
+                            asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur));
+                        }
+#pragma unroll
+                        for (int j = 0; j < NF; ++j)
+                            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], cur, acc[i][j], 0, 0, 0);
+                        __builtin_amdgcn_sched_barrier(0);   // keep the issue order as written
+                    }
+                    if (kx < 2) {   // next tap: its weights and first A fragment
+                        ab = (uint32_t)(uintptr_t)(As + swz64(arow + kx + 1, q));
+                        const int bo = (kx + 1) * BN * 64;
+                        OPK3_DSR(fa0, ab, 0);
+                        switch (kx) {
+                        case 0:
+                            OPK3_DSR(fb[0], bb, BN * 64);
+                            OPK3_DSR(fb[1], bb, BN * 64 + 1024);
+                            if (NF > 2) OPK3_DSR(fb[2], bb, BN * 64 + 2048);
+                            if (NF > 3) OPK3_DSR(fb[3], bb, BN * 64 + 3072);
+                            break;
+                        default:
+                            OPK3_DSR(fb[0], bb, 2 * BN * 64);
+                            OPK3_DSR(fb[1], bb, 2 * BN * 64 + 1024);
+                            if (NF > 2) OPK3_DSR(fb[2], bb, 2 * BN * 64 + 2048);
+                            if (NF > 3) OPK3_DSR(fb[3], bb, 2 * BN * 64 + 3072);
+                            break;
+                        }
+                        (void)bo;
+                    }
+                }
+            } else {
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
                 half8_t fa[MF], fb[NF];
@@ -578,6 +681,7 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
 #pragma unroll
                     for (int j = 0; j < NF; ++j)
                         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+            }
             }
         }
 #undef OPK3P_PREFETCH
@@ -615,20 +719,46 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
         int sidx = blockIdx.x * 64 * NW + tid;    // this lane's sink slot
         asm volatile("" : "+v"(sidx));
         uint2* sink = reinterpret_cast<uint2*>(a.sink) + sidx;
+        uint4* sink4 = reinterpret_cast<uint4*>(a.sink) + sidx;
+        // bias + activation + fp16 pack of fragment (i, j): 4 channels of one position
+#define OPK3P_ACT(i_, j_, lo_, hi_)                                                           \
+    do {                                                                                      \
+        const int cl_ = wn * WN + (j_) * 16 + 4 * q;   /* channel within the n-block */       \
+        const float4_t t_ = acc[i_][j_] + *reinterpret_cast<const float4_t*>(lbias + cl_);    \
+        const float4_t tm_ = t_ * *reinterpret_cast<const float4_t*>(lmul + cl_);             \
+        float v_[4];                                                                          \
+        _Pragma("unroll") for (int r_ = 0; r_ < 4; ++r_) v_[r_] = t_[r_] > 0.f ? t_[r_] : tm_[r_]; \
+        lo_ = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v_[0], v_[1]}, half2_t)); \
+        hi_ = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v_[2], v_[3]}, half2_t)); \
+    } while (0)
+        // fragment pairs (j, j+1): v_permlane16_swap of lane rows q <-> q^1 leaves every lane 8
+        // consecutive channels of its position, 16 (j + (q & 1)) + 8 (q >> 1) .. + 7: one dwordx4
+        // store per pair instead of two dwordx2 (the epilogue is store-issue bound)
+        const int cw = n0 + wn * WN + 16 * (q & 1) + 8 * (q >> 1);
 #pragma unroll
-        for (int j = 0; j < NF; ++j) {
-            const int cl = wn * WN + j * 16 + 4 * q;   // channel within the n-block
-            const float4_t bj = *reinterpret_cast<const float4_t*>(lbias + cl);
-            const float4_t mj = *reinterpret_cast<const float4_t*>(lmul + cl);
+        for (int j = 0; WIDE && j + 1 < NF; j += 2) {
 #pragma unroll
             for (int i = 0; i < MF; ++i) {
-                const float4_t t = acc[i][j] + bj;
-                const float4_t tm = t * mj;
-                float v[4];
+                uint32_t lo0, hi0, lo1, hi1;
+                OPK3P_ACT(i, j, lo0, hi0);
+                OPK3P_ACT(i, j + 1, lo1, hi1);
+                const auto sl = __builtin_amdgcn_permlane16_swap(lo0, lo1, false, false);
+                const auto sh = __builtin_amdgcn_permlane16_swap(hi0, hi1, false, false);
+                const uint4 val = make_uint4(sl[0], sh[0], sl[1], sh[1]);
+                for (int d = 0; d < a.ndst; ++d) {
+                    uint4* p = reinterpret_cast<uint4*>(a.dst[d] + a.dst_coff[d] + cw + j * 16 +
+                                                        prow[i] * a.dst_cs[d]);
+                    *(pok[i] ? p : sink4) = val;
+                }
+            }
+        }
+        // odd fragment count (96 channels): the last one as dwordx2; !WIDE (dev A/B): all of them
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
-                const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
-                const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+        for (int j = WIDE ? NF - NF % 2 : 0; j < NF; ++j) {
+#pragma unroll
+            for (int i = 0; i < MF; ++i) {
+                uint32_t lo, hi;
+                OPK3P_ACT(i, j, lo, hi);
                 for (int d = 0; d < a.ndst; ++d) {
                     uint2* p = reinterpret_cast<uint2*>(a.dst[d] + a.dst_coff[d] + chl + j * 16 +
                                                         prow[i] * a.dst_cs[d]);
@@ -636,6 +766,7 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
                 }
             }
         }
+#undef OPK3P_ACT
         if (!has_next) break;
         m = mn;
         gc += cpt;
@@ -678,6 +809,14 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border)
         s.minb = 2;
         s.nstrips = 1;
         s.sw = W;
+        // dev A/B: OPK_CONV1_TILE=1 -> 512x128 tiles of 16 waves, 2 -> 256x256 tiles of 16 waves
+        // (cout % 256 == 0): fewer tile rows staged per MFMA than 256x128
+        const int t1 = env_int("OPK_CONV1_TILE", 0);
+        if (t1 == 1 && s.bn == 128) {
+            s.bm = 512; s.hr = 512; s.nw = 16; s.minb = 1;
+        } else if (t1 == 2 && cout % 256 == 0) {
+            s.bn = 256; s.nw = 16; s.minb = 1;
+        }
         return s;
     }
     s.nw = 8;
@@ -716,6 +855,7 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
 {
     ConvArgs a = args;   // + the reciprocals of the strip geometry (Strips::map, kernel arguments)
     if (a.border <= 0) a.border = 1;
+    a.wide = env_int("OPK_CONV3_WIDE", 1);
     const int B = a.border;
     a.rcp[0] = (float)(1.0 / ((double)(a.H + 2 * B) * (a.sw + 2 * B)));
     a.rcp[1] = (float)(1.0 / (double)(a.sw + 2 * B));
@@ -740,18 +880,29 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     if (s.nw == 16 && s.persist && nn == 1 && a.sink && a.cus >= nn && a.cout % s.bn == 0 && !a.out32 &&
         VW > 16) {
         bool aligned = true;
-        for (int d = 0; d < a.ndst; ++d) aligned = aligned && ((a.dst_coff[d] | a.dst_cs[d]) & 3) == 0;
+        // 16-byte stores of 8-channel groups
+        for (int d = 0; d < a.ndst; ++d) aligned = aligned && ((a.dst_coff[d] | a.dst_cs[d]) & 7) == 0;
         if (aligned) {   // one workgroup per CU, n-blocks spread evenly over the grid
             const long per_n = std::min<long>(a.cus / nn, (ntiles + nn - 1) / nn);
             const unsigned G = (unsigned)(per_n * nn);
             OPK_CHECK_ARG(G <= 1024, "persistent grid exceeds the sink");
             // (measured, round 1: a 32x32x16-MFMA version of this kernel with double-buffered
             // fragments ran 20 % slower on the 128-channel layers; a pipelined 16x16x32 fragment
-            // schedule spilled at the 128-VGPR budget and ran 4 % slower)
-            if (s.bn == 96)
-                hipLaunchKernelGGL((conv3p_kernel<96>), dim3(G), dim3(1024), 0, stream, a);
-            else
-                hipLaunchKernelGGL((conv3p_kernel<128>), dim3(G), dim3(1024), 0, stream, a);
+            // schedule spilled at the 128-VGPR budget and ran 4 % slower; the explicit-counter
+            // fragment schedule measured 1.5 % faster over the whole CNN, bit-identical)
+            const bool asmr = env_int("OPK_CONV3P_ASMR", 1) != 0;
+            // 16-byte epilogue stores (measured in tools/ab_asmr.sh; OPK_CONV3P_WIDE=0: dwordx2)
+            const bool wide = env_int("OPK_CONV3P_WIDE", 1) != 0;
+#define OPK3P_LAUNCH(BN_, ASMR_, WIDE_)                                                        \
+    hipLaunchKernelGGL((conv3p_kernel<BN_, ASMR_, WIDE_>), dim3(G), dim3(1024), 0, stream, a)
+            if (s.bn == 96) {
+                if (asmr) { if (wide) OPK3P_LAUNCH(96, true, true); else OPK3P_LAUNCH(96, true, false); }
+                else OPK3P_LAUNCH(96, false, true);
+            } else {
+                if (asmr) { if (wide) OPK3P_LAUNCH(128, true, true); else OPK3P_LAUNCH(128, true, false); }
+                else OPK3P_LAUNCH(128, false, true);
+            }
+#undef OPK3P_LAUNCH
             OPK_LAUNCH_CHECK();
             return;
         }
@@ -764,7 +915,13 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
         else if (s.bn == 96) OPK3_LAUNCH(256, 96, 1024, 1, 1, 7);
         else OPK3_LAUNCH(256, 128, 1024, 1, 1, 7);
     } else if (ks == 1) {
-        if (s.bn == 64) OPK3_LAUNCH(256, 64, 256, 1, 2, 1);
+        if (s.nw == 16 && s.bn == 256)
+            hipLaunchKernelGGL((conv3_kernel<256, 256, 256, 1, 1, 1, 16>), grid, dim3(1024), 0,
+                               stream, a);
+        else if (s.nw == 16)
+            hipLaunchKernelGGL((conv3_kernel<512, 128, 512, 1, 1, 1, 16>), grid, dim3(1024), 0,
+                               stream, a);
+        else if (s.bn == 64) OPK3_LAUNCH(256, 64, 256, 1, 2, 1);
         else if (s.bn == 96) OPK3_LAUNCH(256, 96, 256, 1, 2, 1);
         else OPK3_LAUNCH(256, 128, 256, 1, 2, 1);
     } else if (s.bn == 64) {

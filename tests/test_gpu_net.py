@@ -152,7 +152,11 @@ def test_7x7_cpm_stages_vs_oracle(ctx, concat, hw):
 
 
 VARIANTS = {"persistent": {}, "w16": {"OPK_CONV3_PERSIST": "0"},
-            "w8": {"OPK_CONV3_W16": "0"}, "w8_one_per_cu": {"OPK_CONV3_W16": "0", "OPK_CONV3_SMALL": "0"}}
+            "w8": {"OPK_CONV3_W16": "0"}, "w8_one_per_cu": {"OPK_CONV3_W16": "0", "OPK_CONV3_SMALL": "0"},
+            "persistent_compiler_frags": {"OPK_CONV3P_ASMR": "0"}, "persistent_dwordx2": {"OPK_CONV3P_WIDE": "0"},
+            "dwordx2": {"OPK_CONV3P_WIDE": "0", "OPK_CONV3_WIDE": "0"},
+            "w16_dwordx2": {"OPK_CONV3_PERSIST": "0", "OPK_CONV3_WIDE": "0"},
+            "conv1_512x128": {"OPK_CONV1_TILE": "1"}, "conv1_256x256": {"OPK_CONV1_TILE": "2"}}
 ROUNDING_VARIANTS = set()   # variants with another MFMA shape (another fp32 summation order)
 
 
@@ -165,7 +169,8 @@ def test_conv3_tile_variants_bit_identical(ctx):
     L += conv("c3", "c2", 96, 3, "prelu") + conv("c4", "c3", 128, 3, "prelu")
     L += conv("c5", "c4", 96, 3, "relu")
     L.append(dict(name="cat", type="Concat", bottom=["c3", "c5"], top=["cat"]))
-    L += conv("c6", "cat", 128, 3, "prelu") + conv("c6b", "c6", 256, 3, "relu") + conv("c7", "c6b", 52, 1)
+    L += conv("c6", "cat", 128, 3, "prelu") + conv("c6b", "c6", 256, 3, "relu")
+    L += conv("c6c", "c6b", 512, 1, "prelu") + conv("c7", "c6c", 52, 1)
     L.append(dict(name="net_output", type="Concat", bottom=["c7"], top=["net_output"]))
     text = prototxt.emit(L)
     graph = prototxt.parse(text)
