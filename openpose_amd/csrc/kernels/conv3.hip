@@ -811,7 +811,8 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border)
         s.sw = W;
         // dev A/B: OPK_CONV1_TILE=1 -> 512x128 tiles of 16 waves, 2 -> 256x256 tiles of 16 waves
         // (cout % 256 == 0): fewer tile rows staged per MFMA than 256x128
-        const int t1 = env_int("OPK_CONV1_TILE", 0);
+        // (default 2: measured -10..-20 % on the 384->512 and 288->256 layers)
+        const int t1 = env_int("OPK_CONV1_TILE", 2);
         if (t1 == 1 && s.bn == 128) {
             s.bm = 512; s.hr = 512; s.nw = 16; s.minb = 1;
         } else if (t1 == 2 && cout % 256 == 0) {
