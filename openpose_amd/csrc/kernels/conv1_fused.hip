@@ -16,6 +16,8 @@
 //   3. conv1_2 is an implicit GEMM over the halo's "virtual image" of row width VW = 64
 //      (TR x 64 rows, columns >= TC discarded): 2 channel chunks x 9 taps, no barrier inside;
 //   4. bias + activation, fp16 tile to LDS, 2x2 max, one 16-byte store per 8 pooled channels.
+// LDS writes of fp16 results go through v_permlane16_swap of fragment pairs so that every lane
+// writes 16 consecutive bytes (ds_write_b128) instead of 8 (fewer instructions, fewer conflicts).
 // Only the image is read and only pool1's output is written.
 #include "conv.h"
 
@@ -162,6 +164,7 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
                 xf[e] = off[e] >= 0 ? (_Float16)patch[off[e] + hr * PC + hc] : (_Float16)0.f;
             const int y = y0 - 1 + hr, x = x0 - 1 + hc;
             const bool in = y >= 0 && y < H && x >= 0 && x < W;
+            uint32_t pk[4][2];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 float4_t c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1f[g], xf, float4_t{0.f, 0.f, 0.f, 0.f},
@@ -171,13 +174,18 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
                 float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = in ? (t[r] > 0.f ? t[r] : tm[r]) : 0.f;
-                uint2 pk;
-                pk.x = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
-                pk.y = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
-                // channels g*16 + 4q .. +3: chunk g/2, 16-byte piece (g&1)*2 + q/2, half q&1
-                char* dst = reinterpret_cast<char*>(HALO + (g >> 1) * HROWS * 4 +
-                                                    swz64(mh, (g & 1) * 2 + (q >> 1))) + (q & 1) * 8;
-                *reinterpret_cast<uint2*>(dst) = pk;
+                pk[g][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+                pk[g][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+            }
+            // chunk c = channels 32c .. 32c+31 (groups 2c, 2c+1): v_permlane16_swap between lane
+            // rows q and q^1 leaves lane row q channels 16 (q & 1) + 8 (q >> 1) .. +7 of the chunk,
+            // i.e. 16-byte piece 2 (q & 1) + (q >> 1): one ds_write_b128 per chunk (8-lane groups,
+            // at most 2-way bank conflicts) instead of two 4-way conflicting ds_write_b64
+#pragma unroll
+            for (int c = 0; c < 2; ++c) {
+                const auto sl = __builtin_amdgcn_permlane16_swap(pk[2 * c][0], pk[2 * c + 1][0], false, false);
+                const auto sh = __builtin_amdgcn_permlane16_swap(pk[2 * c][1], pk[2 * c + 1][1], false, false);
+                HALO[c * HROWS * 4 + swz64(mh, 2 * (q & 1) + (q >> 1))] = make_uint4(sl[0], sh[0], sl[1], sh[1]);
             }
         }
         __syncthreads();
@@ -216,6 +224,7 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
             const int m = wave * 48 + i * 16 + r16;
+            uint32_t pk[4][2];
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const float4_t t = acc[i][j] + b2[j];
@@ -223,10 +232,16 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
                 float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
-                uint2 pk;
-                pk.x = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
-                pk.y = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
-                *reinterpret_cast<uint2*>(T + m * TSTRIDE + j * 16 + 4 * q) = pk;
+                pk[j][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+                pk[j][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+            }
+            // fragment pairs as in the halo write: 8 consecutive channels per lane, ds_write_b128
+#pragma unroll
+            for (int j = 0; j < 4; j += 2) {
+                const auto sl = __builtin_amdgcn_permlane16_swap(pk[j][0], pk[j + 1][0], false, false);
+                const auto sh = __builtin_amdgcn_permlane16_swap(pk[j][1], pk[j + 1][1], false, false);
+                *reinterpret_cast<uint4*>(T + m * TSTRIDE + j * 16 + 16 * (q & 1) + 8 * (q >> 1)) =
+                    make_uint4(sl[0], sh[0], sl[1], sh[1]);
             }
         }
         __syncthreads();
