@@ -817,6 +817,8 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border)
             s.bm = 512; s.hr = 512; s.nw = 16; s.minb = 1;
         } else if (t1 == 2 && cout % 256 == 0) {
             s.bn = 256; s.nw = 16; s.minb = 1;
+        } else if (s.bn == 64 && env_int("OPK_CONV1_N64W16", 0) != 0) {   // dev A/B: 512x64, 16 waves
+            s.bm = 512; s.hr = 512; s.nw = 16; s.minb = 1;
         }
         return s;
     }
@@ -918,6 +920,9 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     } else if (ks == 1) {
         if (s.nw == 16 && s.bn == 256)
             hipLaunchKernelGGL((conv3_kernel<256, 256, 256, 1, 1, 1, 16>), grid, dim3(1024), 0,
+                               stream, a);
+        else if (s.nw == 16 && s.bn == 64)
+            hipLaunchKernelGGL((conv3_kernel<512, 64, 512, 1, 1, 1, 16>), grid, dim3(1024), 0,
                                stream, a);
         else if (s.nw == 16)
             hipLaunchKernelGGL((conv3_kernel<512, 128, 512, 1, 1, 1, 16>), grid, dim3(1024), 0,

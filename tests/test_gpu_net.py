@@ -156,7 +156,7 @@ VARIANTS = {"persistent": {}, "w16": {"OPK_CONV3_PERSIST": "0"},
             "persistent_compiler_frags": {"OPK_CONV3P_ASMR": "0"}, "persistent_dwordx2": {"OPK_CONV3P_WIDE": "0"},
             "dwordx2": {"OPK_CONV3P_WIDE": "0", "OPK_CONV3_WIDE": "0"},
             "w16_dwordx2": {"OPK_CONV3_PERSIST": "0", "OPK_CONV3_WIDE": "0"},
-            "conv1_512x128": {"OPK_CONV1_TILE": "1"}, "conv1_256x128": {"OPK_CONV1_TILE": "0"}}
+            "conv1_512x128": {"OPK_CONV1_TILE": "1"}, "conv1_256x128": {"OPK_CONV1_TILE": "0"}, "conv1_512x64": {"OPK_CONV1_N64W16": "1"}}
 ROUNDING_VARIANTS = set()   # variants with another MFMA shape (another fp32 summation order)
 
 
