@@ -38,6 +38,7 @@ struct ConvArgs {
     int sw, nstrips;      // conv3 only: strip width and count (conv3_shape)
     float rcp[3];         // conv3 only, set by launch_conv3: 1/((H+2)(sw+2)), 1/(sw+2), 1/nstrips
     int wide;             // conv3 only, set by launch_conv3: 16-byte epilogue stores allowed (dev A/B switch)
+    int prio;             // conv3 persistent: s_setprio(1) around each unit's MFMAs (dev A/B switch)
     void* sink;           // conv3 persistent variant: >= kConv3SinkBytes of scratch (masked stores)
     int cus;              // conv3 persistent variant: compute units (grid size); 0 disables it
     int border;           // zero border of the padded images (conv3 / conv_image; 0 means 1)

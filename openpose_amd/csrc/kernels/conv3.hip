@@ -619,6 +619,7 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
                 if (NF > 2) OPK3_DSR(fb[2], bb, 2048);
                 if (NF > 3) OPK3_DSR(fb[3], bb, 3072);
                 OPK3_DSR(fa0, ab, 0);
+                if (a.prio) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
                 for (int kx = 0; kx < 3; ++kx) {
 #pragma unroll
@@ -665,6 +666,7 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
                         (void)bo;
                     }
                 }
+                if (a.prio) __builtin_amdgcn_s_setprio(0);
             } else {
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
@@ -859,6 +861,7 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     ConvArgs a = args;   // + the reciprocals of the strip geometry (Strips::map, kernel arguments)
     if (a.border <= 0) a.border = 1;
     a.wide = env_int("OPK_CONV3_WIDE", 1);
+    a.prio = env_int("OPK_CONV3P_PRIO", 0);
     const int B = a.border;
     a.rcp[0] = (float)(1.0 / ((double)(a.H + 2 * B) * (a.sw + 2 * B)));
     a.rcp[1] = (float)(1.0 / (double)(a.sw + 2 * B));
