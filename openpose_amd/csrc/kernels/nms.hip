@@ -19,6 +19,7 @@
 //      call.  A plane with more than kNmsCandidates peaks (noise, not poses) is re-scanned in
 //      raster order by its workgroup, so the result never depends on the candidate capacity.
 // -ffp-contract=off keeps the centroid sums bit-identical to the CPU.
+#include <cstdlib>
 #include "kernels.h"
 #include "heat_dev.h"
 #include "../common.h"
@@ -94,13 +95,16 @@ __global__ __launch_bounds__(DT) void nms_detect_kernel(int* __restrict__ scratc
 // is never written.
 constexpr int LT = 256;           // lanes = window columns
 constexpr int LOX = LT - 2;       // tile columns
-constexpr int LOY = 16;           // tile rows
-constexpr int LWR = LOY + 2;      // window rows
-constexpr int LMAXR = 16;         // source rows per window kept in LDS (x8 upsampling needs 7)
+constexpr int LMAXR = 16;         // source rows per window kept in LDS (x8 upsampling of a
+                                  // 34-row window needs 9)
 
+// LOY = tile rows (window rows LOY + 2): 32 measured faster than 16 (half the per-workgroup
+// fixed cost and window halo per pixel); OPK_NMS_LOY selects 16 / 32 / 48 (dev A/B)
+template <int LOY>
 __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ scratch,
                                                              const HeatMap M, int parts, float th)
 {
+    constexpr int LWR = LOY + 2;      // window rows
     // hb (horizontal-pass rows) and win (window values) share LDS: a lane only ever touches its
     // own column of either before the barrier, and win is written after the last hb read
     static_assert(LMAXR <= LWR, "hb fits in win");
@@ -340,9 +344,15 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat, int frames, int
         hipLaunchKernelGGL(nms_detect_kernel, g1, dim3(DT), 0, stream, scratch, heat.heat,
                            heat.channels, parts, h, w, threshold);
     } else {
-        dim3 g1((w + LOX - 1) / LOX, (h + LOY - 1) / LOY, frames * parts);
-        hipLaunchKernelGGL(nms_detect_lazy_kernel, g1, dim3(LT), 0, stream, scratch, heat, parts,
-                           threshold);
+        const char* e = std::getenv("OPK_NMS_LOY");
+        const int loy = e && e[0] ? std::atoi(e) : 16;
+#define OPK_NMS_LAZY(LOY_)                                                                    \
+    hipLaunchKernelGGL(nms_detect_lazy_kernel<LOY_>, dim3((w + LOX - 1) / LOX, (h + LOY_ - 1) / LOY_, \
+                       frames * parts), dim3(LT), 0, stream, scratch, heat, parts, threshold)
+        if (loy == 16) OPK_NMS_LAZY(16);
+        else if (loy == 48) OPK_NMS_LAZY(48);
+        else OPK_NMS_LAZY(32);
+#undef OPK_NMS_LAZY
     }
     OPK_LAUNCH_CHECK();
     dim3 g2(parts, frames);
