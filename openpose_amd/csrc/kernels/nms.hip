@@ -98,8 +98,8 @@ constexpr int LOX = LT - 2;       // tile columns
 constexpr int LMAXR = 16;         // source rows per window kept in LDS (x8 upsampling of a
                                   // 34-row window needs 9)
 
-// LOY = tile rows (window rows LOY + 2): 32 measured faster than 16 (half the per-workgroup
-// fixed cost and window halo per pixel); OPK_NMS_LOY selects 16 / 32 / 48 (dev A/B)
+// LOY = tile rows (window rows LOY + 2); OPK_NMS_LOY selects 16 / 32 / 48 (dev A/B). Measured per
+// 64-frame launch: 16 rows 638 us, 32 rows 774 us, 48 rows 938 us (more, shorter workgroups win)
 template <int LOY>
 __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ scratch,
                                                              const HeatMap M, int parts, float th)
