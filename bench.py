@@ -1,23 +1,30 @@
 #!/usr/bin/env python3
 """bench.py -- OpenPose BODY_25 hot path on MI355X: frames/sec, whole node.
 
-Workload (BASELINE.json configs[1], one GPU; configs[2] when launched with --gpus N under
-torch.distributed.run): BODY_25 at net_resolution -1x368 on synthetic 1280x720 BGR uint8 frames.
-One step = one batch of frames per GPU through the reference's whole per-frame path
-(ScaleAndSizeExtractor -> CvMatToOpInput -> PoseExtractorCaffe::forwardPass):
+Workload (BASELINE.json configs[1] on one GPU; configs[2] with --gpus N): BODY_25 at
+net_resolution -1x368 on synthetic 1280x720 BGR uint8 frames.  One step = one batch of frames per
+GPU through the reference's whole per-frame path (ScaleAndSizeExtractor -> CvMatToOpInput ->
+PoseExtractorCaffe::forwardPass):
     warpAffine 1280x720 -> 656x368 + normalisation -> CNN forward (114 convs, MFMA fp16 / fp32
     accumulate) -> + people overlay -> resize x8 (78 maps) -> NMS (25 parts) -> PAF line integrals
-    -> host people assembly -> keypoints per frame.
+    -> host people assembly -> per-frame keypoint records -> ordered gather to rank 0.
+`--config multiscale` runs BASELINE configs[3] instead (--scale_number 4 --scale_gap 0.25: nets at
+656x368, 480x272, 320x176, 160x80 per frame, their x8 resizes averaged).
 Inputs are resident in HBM before timing: uint8 frames (uniform random pixels) and per-frame
 5-person overlays (synthetic weights carry no meaning, so a deterministic people field is added to
 the net output -- its cost is counted).
 
-Frames shard across ranks with no collective in the data path (frame-parallel replicas, weak
-scaling); the only cross-rank traffic is the barrier and the max-reduce of the timer.
+Multi-GPU (--gpus N): one process per GPU.  Started under torch.distributed.run the ranks come
+from the environment; started directly, this process spawns N ranks (openpose_amd.parallel.
+launch_ranks) before any GPU call and waits for them.  Frames shard across ranks with no
+collective in the data path (frame-parallel replicas, weak scaling); every step, each rank's
+per-frame keypoint records are gathered to rank 0 in frame order (RCCL gather over xGMI, the
+reference's WQueueOrderer), inside the timed region.
 """
 import argparse
 import json
 import os
+import platform
 import sys
 import time
 
@@ -27,10 +34,17 @@ import torch
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+from openpose_amd import parallel  # noqa: E402  (no GPU call at import)
+
 METRIC = "frames/sec whole-node, BODY_25 -1x368 @1280x720, 1/2/4/8 GPU + CPU ref"
 NET_H, NET_W = 368, 656
 PRODUCER = (1280, 720)
+PARTS = 25
 PEAK_FP16_TFLOPS = 2500.0     # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_HBM_GBS = 8000.0         # MI355X HBM3E (MI355X_MICROARCH.md)
+# resizeAndMerge x8 write + NMS read of the 25 part planes per frame at config 2 (SURVEY.md §8d:
+# 1,176,864 + 75,319,296 + 24,140,800 + 38,400 bytes): what the reference's post-processing moves
+POST_BYTES_FRAME = 100_675_360
 
 
 def parse():
@@ -40,17 +54,32 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64,
                     help="frames per step per GPU (throughput mode; DESIGN.md §5 lists 16 too)")
+    ap.add_argument("--config", choices=["body25", "multiscale"], default="body25",
+                    help="body25: BASELINE configs[1]/[2]; multiscale: configs[3] (4 scales)")
     ap.add_argument("--people", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample")
+    ap.add_argument("--dev", action="append", default=[], metavar="KEY=VAL",
+                    help="kernel-variant switch for A/B runs (opk_dev_set; include/opk.h)")
     return ap.parse_args()
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
 
 
 def cpu_baseline(args, params, frames_np, overlays_np):
     """fp32 CPU restatement (oracle/) of the same pipeline on the same uint8 frames: warpAffine +
     normalisation, CNN (im2col + SGEMM, OpenMP), OpenCV-semantics cubic resize, nmsCpu,
-    connectBodyPartsCpu."""
+    connectBodyPartsCpu.  Config 2 for ~cpu_seconds, then config 1 (one 368x368 frame)."""
     import oracle
     from oracle import body25
     graph = body25.layers()
@@ -71,38 +100,54 @@ def cpu_baseline(args, params, frames_np, overlays_np):
         el = time.perf_counter() - t0
         if el >= args.cpu_seconds:
             break
+    # config 1: one 368x368 frame (net input 368x368, output 46x46), the same stages
+    t1 = time.perf_counter()
+    x1 = np.random.default_rng(0).uniform(-0.5, 0.5, (1, 3, 368, 368)).astype(np.float32)
+    o1 = body25.forward(x1, params, graph=graph, nthreads=args.cpu_threads)[0]
+    h1 = oracle.resize_merge([o1], 368, 368)
+    p1 = oracle.nms(h1, 0.05, 128, (0.25, 0.25))
+    oracle.connect(h1, p1, scale=1.0)
+    el1 = time.perf_counter() - t1
     return {"value": done / el, "unit": "frames/s", "cores": args.cpu_threads, "kind": "port",
-            "sample": "%d frame(s) of the full pipeline on 1280x720 frames (warpAffine + CNN fp32 "
-                      "at 656x368 + resize + NMS + connector), oracle/ CPU restatement, %.1f s, "
-                      "%d people found"
-                      % (done, el, people)}
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": "%d frame(s) of the full config-2 pipeline on 1280x720 frames (warpAffine + "
+                      "CNN fp32 at 656x368 + resize + NMS + connector), oracle/ CPU restatement, "
+                      "%.1f s on %d threads, %d people found"
+                      % (done, el, args.cpu_threads, people),
+            "config1": {"value": 1.0 / el1, "unit": "frames/s",
+                        "sample": "1 frame, BODY_25 368x368 net input (161.1 GFLOP) + resize + "
+                                  "NMS + connector, %.1f s" % el1},
+            "published_reference_cpu": "~0.1 FPS BODY_25 CPU-only (doc/06_maximizing_openpose_"
+                                       "speed.md:21), other hardware"}
 
 
 def pmc_traffic(batch):
     """HBM bytes of one CNN forward from the committed rocprofv3 PMC summary (FETCH_SIZE x2 on
     gfx950 + WRITE_SIZE over every kernel of one forward; tools/pmc_summary.py), or None when the
     summary was taken at another batch size."""
-    path = os.path.join(ROOT, "profiles", "round1", "pmc_traffic.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    return d.get("cnn_forward_hbm_bytes") if d.get("batch") == batch else None
+    for rnd in ("round2", "round1"):
+        path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        return d.get("cnn_forward_hbm_bytes") if d.get("batch") == batch else None
+    return None
 
 
-def main():
-    args = parse()
-    rank = int(os.environ.get("RANK", "0"))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+def rank_main(args, rank, world, local):
     torch.cuda.set_device(local)
+    dist = None
     if world > 1:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from openpose_amd import synth
-    from openpose_amd.api import Context, Net, PoseExtractor
+    from openpose_amd.api import Context, Net, PoseExtractor, dev_switches, scale_and_size
+
+    if args.dev:   # A/B runs only; the product configuration has none
+        dev_switches(**{k: int(v) for k, v in (d.split("=", 1) for d in args.dev)}).__enter__()
 
     ctx = Context(local)
     net = Net(ctx, "builtin:BODY_25")
@@ -112,66 +157,103 @@ def main():
     pose = PoseExtractor(ctx, net)
 
     B = args.batch
+    nscales = 4 if args.config == "multiscale" else 1
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     W_IN, H_IN = PRODUCER
     frames = [torch.randint(0, 256, (B, H_IN, W_IN, 3), generator=gen, device="cuda",
                             dtype=torch.uint8) for _ in range(2)]
-    pose.set_input((-1, NET_H))   # --net_resolution -1x368 -> 656x368 for 1280x720
+    pose.set_input((-1, NET_H), scale_number=nscales, scale_gap=0.25)
+    _, net_sizes = scale_and_size(PRODUCER, (-1, NET_H), 1.0, nscales, 0.25)
+    assert net_sizes[0] == (NET_W, NET_H)
+    flops_frame = sum(net.flops_per_frame(h, w) for (w, h) in net_sizes)
+
+    # net-output statistics before any overlay (the overlay is added in place into it)
+    pose.forward_frames(frames[0])
+    out_std = float(net.output_numpy()[:2].std()) if nscales == 1 else None
     ov_np = np.stack([synth.overlay(args.people, NET_H // 8, NET_W // 8, seed=1000 * rank + f)
                       for f in range(B)])
     overlay = torch.from_numpy(ov_np).cuda()
     pose.set_overlay(overlay)
-    flops_frame = net.flops_per_frame(NET_H, NET_W)
-    out_shape = (B, 78, NET_H // 8, NET_W // 8)
+
+    # per-step ordered gather of the per-frame records (capacity: 4x the synthetic people + 8)
+    cap = B * (1 + (4 * args.people + 8) * (PARTS * 3 + 1))
+    gather = parallel.RecordGather(world, rank, cap, args.steps, "cuda")
 
     # Two-stage pipeline (opk_pose_submit / opk_pose_collect): the device work of batch i+1 is
     # enqueued before the host assembly of batch i, which then overlaps it.
-    def step(i):
+    rec_buf = np.empty(cap, np.float32)
+    collected = [0]
+
+    def collect(timed):
+        pose.collect()
+        if timed:
+            i = collected[0]
+            gather.push(i, (i * world + rank) * B, B, pose.records(rec_buf))
+            collected[0] += 1
+
+    def step(i, timed):
         pose.submit_frames(frames[i % 2])
         if pose.pending() > 1:
-            pose.collect()
+            collect(timed)
 
-    def drain():
+    def drain(timed):
         while pose.pending() > 0:
-            pose.collect()
+            collect(timed)
 
     for i in range(args.warmup):
-        step(i)
-    drain()
+        step(i, False)
+    drain(False)
     torch.cuda.synchronize()
-    people = [pose.num_people(f) for f in range(B)]
-    pose.forward_frames(frames[0])
-    out_std = float(net.output_numpy()[:2].std())
-    net_in = pose.net_input_numpy()
-    assert net_in.shape == (B, 3, NET_H, NET_W)
+    people = [pose.num_people(f) for f in range(min(B, 4))]
 
-    # CNN forward time: HIP events recorded by the library around every forward, on the
-    # context stream the conv kernels run on (opk_net_set_timing)
+    # CNN forward and post-processing device times: HIP events recorded by the library around
+    # every forward / every batch's post-processing, on the context stream the kernels run on
     net.set_timing(True)
-    if world > 1:
-        import torch.distributed as dist
+    pose.set_timing(True)
+    if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
-    drain()
+        step(i, True)
+    drain(True)
+    ordered = gather.finish(PARTS)        # rank 0: every frame's record, in frame order
     torch.cuda.synchronize()
-    if world > 1:
+    if dist is not None:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     nfw, fw_ms = net.read_timing()
+    npost, post_ms = pose.read_timing()
     net.set_timing(False)
-    assert nfw == args.steps, nfw
-    net_ms = fw_ms / nfw
-    if world > 1:
-        t = torch.tensor([elapsed, net_ms], device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, net_ms = float(t[0]), float(t[1])
+    pose.set_timing(False)
+    assert nfw == args.steps * nscales, nfw
+    assert npost == args.steps, npost
+    net_ms = fw_ms / args.steps            # all scales of one step
+    post_ms /= npost
+    per_rank = [[rank, elapsed, net_ms, post_ms]]
+    if dist is not None:
+        t = torch.tensor([rank, elapsed, net_ms, post_ms], device="cuda", dtype=torch.float64)
+        allr = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allr, t)
+        per_rank = [x.tolist() for x in allr]
+        elapsed = max(r[1] for r in per_rank)
+        net_ms = max(r[2] for r in per_rank)
+        post_ms = max(r[3] for r in per_rank)
 
     total_frames = world * B * args.steps
+    if rank == 0:
+        assert len(ordered) == total_frames, (len(ordered), total_frames)
     fps = total_frames / elapsed
     achieved = flops_frame * B / (net_ms * 1e-3) / 1e12
+    post_gbs = POST_BYTES_FRAME * B / (post_ms * 1e-3) / 1e9
+    workload = ("BODY_25 net_resolution -1x368 (net input 656x368) on synthetic 1280x720 uint8 "
+                "frames, %d-person overlay per frame; warpAffine+CNN+resize+NMS+PAF+assembly+"
+                "ordered gather" % args.people)
+    if nscales > 1:
+        workload = ("BODY_25 multi-scale --scale_number 4 --scale_gap 0.25 (nets %s) on synthetic "
+                    "1280x720 uint8 frames, %d-person overlay; warpAffine x4 + CNN x4 + merged "
+                    "resize + NMS + PAF + assembly + ordered gather"
+                    % ("/".join("%dx%d" % s for s in net_sizes), args.people))
     result = {
         "metric": METRIC,
         "value": round(fps, 2),
@@ -184,40 +266,71 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "fp16",
+        "dev_switches": args.dev or None,
         "data": "synthetic uint8 BGR 1280x720 frames (uniform random), random-init weights",
         "config": {
-            "workload": "BODY_25 net_resolution -1x368 (net input 656x368) on synthetic 1280x720 "
-                        "uint8 frames, %d-person overlay per frame; warpAffine+CNN+resize+NMS+PAF+"
-                        "assembly" % args.people,
+            "workload": workload,
             "frames_per_step_per_gpu": B,
             "net_input": [NET_H, NET_W],
+            "net_inputs_all_scales": [[h, w] for (w, h) in net_sizes],
             "heatmaps": [78, NET_H, NET_W],
-            "parallelism": "frame-parallel replicas x%d" % world,
+            "parallelism": "frame-parallel replicas x%d (one process per GPU, RCCL ordered "
+                           "gather of per-frame records to rank 0)" % world,
             "compute": "warp u8 fixed-point; conv fp16 x fp16 -> fp32 MFMA; resize/NMS/PAF fp32",
-            "people_per_frame_found": people[:4],
-            "net_output_std_before_overlay": round(out_std, 5),
+            "people_per_frame_found": people,
+            "net_output_std_before_overlay": None if out_std is None else round(out_std, 5),
+            "frames_gathered_in_order": total_frames,
         },
+        "per_rank": [{"rank": int(r[0]), "s": round(r[1], 4), "cnn_ms_per_step": round(r[2], 3),
+                      "post_ms_per_step": round(r[3], 3)} for r in per_rank],
         "roofline": {
             "bound": "mfma",
             "kernel": "BODY_25 CNN forward (113 halo implicit-GEMM conv launches + fused first "
-                      "conv + 3 pools) per step of %d frames" % B,
+                      "conv + 3 pools) per step of %d frames%s"
+                      % (B, "" if nscales == 1 else " x 4 scales"),
             "achieved": round(achieved, 2),
             "peak": PEAK_FP16_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
-            "traffic": pmc_traffic(B),
+            "traffic": pmc_traffic(B) if nscales == 1 else None,
             "traffic_unit": "bytes per launch (HBM, PMC)",
             "algorithmic_gflop_per_launch": round(flops_frame * B / 1e9, 2),
             "avg_launch_ms": round(net_ms, 3),
         },
+        "post_roofline": {
+            "bound": "hbm",
+            "kernel": "post-processing per step (overlay add + lazy resize/NMS detect + NMS "
+                      "finalize + PAF integrals), HIP events on the context stream",
+            "achieved": round(post_gbs, 1),
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": round(post_gbs / PEAK_HBM_GBS, 4),
+            "algorithmic_bytes_per_frame": POST_BYTES_FRAME,
+            "note": "effective rate: the reference's resize-write + NMS-read bytes per frame over "
+                    "the measured time; the lazy heat maps never move those bytes (DESIGN.md §4.2)",
+            "avg_launch_ms": round(post_ms, 3),
+        },
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and nscales == 1 and not args.no_cpu_baseline:
         frames_np = frames[0][:2].cpu().numpy()   # uint8 [2][720][1280][3]
         result["cpu_baseline"] = cpu_baseline(args, params, frames_np, ov_np[:2])
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if dist is not None:
         dist.destroy_process_group()
+
+
+def main():
+    args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # direct start with --gpus N: one child process per GPU, this process touches no GPU
+        sys.exit(parallel.launch_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    rank_main(args, rank, world, local)
 
 
 if __name__ == "__main__":

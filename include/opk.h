@@ -182,6 +182,13 @@ int opk_scale_and_size(int in_w, int in_h, int net_w, int net_h, float dynamic_b
 int opk_cvmat_to_input(opk_ctx* ctx, float* input_dev, const uint8_t* frames_dev, int n, int width,
                        int height, size_t step, double scale, int net_w, int net_h, int normalize);
 
+/* Kernel-variant switches (no reference counterpart; A/B tests and tuning only): key = one of
+ * "CONV3_SMALL", "CONV3_W16", "CONV3_PERSIST", "CONV3_WIDE", "CONV3P_ASMR", "CONV3P_WIDE",
+ * "CONV3P_PRIO", "CONV1_TILE", "CONV1_N64W16", "CONV1_FUSED" (read when a launch is planned);
+ * reset != 0 removes the key (back to the product default).  Process-wide; the environment is
+ * never consulted. */
+int opk_dev_set(const char* key, int value, int reset);
+
 /* ---- Net: replaces op::Net / op::NetCaffe (include/openpose/net/net.hpp:8-18,
  *      netCaffe.hpp:12-13).  prototxt: a Caffe prototxt path, or one of the reference's networks
  *      generated in the library: "builtin:BODY_25", "builtin:COCO_18", "builtin:MPI_15",
@@ -216,7 +223,11 @@ int opk_net_flops_per_frame(opk_net* net, int h, int w, double* flops);
  * forwards since the last read and their summed device time in milliseconds. */
 int opk_net_set_timing(opk_net* net, int enable);
 int opk_net_read_timing(opk_net* net, int* forwards, double* total_ms);
-/* device pointer + NCHW shape of the last forward's net_output blob */
+/* device pointer + NCHW shape of the last forward's net_output blob.  Valid right after
+ * opk_net_create, as NetCaffe::getOutputBlobArray is (poseExtractorCaffe.cpp:94-95 takes it once,
+ * before any forward, and keeps it): before the first forward *output_dev is NULL and shape is
+ * {0, out_channels, 0, 0}.  The buffer of one input shape is stable across forwards of that
+ * shape (the values are the latest forward's). */
 int opk_net_output(opk_net* net, float** output_dev, int shape[4]);
 
 /* ---- Pose extractor: replaces op::PoseExtractorCaffe::forwardPass
@@ -289,6 +300,18 @@ int opk_pose_num_people(opk_pose* pose, int frame);
 /* keypoints_host [max_people][parts][3], scores_host [max_people] of one collected frame */
 int opk_pose_keypoints(opk_pose* pose, int frame, float* keypoints_host, float* scores_host,
                        int max_people);
+/* Post-processing timing (measurement hook, no reference counterpart): while enabled the device
+ * work of every submitted batch after its net forward (overlay add, NMS, PAF integrals) is
+ * bracketed by HIP events on the context stream; read waits for them and returns the number of
+ * batches since the last read and their summed device time in milliseconds. */
+int opk_pose_set_timing(opk_pose* pose, int enable);
+int opk_pose_read_timing(opk_pose* pose, int* batches, double* total_ms);
+/* Every frame of the last collected batch as one packed host record (the result the reference's
+ * WQueueOrderer re-sequences, wQueueOrderer.hpp:62-141): for each frame f in order,
+ *   [people_f, keypoints_f (people_f x parts x 3), scores_f (people_f)]  (all float).
+ * *used receives the floats needed; with capacity < *used nothing is written and the call fails
+ * with OPK_ERR_ARG (records may be NULL to query the size). */
+int opk_pose_records(opk_pose* pose, float* records_host, size_t capacity, size_t* used);
 /* device pointers of the last forward's heatmaps [n][heat_channels][H][W] and peaks
  * [n][parts][128][3].
  * The pipeline evaluates heat-map values lazily from the net output (NMS and PAF scoring compute

@@ -37,6 +37,7 @@
 #include <openpose/pose/poseParameters.hpp>
 
 #include "opk.h"
+#include "poseExtractorHip.hpp"
 
 namespace op
 {
@@ -244,32 +245,372 @@ namespace op
             check(opk_memcpy_h2d(mCtx, mInput, inputNetData.getConstPtr(), bytes), __LINE__, __FUNCTION__);
             check(opk_net_forward(mNet, (const float*)mInput, size[0], size[2], size[3]), __LINE__,
                   __FUNCTION__);
+            if (spOutput)
+                refreshOutput();   // the blob handed out at init now holds this forward's output
         }
 
+        // NetCaffe returns a live wrapper of its output blob (netCaffe.cpp:263-268), and
+        // addCaffeNetOnThread takes it ONCE, right after initializationOnThread and before any
+        // forward (poseExtractorCaffe.cpp:94-95), then reads it after every forward.  Here: one
+        // ArrayCpuGpu per net, valid from the first call ({1, C, 1, 1} before a forward) and
+        // refreshed by every forwardPass (Reshape to the new output + host copy).  ArrayCpuGpu
+        // exists only in USE_CAFFE builds (arrayCpuGpu.cpp:23-40); without CUDA their Caffe layers
+        // run the *Cpu functions on cpu_data(), which is what this keeps current.  A Caffe-free
+        // pipeline uses op::PoseExtractorHip instead (below), which never builds this blob.
         std::shared_ptr<ArrayCpuGpu<float>> getOutputBlobArray() const
+        {
+            if (!spOutput)
+            {
+                float* out = nullptr;
+                int shape[4];
+                check(opk_net_output(mNet, &out, shape), __LINE__, __FUNCTION__);
+                spOutput = std::make_shared<ArrayCpuGpu<float>>(1, shape[1], 1, 1);
+                if (out != nullptr)
+                    refreshOutput();
+            }
+            return spOutput;
+        }
+
+    private:
+        void refreshOutput() const
         {
             float* out = nullptr;
             int shape[4];
             check(opk_net_output(mNet, &out, shape), __LINE__, __FUNCTION__);
-            Array<float> host({shape[0], shape[1], shape[2], shape[3]});
-            check(opk_memcpy_d2h(mCtx, host.getPtr(), out, host.getVolume() * sizeof(float)), __LINE__,
-                  __FUNCTION__);
-            // same wrapping as the poseNetOutput injection path (poseExtractorCaffe.cpp:258-261)
-            return std::make_shared<ArrayCpuGpu<float>>(host, false);
+            spOutput->Reshape(shape[0], shape[1], shape[2], shape[3]);
+            check(opk_memcpy_d2h(mCtx, spOutput->mutable_cpu_data(), out,
+                                 (size_t)spOutput->count() * sizeof(float)), __LINE__, __FUNCTION__);
         }
 
-    private:
         const std::string mProto, mModel;
         const int mGpuId;
         opk_ctx* mCtx = nullptr;
         opk_net* mNet = nullptr;
         mutable void* mInput = nullptr;
         mutable size_t mInputBytes = 0;
+        mutable std::shared_ptr<ArrayCpuGpu<float>> spOutput;
     };
 
     std::shared_ptr<Net> makeNetHip(const std::string& proto, const std::string& model, const int gpuId)
     {
         return std::make_shared<NetHip>(proto, model, gpuId);
+    }
+
+    // ---- op::PoseExtractorHip: PoseExtractorNet on libopk_hip (no Caffe, no CUDA) ---------------
+    struct PoseExtractorHip::ImplPoseExtractorHip
+    {
+        PoseModel poseModel;
+        int gpuId;
+        std::string proto, model;
+        bool enableNet, maximizePositives;
+        int parts = 0, heatChannels = 0;
+        opk_ctx* ctx = nullptr;
+        opk_net* net = nullptr;
+        opk_pose* pose = nullptr;
+        std::vector<void*> inputs;          // device net inputs, one per scale
+        std::vector<size_t> inputBytes;
+        void* injected = nullptr;           // device copy of poseNetOutput
+        size_t injectedBytes = 0;
+        int heatH = 0, heatW = 0;
+        // host copies, made on request and valid until the next forwardPass
+        mutable std::vector<float> heatHost, peaksHost;
+        mutable bool heatFresh = false, peaksFresh = false;
+
+        ~ImplPoseExtractorHip()
+        {
+            if (pose)
+                opk_pose_destroy(pose);
+            if (net)
+                opk_net_destroy(net);
+            if (ctx)
+            {
+                for (auto* p : inputs)
+                    if (p)
+                        opk_free(ctx, p);
+                if (injected)
+                    opk_free(ctx, injected);
+            }
+        }
+
+        void* deviceBuffer(void*& buffer, size_t& capacity, const size_t bytes)
+        {
+            if (bytes > capacity)
+            {
+                if (buffer)
+                    opk_free(ctx, buffer);
+                buffer = nullptr;
+                check(opk_malloc(ctx, &buffer, bytes), __LINE__, __FUNCTION__);
+                capacity = bytes;
+            }
+            return buffer;
+        }
+    };
+
+    PoseExtractorHip::PoseExtractorHip(
+        const PoseModel poseModel, const std::string& modelFolder, const int gpuId,
+        const std::vector<HeatMapType>& heatMapTypes, const ScaleMode heatMapScaleMode,
+        const bool addPartCandidates, const bool maximizePositives, const std::string& protoTxtPath,
+        const std::string& caffeModelPath, const float upsamplingRatio, const bool enableNet,
+        const bool enableGoogleLogging) :
+        PoseExtractorNet{poseModel, heatMapTypes, heatMapScaleMode, addPartCandidates, maximizePositives},
+        upImpl{new ImplPoseExtractorHip{}}
+    {
+        try
+        {
+            (void)enableGoogleLogging;
+            // heat maps at the net input resolution (mUpsamplingRatio <= 0, poseExtractorCaffe.cpp:274-276)
+            if (upsamplingRatio > 0.f && upsamplingRatio != getPoseNetDecreaseFactor(poseModel))
+                error("libopk_hip produces heat maps at the net input resolution only (--upsampling_ratio 0).",
+                      __LINE__, __FUNCTION__, __FILE__);
+            upImpl->poseModel = poseModel;
+            upImpl->gpuId = gpuId;
+            upImpl->enableNet = enableNet;
+            upImpl->maximizePositives = maximizePositives;
+            // the same paths addCaffeNetOnThread builds (poseExtractorCaffe.cpp:82-86)
+            upImpl->proto = modelFolder + (protoTxtPath.empty() ? getPoseProtoTxt(poseModel) : protoTxtPath);
+            upImpl->model = modelFolder + (caffeModelPath.empty() ? getPoseTrainedModel(poseModel) : caffeModelPath);
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+        }
+    }
+
+    PoseExtractorHip::~PoseExtractorHip()
+    {
+    }
+
+    void PoseExtractorHip::netInitializationOnThread()
+    {
+        try
+        {
+            auto& impl = *upImpl;
+            impl.ctx = threadContext(impl.gpuId);   // binds this thread to the GPU (netCaffe.cpp:169-170)
+            if (impl.enableNet)
+                check(opk_net_create(impl.ctx, impl.proto.c_str(), impl.model.c_str(), &impl.net), __LINE__,
+                      __FUNCTION__);
+            // the connector the reference would run: the CPU path's assembly where its CPU
+            // connector exists, connectBodyPartsGpu's for the other models (BODY_135, ...)
+            const auto numberBodyParts = (int)getPoseNumberBodyParts(impl.poseModel);
+            const bool cpuModel = numberBodyParts == 25 || numberBodyParts == 18 || numberBodyParts == 15;
+            check(opk_pose_create_model(impl.ctx, impl.net, (int)impl.poseModel, impl.maximizePositives ? 1 : 0,
+                                        cpuModel ? OPK_CONNECT_CPU : OPK_CONNECT_GPU, &impl.pose),
+                  __LINE__, __FUNCTION__);
+            check(opk_pose_model_info((int)impl.poseModel, &impl.parts, nullptr, nullptr, &impl.heatChannels,
+                                      nullptr, nullptr), __LINE__, __FUNCTION__);
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+        }
+    }
+
+    void PoseExtractorHip::forwardPass(
+        const std::vector<Array<float>>& inputNetData, const Point<int>& inputDataSize,
+        const std::vector<double>& scaleInputToNetInputs, const Array<float>& poseNetOutput)
+    {
+        try
+        {
+            auto& impl = *upImpl;
+            if (!impl.pose)
+                error("netInitializationOnThread() was not called.", __LINE__, __FUNCTION__, __FILE__);
+            // sanity checks of poseExtractorCaffe.cpp:213-231
+            if (inputNetData.empty())
+                error("Empty inputNetData.", __LINE__, __FUNCTION__, __FILE__);
+            for (const auto& inputNetDataI : inputNetData)
+                if (inputNetDataI.empty())
+                    error("Empty inputNetData.", __LINE__, __FUNCTION__, __FILE__);
+            if (inputNetData.size() != scaleInputToNetInputs.size())
+                error("Size(inputNetData) must be same than size(scaleInputToNetInputs).",
+                      __LINE__, __FUNCTION__, __FILE__);
+            if (poseNetOutput.empty() != impl.enableNet)
+                error("Either use OpenPose default network (`--body 1`) or fill the `poseNetOutput` argument"
+                      " (only 1 of those 2, not both).", __LINE__, __FUNCTION__, __FILE__);
+            // PoseProperty values (set/increase may change them between frames)
+            const PoseProperty props[] = {
+                PoseProperty::NMSThreshold, PoseProperty::ConnectInterMinAboveThreshold,
+                PoseProperty::ConnectInterThreshold, PoseProperty::ConnectMinSubsetCnt,
+                PoseProperty::ConnectMinSubsetScore};
+            const int opkProps[] = {
+                OPK_PROP_NMS_THRESHOLD, OPK_PROP_INTER_MIN_ABOVE_THRESHOLD, OPK_PROP_INTER_THRESHOLD,
+                OPK_PROP_MIN_SUBSET_CNT, OPK_PROP_MIN_SUBSET_SCORE};
+            for (auto i = 0; i < 5; i++)
+                check(opk_pose_set_property(impl.pose, opkProps[i], get(props[i])), __LINE__, __FUNCTION__);
+
+            const auto numberScales = inputNetData.size();
+            const int netH = inputNetData[0].getSize(2), netW = inputNetData[0].getSize(3);
+            if (impl.enableNet)
+            {
+                impl.inputs.resize(numberScales, nullptr);
+                impl.inputBytes.resize(numberScales, 0);
+                std::vector<const float*> ptrs(numberScales);
+                std::vector<int> hw(2 * numberScales);
+                for (auto i = 0u; i < numberScales; i++)
+                {
+                    const auto& in = inputNetData[i];   // {1, 3, H, W} (netCaffe.cpp:220-237)
+                    if (in.getNumberDimensions() != 4 || in.getSize(1) != 3)
+                        error("Input must be NCHW with 3 channels.", __LINE__, __FUNCTION__, __FILE__);
+                    const size_t bytes = in.getVolume() * sizeof(float);
+                    void* dev = impl.deviceBuffer(impl.inputs[i], impl.inputBytes[i], bytes);
+                    check(opk_memcpy_h2d(impl.ctx, dev, in.getConstPtr(), bytes), __LINE__, __FUNCTION__);
+                    ptrs[i] = static_cast<const float*>(dev);
+                    hw[2 * i] = in.getSize(2);
+                    hw[2 * i + 1] = in.getSize(3);
+                }
+                if (numberScales == 1)
+                    check(opk_pose_forward(impl.pose, ptrs[0], inputNetData[0].getSize(0), netH, netW,
+                                           inputDataSize.x, inputDataSize.y), __LINE__, __FUNCTION__);
+                else
+                    check(opk_pose_forward_multi(impl.pose, ptrs.data(), hw.data(), (int)numberScales,
+                                                 inputNetData[0].getSize(0), inputDataSize.x, inputDataSize.y),
+                          __LINE__, __FUNCTION__);
+            }
+            else
+            {
+                // injected net output (poseExtractorCaffe.cpp:249-262): one scale, [1][C][h][w]
+                if (numberScales != 1u)
+                    error("Size(inputNetData) must match the provided heatmaps batch size (1).",
+                          __LINE__, __FUNCTION__, __FILE__);
+                if (poseNetOutput.getNumberDimensions() != 4 || poseNetOutput.getSize(1) != impl.heatChannels)
+                    error("poseNetOutput must be [1][heat channels][h][w].", __LINE__, __FUNCTION__, __FILE__);
+                const size_t bytes = poseNetOutput.getVolume() * sizeof(float);
+                void* dev = impl.deviceBuffer(impl.injected, impl.injectedBytes, bytes);
+                check(opk_memcpy_h2d(impl.ctx, dev, poseNetOutput.getConstPtr(), bytes), __LINE__, __FUNCTION__);
+                check(opk_pose_forward_net_output(impl.pose, static_cast<const float*>(dev), poseNetOutput.getSize(0),
+                                                  poseNetOutput.getSize(2), poseNetOutput.getSize(3), netH, netW,
+                                                  inputDataSize.x, inputDataSize.y),
+                      __LINE__, __FUNCTION__);
+            }
+            // results of frame 0 (peopleVectorToPeopleArray, bodyPartConnectorBase.cpp:895-907)
+            const int people = opk_pose_num_people(impl.pose, 0);
+            if (people > 0)
+            {
+                mPoseKeypoints.reset({people, impl.parts, 3}, 0.f);
+                mPoseScores.reset(people);
+                check(opk_pose_keypoints(impl.pose, 0, mPoseKeypoints.getPtr(), mPoseScores.getPtr(), people),
+                      __LINE__, __FUNCTION__);
+            }
+            else
+            {
+                mPoseKeypoints.reset();
+                mPoseScores.reset();
+            }
+            mScaleNetToOutput = opk_pose_scale_net_to_output(impl.pose);
+            mNetOutputSize = Point<int>{netW, netH};   // ratio 1 (poseExtractorCaffe.cpp:271-279)
+            impl.heatH = netH;
+            impl.heatW = netW;
+            impl.heatFresh = false;
+            impl.peaksFresh = false;
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+        }
+    }
+
+    const float* PoseExtractorHip::getCandidatesCpuConstPtr() const
+    {
+        try
+        {
+            checkThread();
+            auto& impl = *upImpl;
+            if (!impl.peaksFresh)
+            {
+                float* dev = nullptr;
+                int shape[4];
+                check(opk_pose_peaks(impl.pose, &dev, shape), __LINE__, __FUNCTION__);
+                impl.peaksHost.resize((size_t)shape[1] * shape[2] * shape[3]);   // frame 0
+                check(opk_memcpy_d2h(impl.ctx, impl.peaksHost.data(), dev, impl.peaksHost.size() * sizeof(float)),
+                      __LINE__, __FUNCTION__);
+                impl.peaksFresh = true;
+            }
+            return impl.peaksHost.data();
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+            return nullptr;
+        }
+    }
+
+    const float* PoseExtractorHip::getCandidatesGpuConstPtr() const
+    {
+        try
+        {
+            checkThread();
+            float* dev = nullptr;
+            int shape[4];
+            check(opk_pose_peaks(upImpl->pose, &dev, shape), __LINE__, __FUNCTION__);
+            return dev;
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+            return nullptr;
+        }
+    }
+
+    const float* PoseExtractorHip::getHeatMapCpuConstPtr() const
+    {
+        try
+        {
+            checkThread();
+            auto& impl = *upImpl;
+            if (!impl.heatFresh)
+            {
+                float* dev = nullptr;
+                int shape[4];
+                check(opk_pose_heatmaps(impl.pose, &dev, shape), __LINE__, __FUNCTION__);
+                impl.heatHost.resize((size_t)shape[1] * shape[2] * shape[3]);   // frame 0
+                check(opk_memcpy_d2h(impl.ctx, impl.heatHost.data(), dev, impl.heatHost.size() * sizeof(float)),
+                      __LINE__, __FUNCTION__);
+                impl.heatFresh = true;
+            }
+            return impl.heatHost.data();
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+            return nullptr;
+        }
+    }
+
+    const float* PoseExtractorHip::getHeatMapGpuConstPtr() const
+    {
+        try
+        {
+            checkThread();
+            float* dev = nullptr;
+            int shape[4];
+            check(opk_pose_heatmaps(upImpl->pose, &dev, shape), __LINE__, __FUNCTION__);
+            return dev;
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+            return nullptr;
+        }
+    }
+
+    std::vector<int> PoseExtractorHip::getHeatMapSize() const
+    {
+        try
+        {
+            checkThread();
+            return {1, upImpl->heatChannels, upImpl->heatH, upImpl->heatW};   // spHeatMapsBlob->shape()
+        }
+        catch (const std::exception& e)
+        {
+            error(e.what(), __LINE__, __FUNCTION__, __FILE__);
+            return {};
+        }
+    }
+
+    const float* PoseExtractorHip::getPoseGpuConstPtr() const
+    {
+        // as PoseExtractorCaffe::getPoseGpuConstPtr (poseExtractorCaffe.cpp:724-741)
+        error("GPU pointer for people pose data not implemented yet.", __LINE__, __FUNCTION__, __FILE__);
+        return nullptr;
     }
 
     // ---- op::CvMatToOpInput on libopk_hip --------------------------------------------------------

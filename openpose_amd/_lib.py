@@ -23,6 +23,7 @@ _fp = _c.POINTER(_c.c_float)
 _SIGS = {
     "opk_last_error": (_c.c_char_p, []),
     "opk_version": (_i, []),
+    "opk_dev_set": (_i, [_c.c_char_p, _i, _i]),
     "opk_ctx_create": (_i, [_i, _p, _c.POINTER(_p)]),
     "opk_ctx_create_private_stream": (_i, [_i, _c.POINTER(_p)]),
     "opk_ctx_destroy": (_i, [_p]),
@@ -67,6 +68,9 @@ _SIGS = {
     "opk_pose_pending": (_i, [_p]),
     "opk_pose_num_people": (_i, [_p, _i]),
     "opk_pose_keypoints": (_i, [_p, _i, _p, _p, _i]),
+    "opk_pose_set_timing": (_i, [_p, _i]),
+    "opk_pose_read_timing": (_i, [_p, _ip, _c.POINTER(_d)]),
+    "opk_pose_records": (_i, [_p, _p, _c.c_size_t, _c.POINTER(_c.c_size_t)]),
     "opk_pose_heatmaps": (_i, [_p, _c.POINTER(_p), _ip]),
     "opk_pose_peaks": (_i, [_p, _c.POINTER(_p), _ip]),
     "opk_pose_scale_net_to_output": (_f, [_p]),

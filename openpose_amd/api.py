@@ -41,6 +41,26 @@ def _close_live():
                 pass
 
 
+class dev_switches:
+    """Context manager setting kernel-variant switches (opk_dev_set; A/B tests and tuning only),
+    e.g. `with dev_switches(CONV3_W16=0): ...`; the product defaults are restored on exit."""
+
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        L = _lib.load()
+        for k, v in self.kv.items():
+            check(L.opk_dev_set(k.encode(), int(v), 0))
+        return self
+
+    def __exit__(self, *exc):
+        L = _lib.load()
+        for k in self.kv:
+            L.opk_dev_set(k.encode(), 0, 1)
+        return False
+
+
 class Context:
     """One opk_ctx bound to a device; runs on torch's current stream of that device."""
 
@@ -445,6 +465,29 @@ class PoseExtractor:
         check(self.L.opk_pose_keypoints(self.h, frame, kp.ctypes.data_as(ctypes.c_void_p),
                                         ks.ctypes.data_as(ctypes.c_void_p), n))
         return kp[:n], ks[:n]
+
+    def set_timing(self, on=True):
+        check(self.L.opk_pose_set_timing(self.h, int(on)))
+
+    def read_timing(self):
+        """(batches, summed post-processing device ms) since the last read."""
+        n, ms = ctypes.c_int(0), ctypes.c_double(0)
+        check(self.L.opk_pose_read_timing(self.h, ctypes.byref(n), ctypes.byref(ms)))
+        return n.value, ms.value
+
+    def records(self, out=None):
+        """Packed results of every frame of the last collected batch (opk_pose_records):
+        per frame [people, keypoints (people x parts x 3), scores (people)], float32.  With `out`
+        (a float32 numpy buffer) the records are written there; returns the filled view."""
+        used = ctypes.c_size_t(0)
+        check(self.L.opk_pose_records(self.h, None, 0, ctypes.byref(used)))
+        if out is None:
+            out = np.empty(used.value, np.float32)
+        if out.size < used.value:
+            raise ValueError("records buffer holds %d floats, %d needed" % (out.size, used.value))
+        check(self.L.opk_pose_records(self.h, out.ctypes.data_as(ctypes.c_void_p), out.size,
+                                      ctypes.byref(used)))
+        return out[:used.value]
 
     def scale_net_to_output(self):
         return self.L.opk_pose_scale_net_to_output(self.h)

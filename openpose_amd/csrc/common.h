@@ -33,6 +33,11 @@ struct Error : std::runtime_error {
 // after a kernel launch (reference: cudaCheck -> cudaPeekAtLastError, gpu/cuda.cpp:18-26)
 #define OPK_LAUNCH_CHECK() OPK_HIP(hipPeekAtLastError())
 
+// Kernel-variant switches (A/B tests and tuning only): a process-wide table written solely through
+// opk_dev_set (include/opk.h) -- never read from the environment, so nothing a user's shell
+// exports can change which kernels run.  Unset keys give dflt (the product configuration).
+int dev_switch(const char* key, int dflt);
+
 // Device scratch that only grows (one per context and purpose); never freed inside a launch
 // sequence so the launch functions stay graph-capturable.
 struct DevBuf {

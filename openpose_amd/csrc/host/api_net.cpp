@@ -118,8 +118,7 @@ int opk_net_output(opk_net* net, float** out, int shape[4])
 {
     return guarded_net([&] {
         OPK_CHECK_ARG(net && out && shape, "NULL argument");
-        OPK_CHECK_ARG(net->net->frames() > 0, "no forward pass yet");
-        *out = net->net->output();
+        *out = net->net->output();   // NULL (and a {0, C, 0, 0} shape) before the first forward
         shape[0] = net->net->frames();
         shape[1] = net->net->out_channels();
         shape[2] = net->net->out_h();
@@ -252,6 +251,46 @@ int opk_pose_keypoints(opk_pose* p, int frame, float* kp, float* ks, int max_peo
         const int parts = opk::pose_model(p->pose->model()).parts;
         if (kp && n > 0) std::memcpy(kp, k.data(), sizeof(float) * n * parts * 3);
         if (ks && n > 0) std::memcpy(ks, s.data(), sizeof(float) * n);
+    });
+}
+
+int opk_pose_set_timing(opk_pose* p, int enable)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->set_timing(enable != 0);
+    });
+}
+
+int opk_pose_read_timing(opk_pose* p, int* batches, double* total_ms)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->read_timing(batches, total_ms);
+    });
+}
+
+int opk_pose_records(opk_pose* p, float* rec, size_t capacity, size_t* used)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p && used, "NULL argument");
+        const opk::PoseHip& pose = *p->pose;
+        const int parts = opk::pose_model(pose.model()).parts;
+        size_t need = 0;
+        for (int f = 0; f < pose.frames(); ++f) need += 1 + (size_t)pose.num_people(f) * (parts * 3 + 1);
+        *used = need;
+        if (!rec) return;
+        OPK_CHECK_ARG(capacity >= need, "records buffer too small");
+        float* o = rec;
+        for (int f = 0; f < pose.frames(); ++f) {
+            const int n = pose.num_people(f);
+            *o++ = (float)n;
+            if (n == 0) continue;
+            std::memcpy(o, pose.keypoints(f).data(), sizeof(float) * n * parts * 3);
+            o += (size_t)n * parts * 3;
+            std::memcpy(o, pose.scores(f).data(), sizeof(float) * n);
+            o += n;
+        }
     });
 }
 

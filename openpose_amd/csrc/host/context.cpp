@@ -87,4 +87,47 @@ int* Context::nms_candidates(int frames, int parts)
     return static_cast<int*>(nms_scratch.ptr);
 }
 
+EventTimer::~EventTimer()
+{
+    for (auto* v : {&events_, &free_})
+        for (auto& e : *v) {
+            (void)hipEventDestroy(e.first);
+            (void)hipEventDestroy(e.second);
+        }
+}
+
+void EventTimer::begin(hipStream_t s)
+{
+    if (!on) return;
+    if (free_.empty()) {
+        std::pair<hipEvent_t, hipEvent_t> e;
+        OPK_HIP(hipEventCreate(&e.first));
+        OPK_HIP(hipEventCreate(&e.second));
+        free_.push_back(e);
+    }
+    events_.push_back(free_.back());
+    free_.pop_back();
+    OPK_HIP(hipEventRecord(events_.back().first, s));
+}
+
+void EventTimer::end(hipStream_t s)
+{
+    if (on && !events_.empty()) OPK_HIP(hipEventRecord(events_.back().second, s));
+}
+
+void EventTimer::read(int* count, double* total_ms)
+{
+    double t = 0;
+    for (auto& e : events_) {
+        OPK_HIP(hipEventSynchronize(e.second));
+        float ms = 0.f;
+        OPK_HIP(hipEventElapsedTime(&ms, e.first, e.second));
+        t += ms;
+        free_.push_back(e);
+    }
+    if (count) *count = (int)events_.size();
+    if (total_ms) *total_ms = t;
+    events_.clear();
+}
+
 }  // namespace opk

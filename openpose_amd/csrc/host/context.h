@@ -53,4 +53,19 @@ struct Context {
     }
 };
 
+// Device-time measurement hook (no reference counterpart): while enabled, begin()/end() bracket a
+// region of stream work with a pair of HIP events; read() waits for every recorded pair and
+// returns their count and summed milliseconds.
+class EventTimer {
+public:
+    ~EventTimer();
+    bool on = false;
+    void begin(hipStream_t s);
+    void end(hipStream_t s);
+    void read(int* count, double* total_ms);
+
+private:
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> events_, free_;
+};
+
 }  // namespace opk

@@ -35,10 +35,7 @@ int pick_bn(int cout)
 NetHip::NetHip(Context* ctx, std::vector<LayerDesc> layers, const std::string& output_blob)
     : ctx_(ctx), output_blob_(output_blob)
 {
-    const char* v = std::getenv("OPK_CONV_V1");   // A/B switch to the v1 kernel (dev only)
-    conv_v1_ = v && v[0] == '1';
     plan(layers);
-    conv_v1_ = conv_v1_ && border_ == 1;   // the v1 kernels know 1-pixel borders only
     if (ctx_->device >= 0) {
         ctx_->bind();
         OPK_HIP(hipDeviceGetAttribute(&cus_, hipDeviceAttributeMultiprocessorCount, ctx_->device));
@@ -243,14 +240,12 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
     OPK_CHECK_ARG(c.info.act != 2 || slope, name + ": PReLU slopes required");
     const int K = c.ksteps * kConvBK;
     const int cin = c.info.cin, k = c.info.k;
-    // the v1/v2 kernels (dev fallbacks) take 1x1 / 3x3 convolutions on 1-pixel borders only
-    const bool legacy = k != 7 && border_ == 1;
-    const bool need_packed = legacy || c.from_image;   // conv_image reads this layout too
+    const bool need_packed = c.from_image;   // conv_image's layout: [cout_pad][64]
     std::vector<uint16_t> packed(need_packed ? (size_t)c.cout_pad * K : 0, 0);
     auto f2h = [](float v) { _Float16 h = (_Float16)v; return __builtin_bit_cast(uint16_t, h); };
     for (int co = 0; co < c.info.cout && need_packed; ++co) {
         uint16_t* dst = packed.data() + (size_t)co * K;
-        if (c.from_image) {   // K index (ky*3 + kx)*3 + ci, matching launch_im2col3
+        if (c.from_image) {   // K index (ky*3 + kx)*3 + ci
             for (int ci = 0; ci < 3; ++ci)
                 for (int ky = 0; ky < 3; ++ky)
                     for (int kx = 0; kx < 3; ++kx)
@@ -346,14 +341,12 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
     }
     std::vector<uint16_t*>& ptr = S.base;
     ptr.assign(bufs_.size(), nullptr);
-    {
-        const char* e = std::getenv("OPK_CONV1_FUSED");   // dev A/B switch: 0 disables the fusion
-        S.fused1 = fuse1_.a >= 0 && !conv_v1_ && !(e && e[0] == '0') && border_ == 1 &&
-                   conv1_fused_supported(h, w, 64, 64);
-    }
+    // CONV1_FUSED=0 (opk_dev_set, A/B tests): the three separate kernels instead of the fusion
+    S.fused1 = fuse1_.a >= 0 && dev_switch("CONV1_FUSED", 1) != 0 && border_ == 1 &&
+               conv1_fused_supported(h, w, 64, 64);
     for (size_t i = 0; i < bufs_.size(); ++i) {
         S.mem.push_back(std::make_unique<DevBuf>());
-        if ((int)i == image_buf_ && !conv_v1_) continue;   // conv_image reads the NCHW input itself
+        if ((int)i == image_buf_) continue;   // conv_image reads the NCHW input itself
         if (S.fused1 && ((int)i == fuse1_.abuf || (int)i == fuse1_.bbuf))
             continue;   // conv1_1 / conv1_2 outputs live only inside conv1_fused_kernel
         // zeroed guards: the kernels read up to W+3 positions before the first frame and up to
@@ -367,8 +360,6 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
         OPK_HIP(hipMemsetAsync(raw, 0, bytes, ctx_->stream));
         ptr[i] = raw + head * bufs_[i].cs;
     }
-    const char* e3 = std::getenv("OPK_CONV3");   // dev A/B switch: OPK_CONV3=0 disables the halo kernel
-    const bool allow3 = (!conv_v1_ && !(e3 && e3[0] == '0')) || border_ != 1;
     const size_t out_bytes = (size_t)n * out_c_ * lh_[out_level_] * lw_[out_level_] * 4;
     S.out32 = static_cast<float*>(S.out_mem.get(out_bytes));
     void* sink = sink_.get(kConv3SinkBytes);
@@ -389,10 +380,9 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
             a.tapoff[0] = Wp + 1;
         a.border = border_;
         a.ksteps = c.ksteps;
-        const bool use3 = allow3 && !c.from_image && c.w3.ptr != nullptr;
+        const bool use3 = !c.from_image;
         S.use3[ci] = use3;
-        OPK_CHECK_ARG(use3 || c.from_image || (c.info.k != 7 && border_ == 1),
-                      c.info.name + ": 7x7 / wide-border convolutions run on the conv3 kernels only");
+        OPK_CHECK_ARG(use3 || c.w.ptr != nullptr, c.info.name + ": weights not set");
         if (use3) {
             const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, c.info.k, border_);
             a.sw = s3.sw;
@@ -432,19 +422,9 @@ void NetHip::forward(const float* input, int n, int h, int w)
     ctx_->bind();
     ShapePlan& S = *shape_plan(n, h, w);
     cur_ = &S;
-    if (timing_) {
-        if (free_events_.empty()) {
-            std::pair<hipEvent_t, hipEvent_t> e;
-            OPK_HIP(hipEventCreate(&e.first));
-            OPK_HIP(hipEventCreate(&e.second));
-            free_events_.push_back(e);
-        }
-        events_.push_back(free_events_.back());
-        free_events_.pop_back();
-        OPK_HIP(hipEventRecord(events_.back().first, ctx_->stream));
-    }
+    timer_.begin(ctx_->stream);
     forward_launches(S, input, n, h, w);
-    if (timing_) OPK_HIP(hipEventRecord(events_.back().second, ctx_->stream));
+    timer_.end(ctx_->stream);
 }
 
 void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, int w)
@@ -452,7 +432,6 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
     const std::vector<uint16_t*>& ptr = S.base;
     const std::vector<int>& lh_ = S.lh;
     const std::vector<int>& lw_ = S.lw;
-    if (conv_v1_) launch_im2col3(ptr[image_buf_], input, n, h, w, ctx_->stream);
     size_t first = 0;
     if (S.fused1) {
         const ConvPlan& a = convs_[fuse1_.a];
@@ -484,10 +463,8 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
         if (s.conv) {
             const ConvPlan& c = convs_[s.idx];
             const ConvArgs& a = S.args[s.idx];
-            if (conv_v1_) launch_conv(a, c.bn > 128 ? 128 : c.bn, ctx_->stream);
-            else if (c.from_image) launch_conv_image(a, input, ctx_->stream);
-            else if (S.use3[s.idx]) launch_conv3(a, ctx_->stream);
-            else launch_conv2(a, c.bn, ctx_->stream);
+            if (c.from_image) launch_conv_image(a, input, ctx_->stream);
+            else launch_conv3(a, ctx_->stream);
         } else {
             const PoolPlan& p = pools_[s.idx];
             const int L = p.level_in;
@@ -529,33 +506,16 @@ int NetHip::load_caffemodel(const std::string& path)
     return loaded;
 }
 
-NetHip::~NetHip()
-{
-    for (auto* v : {&events_, &free_events_})
-        for (auto& e : *v) {
-            (void)hipEventDestroy(e.first);
-            (void)hipEventDestroy(e.second);
-        }
-}
+NetHip::~NetHip() = default;
 
 void NetHip::set_timing(bool on)
 {
-    timing_ = on;
+    timer_.on = on;
 }
 
 void NetHip::read_timing(int* count, double* total_ms)
 {
-    double t = 0;
-    for (auto& e : events_) {
-        OPK_HIP(hipEventSynchronize(e.second));
-        float ms = 0.f;
-        OPK_HIP(hipEventElapsedTime(&ms, e.first, e.second));
-        t += ms;
-        free_events_.push_back(e);
-    }
-    if (count) *count = (int)events_.size();
-    if (total_ms) *total_ms = t;
-    events_.clear();
+    timer_.read(count, total_ms);
 }
 
 }  // namespace opk

@@ -95,7 +95,6 @@ private:
     std::vector<BufSpec> bufs_;
     int out_level_ = 0, out_c_ = 0, nlevels_ = 1;
     int image_buf_ = -1;
-    bool conv_v1_ = false;
     struct Fuse1 { int a = -1, b = -1, p = -1, abuf = -1, bbuf = -1; };
     Fuse1 fuse1_;                 // conv1_1 -> conv1_2 -> pool1 (conv1_fused.hip) when planned
     int cus_ = 256;               // compute units (persistent-kernel grid)
@@ -104,9 +103,7 @@ private:
     std::vector<std::unique_ptr<ShapePlan>> shapes_;   // oldest first
     ShapePlan* cur_ = nullptr;    // shape of the last forward
     DevBuf sink_;                 // persistent conv3: target of masked-off stores
-    bool timing_ = false;
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> events_;   // recorded forwards
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> free_events_;
+    EventTimer timer_;            // forwards bracketed by HIP events (set_timing)
 };
 
 }  // namespace opk

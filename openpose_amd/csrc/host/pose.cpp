@@ -265,6 +265,7 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
     ctx_->bind();
     hipStream_t s = ctx_->stream;
     Slot& sl = slots_[(head_ + count_) & 1];
+    timer_.begin(s);
     if (overlay_) {   // synthetic people on the first scale's output
         const size_t out_elems = (size_t)n * C * outs[0].h * outs[0].w;
         launch_add_inplace(const_cast<float*>(outs[0].ptr), overlay_, out_elems, s);
@@ -312,6 +313,7 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
     float* rec = static_cast<float*>(sl.records.get((size_t)n * rf * 4));
     launch_paf_scores_compact(rec, (int)rf, heat, peaks, n, kMaxPeaks, pt, inter_th, inter_min,
                               reject, near, s);
+    timer_.end(s);
     OPK_HIP(hipEventRecord(sl.done, s));
     sl.n = n;
     sl.H = H;

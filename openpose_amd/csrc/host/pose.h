@@ -65,6 +65,10 @@ public:
     // out [parts][kMaxPeaks][3], counts [parts]
     void candidates(int frame, float* out, int* counts) const;
     float scale_net_to_output() const { return scale_net_to_output_; }
+    // device time of the post-processing of every submitted batch (overlay add, NMS, PAF
+    // integrals: the work after the net forward), HIP events on the context stream
+    void set_timing(bool on) { timer_.on = on; }
+    void read_timing(int* count, double* total_ms) { timer_.read(count, total_ms); }
     int model() const { return model_; }
 
     static constexpr int kMaxPeaks = kPoseMaxPeople;   // peaks blob [parts][128][3]
@@ -101,6 +105,7 @@ private:
     double props_[5];
     const float* overlay_ = nullptr;
     hipStream_t copy_ = nullptr;         // D2H of collected batches (overlaps the next batch)
+    EventTimer timer_;
 
     Slot slots_[2];
     int head_ = 0, count_ = 0, last_ = -1;

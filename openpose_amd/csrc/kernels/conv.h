@@ -13,7 +13,6 @@ namespace opk {
 //       discarded: every 3x3 tap is then a constant shift of the whole tile),
 //   N = output channels, K = taps * cin_pad (tap-major, channels inner, 32-channel chunks).
 constexpr int kConvMaxDst = 6;
-constexpr int kConvBM = 128;
 constexpr int kConvBK = 64;
 
 struct ConvArgs {
@@ -37,18 +36,14 @@ struct ConvArgs {
     int out32_c, out32_coff;
     int sw, nstrips;      // conv3 only: strip width and count (conv3_shape)
     float rcp[3];         // conv3 only, set by launch_conv3: 1/((H+2)(sw+2)), 1/(sw+2), 1/nstrips
-    int wide;             // conv3 only, set by launch_conv3: 16-byte epilogue stores allowed (dev A/B switch)
-    int prio;             // conv3 persistent: s_setprio(1) around each unit's MFMAs (dev A/B switch)
+    int wide;             // conv3 only, set by launch_conv3: 16-byte epilogue stores allowed (CONV3_WIDE)
+    int prio;             // conv3 persistent: s_setprio(1) around each unit's MFMAs (CONV3P_PRIO)
     void* sink;           // conv3 persistent variant: >= kConv3SinkBytes of scratch (masked stores)
     int cus;              // conv3 persistent variant: compute units (grid size); 0 disables it
     int border;           // zero border of the padded images (conv3 / conv_image; 0 means 1)
 };
 
-// v1 (conv.hip): 256 lanes, 128 x bn tile, register-staged; bn: 32, 64, 96 or 128
-void launch_conv(const ConvArgs& a, int bn, hipStream_t stream);
-// v2 (conv2.hip): 512 lanes, 256 x bn tile, LDS-DMA 3-slot ring; bn: 32, 64, 96, 128 or 256
-void launch_conv2(const ConvArgs& a, int bn, hipStream_t stream);
-// v3 (conv3.hip): 3x3 and 1x1, input halo staged once per 32-channel chunk over a "virtual image" of
+// conv3.hip: 7x7, 3x3 and 1x1, input halo staged once per 32-channel chunk over a "virtual image" of
 // column strips (sw interior columns each).  Tile BM x BN = 256 x 128 / 96 (<= 80 KB LDS, two
 // workgroups per CU, or 136 KB, one), 512 x 64 for cout <= 64; optional fp32 NCHW output (out32).
 // Weights packed [cout_pad/BN][cin_pad/32][ky][kx][BN][32] (BN = conv3_shape(...).bn).  Reads padded positions down to -1
@@ -66,13 +61,8 @@ struct Conv3Shape {
 Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border = 1);
 void launch_conv3(const ConvArgs& a, hipStream_t stream);
 
-// NCHW fp32 [frames][3][H][W] -> padded NHWC fp16 [frames][H+2][W+2][32] holding, at each pixel,
-// the 27 values of its 3x3x3 window (channel q = (ky*3+kx)*3 + ci), then zeros: conv1_1 becomes
-// a 1-tap GEMM with K = 32.
-void launch_im2col3(uint16_t* out, const float* in, int frames, int H, int W, hipStream_t stream);
-
 // First conv (3 input channels, 3x3, cout <= 64) straight from the fp32 NCHW input [frames][3][H][W]
-// (conv_image.hip); weights as packed for v1/v2 ([cout_pad][64], K order (ky*3 + kx)*3 + ci).
+// (conv_image.hip); weights [cout_pad][64], K order (ky*3 + kx)*3 + ci.
 void launch_conv_image(const ConvArgs& a, const float* image, hipStream_t stream);
 
 // conv1_1 (3 -> 64) + act -> conv1_2 (64 -> 64) + act -> 2x2/2 max pool in one persistent kernel

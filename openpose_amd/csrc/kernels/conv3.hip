@@ -357,7 +357,7 @@ void conv3_kernel(const ConvArgs a)
     const bool vec = (a.cout & 3) == 0;
     // 16-byte stores (see conv3p_kernel): fragment pairs exchanged between lane rows q and q^1 by
     // v_permlane16_swap, each lane then holds 8 consecutive channels of its position.  Needs whole
-    // 8-channel groups and 16-byte aligned destination slices; OPK_CONV3_WIDE=0 (dev A/B) disables.
+    // 8-channel groups and 16-byte aligned destination slices; CONV3_WIDE=0 (opk_dev_set) disables.
     bool wide = NF % 2 == 0 && (a.cout & 7) == 0 && !a.out32 && a.wide;
     for (int d = 0; d < a.ndst; ++d) wide = wide && ((a.dst_coff[d] | a.dst_cs[d]) & 7) == 0;
     if (wide) {
@@ -781,21 +781,13 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
 
 }  // namespace
 
-namespace {
-int env_int(const char* name, int dflt)
-{
-    const char* e = std::getenv(name);
-    return e && e[0] ? std::atoi(e) : dflt;
-}
-}  // namespace
-
 Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border)
 {
-    // dev A/B switches (read per call so tests can compare variants in one process):
-    // OPK_CONV3_SMALL=0 -> no two-per-CU tiles, OPK_CONV3_W16=0 -> no 16-wave tiles,
-    // OPK_CONV3_PERSIST=0 -> 16-wave tiles without the persistent kernel
-    const bool small = env_int("OPK_CONV3_SMALL", 1) != 0;
-    const int big16 = env_int("OPK_CONV3_W16", 1);
+    // variant switches (opk_dev_set; read per call so tests can compare variants in one process):
+    // CONV3_SMALL=0 -> no two-per-CU tiles, CONV3_W16=0 -> no 16-wave tiles,
+    // CONV3_PERSIST=0 -> 16-wave tiles without the persistent kernel
+    const bool small = dev_switch("CONV3_SMALL", 1) != 0;
+    const int big16 = dev_switch("CONV3_W16", 1);
     OPK_CHECK_ARG(ks == 1 || ks == 3 || ks == 7, "conv3: 1x1, 3x3 or 7x7");
     OPK_CHECK_ARG(border >= 1 && border >= ks / 2, "conv3: the zero border must cover the pad");
     Conv3Shape s;
@@ -811,15 +803,15 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border)
         s.minb = 2;
         s.nstrips = 1;
         s.sw = W;
-        // dev A/B: OPK_CONV1_TILE=1 -> 512x128 tiles of 16 waves, 2 -> 256x256 tiles of 16 waves
+        // dev A/B: CONV1_TILE=1 -> 512x128 tiles of 16 waves, 2 -> 256x256 tiles of 16 waves
         // (cout % 256 == 0): fewer tile rows staged per MFMA than 256x128
         // (default 2: measured -10..-20 % on the 384->512 and 288->256 layers)
-        const int t1 = env_int("OPK_CONV1_TILE", 2);
+        const int t1 = dev_switch("CONV1_TILE", 2);
         if (t1 == 1 && s.bn == 128) {
             s.bm = 512; s.hr = 512; s.nw = 16; s.minb = 1;
         } else if (t1 == 2 && cout % 256 == 0) {
             s.bn = 256; s.nw = 16; s.minb = 1;
-        } else if (s.bn == 64 && env_int("OPK_CONV1_N64W16", 0) != 0) {   // dev A/B: 512x64, 16 waves
+        } else if (s.bn == 64 && dev_switch("CONV1_N64W16", 0) != 0) {   // dev A/B: 512x64, 16 waves
             s.bm = 512; s.hr = 512; s.nw = 16; s.minb = 1;
         }
         return s;
@@ -836,7 +828,7 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border)
         // (measured, round 1: 4-wave 256x128 two-per-CU tiles and 8-wave 512x128 tiles of 128x64
         // wave tiles were both slower than these on every BODY_25 layer)
         if (s.bn != 64 && big16 && tiles >= 3 * 256) {   // 512 x {128,96} tiles, 16 waves
-            s.persist = env_int("OPK_CONV3_PERSIST", 1) != 0;
+            s.persist = dev_switch("CONV3_PERSIST", 1) != 0;
             // the persistent kernel keeps bias/slopes in LDS: 688 halo rows
             s.bm = 512; s.hr = s.persist ? kP_HR : 704; s.tapu = 3; s.minb = 1; s.nw = 16;
         } else if (small && tiles >= 2 * 256) {   // <= 80 KB of LDS
@@ -860,8 +852,8 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
 {
     ConvArgs a = args;   // + the reciprocals of the strip geometry (Strips::map, kernel arguments)
     if (a.border <= 0) a.border = 1;
-    a.wide = env_int("OPK_CONV3_WIDE", 1);
-    a.prio = env_int("OPK_CONV3P_PRIO", 0);
+    a.wide = dev_switch("CONV3_WIDE", 1);
+    a.prio = dev_switch("CONV3P_PRIO", 0);
     const int B = a.border;
     a.rcp[0] = (float)(1.0 / ((double)(a.H + 2 * B) * (a.sw + 2 * B)));
     a.rcp[1] = (float)(1.0 / (double)(a.sw + 2 * B));
@@ -896,9 +888,9 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
             // fragments ran 20 % slower on the 128-channel layers; a pipelined 16x16x32 fragment
             // schedule spilled at the 128-VGPR budget and ran 4 % slower; the explicit-counter
             // fragment schedule measured 1.5 % faster over the whole CNN, bit-identical)
-            const bool asmr = env_int("OPK_CONV3P_ASMR", 1) != 0;
-            // 16-byte epilogue stores (measured in tools/ab_asmr.sh; OPK_CONV3P_WIDE=0: dwordx2)
-            const bool wide = env_int("OPK_CONV3P_WIDE", 1) != 0;
+            const bool asmr = dev_switch("CONV3P_ASMR", 1) != 0;
+            // 16-byte epilogue stores (measured in tools/ab_asmr.sh; CONV3P_WIDE=0: dwordx2)
+            const bool wide = dev_switch("CONV3P_WIDE", 1) != 0;
 #define OPK3P_LAUNCH(BN_, ASMR_, WIDE_)                                                        \
     hipLaunchKernelGGL((conv3p_kernel<BN_, ASMR_, WIDE_>), dim3(G), dim3(1024), 0, stream, a)
             if (s.bn == 96) {

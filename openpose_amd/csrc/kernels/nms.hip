@@ -98,8 +98,8 @@ constexpr int LOX = LT - 2;       // tile columns
 constexpr int LMAXR = 16;         // source rows per window kept in LDS (x8 upsampling of a
                                   // 34-row window needs 9)
 
-// LOY = tile rows (window rows LOY + 2); OPK_NMS_LOY selects 16 / 32 / 48 (dev A/B). Measured per
-// 64-frame launch: 16 rows 638 us, 32 rows 774 us, 48 rows 938 us (more, shorter workgroups win)
+// LOY = tile rows (window rows LOY + 2).  Measured per 64-frame launch (round 1): 16 rows 638 us,
+// 32 rows 774 us, 48 rows 938 us (more, shorter workgroups win); 16 is the one compiled
 template <int LOY>
 __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ scratch,
                                                              const HeatMap M, int parts, float th)
@@ -344,15 +344,9 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat, int frames, int
         hipLaunchKernelGGL(nms_detect_kernel, g1, dim3(DT), 0, stream, scratch, heat.heat,
                            heat.channels, parts, h, w, threshold);
     } else {
-        const char* e = std::getenv("OPK_NMS_LOY");
-        const int loy = e && e[0] ? std::atoi(e) : 16;
-#define OPK_NMS_LAZY(LOY_)                                                                    \
-    hipLaunchKernelGGL(nms_detect_lazy_kernel<LOY_>, dim3((w + LOX - 1) / LOX, (h + LOY_ - 1) / LOY_, \
-                       frames * parts), dim3(LT), 0, stream, scratch, heat, parts, threshold)
-        if (loy == 16) OPK_NMS_LAZY(16);
-        else if (loy == 48) OPK_NMS_LAZY(48);
-        else OPK_NMS_LAZY(32);
-#undef OPK_NMS_LAZY
+        constexpr int loy = 16;
+        hipLaunchKernelGGL(nms_detect_lazy_kernel<loy>, dim3((w + LOX - 1) / LOX, (h + loy - 1) / loy,
+                           frames * parts), dim3(LT), 0, stream, scratch, heat, parts, threshold);
     }
     OPK_LAUNCH_CHECK();
     dim3 g2(parts, frames);

@@ -8,6 +8,14 @@ frames assigned to ranks in contiguous blocks (no data-path collective: every ra
 hot path on its own frames), and the per-frame keypoint records gathered to rank 0 in frame order
 (the only collective; a few KB per frame).
 """
+import os
+import socket
+import subprocess
+import sys
+import time
+
+import numpy as np
+import torch
 import torch.distributed as dist
 
 
@@ -48,3 +56,137 @@ def run_sharded(process_batch, n_frames, batch, rank, world):
     for i in range(0, len(mine), batch):
         out.update(process_batch(mine[i:i + batch]))
     return out
+
+
+# ---- launcher: one process per GPU --------------------------------------------------------------
+def free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, port=None, env=None, timeout=None):
+    """Start `python argv...` n times as ranks 0..n-1 of one job (RANK, LOCAL_RANK, WORLD_SIZE,
+    MASTER_ADDR=127.0.0.1, MASTER_PORT) and wait for all of them.  The reference starts one worker
+    thread per GPU (wrapperAuxiliary.hpp:328-337); here each GPU gets a process, started as a child
+    of a parent that itself makes no GPU call.  If a rank fails, the others are terminated (by
+    PID).  Returns 0 or the first non-zero exit status."""
+    port = port or free_port()
+    procs = []
+    for r in range(n):
+        e = dict(os.environ if env is None else env)
+        e.update(RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=e))
+    t0 = time.time()
+    rc = 0
+    alive = list(procs)
+    while alive:
+        for p in list(alive):
+            code = p.poll()
+            if code is None:
+                continue
+            alive.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in alive:
+                    q.terminate()
+        if timeout is not None and time.time() - t0 > timeout and alive:
+            for q in alive:
+                q.kill()
+            rc = rc or 124
+        time.sleep(0.05)
+    return rc
+
+
+# ---- ordered per-step result gather (WQueueOrderer) ----------------------------------------------
+HEAD = 5   # record header: rank, step, first frame id, frames, payload floats
+
+
+class RecordGather:
+    """Gathers every rank's per-frame result records to rank 0 once per step, in frame order.
+
+    The reference's WQueueOrderer (include/openpose/thread/wQueueOrderer.hpp:62-141) re-sequences
+    the datums that its per-GPU workers finish out of order.  Here the frames of step i are split
+    into contiguous per-rank slices (rank r holds frames (i * world + r) * batch ...), each rank
+    packs its slice's records (PoseExtractor.records(): per frame [people, keypoints, scores]),
+    and one gather per step (RCCL over xGMI on the GPU box, gloo on CPU) moves them to rank 0.
+    `finish()` on rank 0 returns the records of every frame in frame order and raises if a frame
+    is missing or duplicated.  `capacity` = floats per rank and step (records beyond it raise)."""
+
+    def __init__(self, world, rank, capacity, steps, device, group=None):
+        self.world, self.rank, self.steps, self.group = world, rank, steps, group
+        self.device = torch.device(device)
+        self.cap = int(capacity)
+        cuda = self.device.type == "cuda"
+        self.send = torch.zeros(HEAD + self.cap, dtype=torch.float32, device=self.device)
+        # two host staging buffers: the upload of step i may still be in flight while step i+1
+        # packs (cuda: pinned memory + one event per buffer)
+        self.host = [torch.zeros(HEAD + self.cap, dtype=torch.float32, pin_memory=cuda)
+                     for _ in range(2)]
+        self.events = [torch.cuda.Event() if cuda else None for _ in range(2)]
+        self.recv = (torch.zeros((steps, world, HEAD + self.cap), dtype=torch.float32,
+                                 device=self.device) if rank == 0 else None)
+
+    def push(self, step, first_frame, n_frames, records):
+        n = int(records.size)
+        if n > self.cap:
+            raise RuntimeError("rank %d step %d: %d record floats exceed the gather capacity %d"
+                               % (self.rank, step, n, self.cap))
+        k = step % 2
+        if self.events[k] is not None and step >= 2:
+            self.events[k].synchronize()
+        h = self.host[k].numpy()
+        h[:HEAD] = (self.rank, step, first_frame, n_frames, n)
+        h[HEAD:HEAD + n] = records
+        self.send[:HEAD + n].copy_(self.host[k][:HEAD + n], non_blocking=True)
+        if self.events[k] is not None:
+            self.events[k].record()
+        if self.world == 1:
+            self.recv[step, 0].copy_(self.send)
+        else:
+            dist.gather(self.send, list(self.recv[step].unbind(0)) if self.rank == 0 else None,
+                        dst=0, group=self.group)
+
+    def finish(self, parts):
+        """Rank 0: [(keypoints [people, parts, 3], scores [people]), ...] for frames 0..F-1."""
+        if self.rank != 0:
+            return None
+        rec = self.recv.cpu().numpy()
+        frames = {}
+        for i in range(self.steps):
+            for r in range(self.world):
+                head = rec[i, r, :HEAD]
+                rank, step, first, nf, n = (int(v) for v in head)
+                if rank != r or step != i:
+                    raise RuntimeError("step %d rank %d: record header %s" % (i, r, head.tolist()))
+                body = rec[i, r, HEAD:HEAD + n]
+                o = 0
+                for f in range(first, first + nf):
+                    people = int(body[o])
+                    o += 1
+                    kp = body[o:o + people * parts * 3].reshape(people, parts, 3)
+                    o += people * parts * 3
+                    ks = body[o:o + people]
+                    o += people
+                    if f in frames:
+                        raise RuntimeError("frame %d produced twice" % f)
+                    frames[f] = (kp.copy(), ks.copy())
+                if o != n:
+                    raise RuntimeError("step %d rank %d: %d of %d record floats parsed" % (i, r, o, n))
+        ids = sorted(frames)
+        if ids != list(range(len(ids))):
+            raise RuntimeError("frames missing from the gather: %s"
+                               % sorted(set(range(ids[-1] + 1)) - set(ids)))
+        return [frames[i] for i in ids]
+
+
+def pack_records(results, parts):
+    """Host-side packing of [(keypoints, scores), ...] into the opk_pose_records layout."""
+    out = []
+    for kp, ks in results:
+        kp = np.asarray(kp, np.float32).reshape(-1, parts, 3)
+        out.append(np.float32([kp.shape[0]]))
+        out.append(kp.reshape(-1))
+        out.append(np.asarray(ks, np.float32).reshape(-1))
+    return np.concatenate(out) if out else np.zeros(0, np.float32)

@@ -72,13 +72,17 @@ def lib():
 
 
 def ref_lib():
-    """The reference's own connector (compiled from /root/reference), or None if unavailable."""
+    """The reference's own connector (compiled from /root/reference), or None if unavailable.
+
+    Only where the reference tree itself is present (this container): a copy of oracle/_ref that
+    travelled with the repository to the GPU box is never loaded there -- the GPU tests check
+    against the committed fixtures (tests/golden/) that this build produced."""
     global _REF
     if _REF is None:
+        if not os.path.isdir("/root/reference"):
+            return None
         path = os.path.join(_HERE, "_ref", "libref_connector.so")
         if not os.path.exists(path):
-            if not os.path.isdir("/root/reference"):
-                return None
             build(ref=True)
         R = ctypes.CDLL(path, mode=os.RTLD_LAZY)  # OpenCV-only symbols stay unresolved
         R.ref_connect_cpu.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _i, _f, _f, _i,

@@ -2,6 +2,7 @@
 frame exactly once, in frame order, identical to a single-process run.  Per-frame work is the
 product's host people assembly (libopk_hip.so, no GPU needed) on synthetic people fields."""
 import os
+import sys
 import tempfile
 
 import numpy as np
@@ -62,3 +63,54 @@ def test_frame_parallel_gloo_world2():
 def test_gather_detects_missing_frames():
     with pytest.raises(RuntimeError, match="missing"):
         parallel.gather_in_order({0: 1, 2: 3}, 1, 0)
+
+
+def test_launcher_ordered_gather_gloo():
+    """bench.py --gpus N's launcher (parallel.launch_ranks: N child processes, RANK/WORLD_SIZE/
+    MASTER_* set, parent makes no device call) + the per-step RecordGather: rank 0 receives every
+    frame exactly once, in frame order, with its records intact."""
+    from tests.rank_stub import frame_result
+    steps, batch, parts = 3, 5, 25
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res.npz")
+        stub = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rank_stub.py")
+        rc = parallel.launch_ranks(2, [stub, out, str(steps), str(batch), str(parts)], timeout=120)
+        assert rc == 0
+        got = np.load(out)
+        n = int(got["n"])
+        assert n == 2 * steps * batch
+        for f in range(n):
+            kp, ks = frame_result(f, parts)
+            np.testing.assert_array_equal(got["kp%d" % f], kp)
+            np.testing.assert_array_equal(got["ks%d" % f], ks)
+
+
+def test_launcher_propagates_failure():
+    rc = parallel.launch_ranks(2, ["-c", "import os, sys; sys.exit(3 if os.environ['RANK'] == '1' "
+                                         "else 0)"], timeout=60)
+    assert rc == 3
+
+
+def test_record_gather_rejects_duplicates_and_gaps():
+    g = parallel.RecordGather(1, 0, 100, 2, "cpu")
+    rec = parallel.pack_records([(np.zeros((0, 25, 3)), np.zeros(0))] * 2, 25)
+    g.push(0, 0, 2, rec)
+    g.push(1, 3, 2, rec)          # frames 3, 4: frame 2 never produced
+    with pytest.raises(RuntimeError, match="missing"):
+        g.finish(25)
+    g = parallel.RecordGather(1, 0, 100, 2, "cpu")
+    g.push(0, 0, 2, rec)
+    g.push(1, 1, 2, rec)          # frame 1 twice
+    with pytest.raises(RuntimeError, match="twice"):
+        g.finish(25)
+    with pytest.raises(RuntimeError, match="capacity"):
+        g.push(0, 0, 2, np.zeros(101, np.float32))
+
+
+def test_bench_rejects_world_mismatch():
+    import subprocess
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    bench = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "bench.py")
+    r = subprocess.run([sys.executable, bench, "--gpus", "4"], env=env, capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr

@@ -14,13 +14,14 @@ import torch
 import oracle
 from oracle import body25
 from openpose_amd import synth
-from openpose_amd.api import Net
+from openpose_amd.api import Net, dev_switches
 from tests import prototxt
 
 pytestmark = pytest.mark.gpu
 
 SMALL_TOL = 4e-3      # relative L2, graphs of <= 6 layers
-BODY25_TOL = 2e-2     # relative L2, the full 114-conv network
+BODY25_TOL = 5e-3     # relative L2, the full 114-conv network (measured 1.5-2.5e-3)
+CHANNEL_TOL = 2e-2    # relative L2 of any single output channel of a frame (measured < 6e-3)
 
 
 def rel_l2(a, b):
@@ -97,6 +98,63 @@ def test_body25_vs_oracle(ctx, n, h, w):
     assert err < BODY25_TOL
 
 
+def channel_errors(got, ref):
+    """relative L2 per (frame, channel) plane"""
+    d = np.linalg.norm((got - ref).reshape(got.shape[0], got.shape[1], -1), axis=2)
+    r = np.linalg.norm(ref.reshape(ref.shape[0], ref.shape[1], -1), axis=2)
+    return d / np.maximum(r, 1e-30)
+
+
+def test_body25_bench_geometry_vs_oracle(ctx):
+    """The net at the bench's shape (64 x 3 x 368 x 656: the persistent 16-wave 512-row tiles,
+    the 256x256 1x1 tiles, the fused conv1 kernel and the strip geometry the bench runs), frames
+    0, 31 and 63 against the fp32 oracle (frames are independent; every tile row of the first
+    and last frames is covered), whole-frame and per-channel tolerance."""
+    graph = body25.layers()
+    params = synth.he_weights(graph, seed=13)
+    n, h, w = 64, 368, 656
+    rng = np.random.default_rng(14)
+    x = rng.uniform(-0.5, 0.5, (n, 3, h, w)).astype(np.float32)
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(params)
+    net.forward(torch.from_numpy(x).cuda())
+    got = net.output_numpy()
+    assert got.shape == (n, 78, h // 8, w // 8)
+    pick = [0, 31, 63]
+    ref = body25.forward(x[pick], params, graph=graph)
+    err = rel_l2(got[pick], ref)
+    ch = channel_errors(got[pick], ref)
+    print("BODY_25 64x368x656 frames %s rel-L2 %.3e, worst channel %.3e" % (pick, err, ch.max()))
+    assert err < BODY25_TOL
+    assert ch.max() < CHANNEL_TOL
+
+
+def test_net_output_query_follows_addCaffeNetOnThread(ctx):
+    """The call sequence PoseExtractorCaffe uses (poseExtractorCaffe.cpp:82-95): create the net,
+    query its output blob BEFORE any forward (it is kept for every frame), forward, read it,
+    forward again: the blob of one input shape keeps its device pointer and holds the new
+    values (NetCaffe's live blob, netCaffe.cpp:263-268)."""
+    graph = body25.layers()
+    params = synth.he_weights(graph, seed=15)
+    net = Net(ctx, "builtin:BODY_25")
+    p0, shape0 = net.output()
+    assert p0 is None and shape0 == (0, 78, 0, 0)
+    net.set_params(params)
+    rng = np.random.default_rng(16)
+    x1 = rng.uniform(-0.5, 0.5, (2, 3, 64, 96)).astype(np.float32)
+    x2 = rng.uniform(-0.5, 0.5, (2, 3, 64, 96)).astype(np.float32)
+    net.forward(torch.from_numpy(x1).cuda())
+    p1, shape1 = net.output()
+    v1 = net.output_numpy()
+    net.forward(torch.from_numpy(x2).cuda())
+    p2, shape2 = net.output()
+    v2 = net.output_numpy()
+    assert p1 is not None and p1 == p2 and shape1 == shape2 == (2, 78, 8, 12)
+    assert not np.array_equal(v1, v2)
+    ref2 = body25.forward(x2, params, graph=graph)
+    assert rel_l2(v2, ref2) < BODY25_TOL
+
+
 @pytest.mark.parametrize("hw,acts", [((24, 40), ("relu", "relu")), ((26, 130), ("relu", "prelu")),
                                      ((14, 6), ("prelu", "relu"))])
 def test_conv1_fused_matches_unfused(ctx, hw, acts):
@@ -109,12 +167,9 @@ def test_conv1_fused_matches_unfused(ctx, hw, acts):
     L.append(dict(name="net_output", type="Concat", bottom=["c4"], top=["net_output"]))
     x = np.random.default_rng(7).uniform(-0.5, 0.5, (3, 3) + hw).astype(np.float32)
     outs = []
-    for fused in ("1", "0"):
-        os.environ["OPK_CONV1_FUSED"] = fused
-        try:
+    for fused in (1, 0):
+        with dev_switches(CONV1_FUSED=fused):
             got, ref = run_graph(ctx, L, x, seed=3)
-        finally:
-            os.environ.pop("OPK_CONV1_FUSED", None)
         assert rel_l2(got, ref) < SMALL_TOL
         outs.append(got)
     np.testing.assert_array_equal(outs[0], outs[1])
@@ -151,12 +206,13 @@ def test_7x7_cpm_stages_vs_oracle(ctx, concat, hw):
     assert got.shape == ref.shape and err < SMALL_TOL
 
 
-VARIANTS = {"persistent": {}, "w16": {"OPK_CONV3_PERSIST": "0"},
-            "w8": {"OPK_CONV3_W16": "0"}, "w8_one_per_cu": {"OPK_CONV3_W16": "0", "OPK_CONV3_SMALL": "0"},
-            "persistent_compiler_frags": {"OPK_CONV3P_ASMR": "0"}, "persistent_dwordx2": {"OPK_CONV3P_WIDE": "0"},
-            "dwordx2": {"OPK_CONV3P_WIDE": "0", "OPK_CONV3_WIDE": "0"},
-            "w16_dwordx2": {"OPK_CONV3_PERSIST": "0", "OPK_CONV3_WIDE": "0"},
-            "conv1_512x128": {"OPK_CONV1_TILE": "1"}, "conv1_256x128": {"OPK_CONV1_TILE": "0"}, "conv1_512x64": {"OPK_CONV1_N64W16": "1"}}
+VARIANTS = {"persistent": {}, "w16": {"CONV3_PERSIST": 0},
+            "w8": {"CONV3_W16": 0, "CONV1_TILE": 0}, "w8_one_per_cu": {"CONV3_W16": 0, "CONV3_SMALL": 0},
+            "persistent_compiler_frags": {"CONV3P_ASMR": 0}, "persistent_dwordx2": {"CONV3P_WIDE": 0},
+            "dwordx2": {"CONV3P_WIDE": 0, "CONV3_WIDE": 0},
+            "w16_dwordx2": {"CONV3_PERSIST": 0, "CONV3_WIDE": 0},
+            "conv1_512x128": {"CONV1_TILE": 1}, "conv1_256x256": {"CONV1_TILE": 2},
+            "conv1_512x64": {"CONV1_N64W16": 1}}
 ROUNDING_VARIANTS = set()   # variants with another MFMA shape (another fp32 summation order)
 
 
@@ -181,17 +237,13 @@ def test_conv3_tile_variants_bit_identical(ctx):
         path = f.name
     outs = {}
     try:
-        for name, env in VARIANTS.items():
-            os.environ.update(env)
-            try:
+        for name, sw in VARIANTS.items():
+            with dev_switches(**sw):
                 net = Net(ctx, path)
                 net.set_params(params)
                 net.forward(torch.from_numpy(x).cuda())
                 outs[name] = net.output_numpy()
                 net.close()
-            finally:
-                for k in env:
-                    os.environ.pop(k, None)
     finally:
         os.unlink(path)
     assert np.isfinite(outs["w8"]).all() and np.abs(outs["w8"]).max() > 0

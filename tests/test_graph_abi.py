@@ -93,3 +93,13 @@ def test_unsupported_layers_are_rejected():
             Net(ctx, path)
     finally:
         os.unlink(path)
+
+
+def test_net_output_is_queryable_before_any_forward():
+    """NetCaffe::getOutputBlobArray is called once right after initialization, before any forward
+    (poseExtractorCaffe.cpp:94-95): opk_net_output answers then, with no device work."""
+    ctx = Context.host_only()
+    net = Net(ctx, "builtin:BODY_25")
+    assert net.output() == (None, (0, 78, 0, 0))
+    hand = Net(ctx, "builtin:HAND")
+    assert hand.output() == (None, (0, 22, 0, 0))

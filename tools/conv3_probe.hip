@@ -12,9 +12,18 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 using namespace opk;
+
+// the library's opk_dev_set table is not linked into this dev tool: variant switches come from
+// OPK_<KEY> environment variables here (tools/probe_run.sh)
+int opk::dev_switch(const char* key, int dflt)
+{
+    const char* e = std::getenv((std::string("OPK_") + key).c_str());
+    return e && e[0] ? std::atoi(e) : dflt;
+}
 
 #define CK(x)                                                                  \
     do {                                                                       \
