@@ -1,11 +1,14 @@
 // heat_dev.h -- device side of HeatMap (kernels.h): one full-resolution heat-map value, read from
 // HBM or evaluated on the fly with the resize/merge arithmetic of resize.hip.
 //
-// cv::resize INTER_CUBIC numerics (resizeAndMergeBase.cpp:9-113 -> OpenCV): horizontal pass of the
-// four source rows around the target row ((t0 + t1) + t2) + t3 with the column's coefficients,
-// then the vertical combination in the same order; sources merged in order as v + acc, and the
-// sum times (float)(1/N) for N > 1.  Compiled with -ffp-contract=off everywhere it is used, so
-// resize_merge_kernel, the NMS and the PAF scorer all produce the same bits for a pixel.
+// cv::resize INTER_CUBIC numerics (resizeAndMergeBase.cpp:9-113 -> OpenCV 4.x): horizontal pass of
+// the four source rows around the target row ((t0 + t1) + t2) + t3 with the column's coefficients
+// (HResizeCubic), then the vertical combination of VResizeCubic: columns inside the whole 4-float
+// vectors of OpenCV's SIMD kernel sum h0 b0 + (h1 b1 + (h2 b2 + h3 b3)) (VResizeCubicVec_32f,
+// v_fma = mul + add on the SSE baseline), the tail columns (w % 4 of them) left to right;
+// sources merged in order as v + acc, and the sum times (float)(1/N) for N > 1 (oracle/resize.c
+// states the OpenCV text this follows).  Compiled with -ffp-contract=off everywhere it is used,
+// so resize_merge_kernel, the NMS and the PAF scorer all produce the same bits for a pixel.
 #pragma once
 #include "kernels.h"
 
@@ -21,6 +24,27 @@ __device__ __forceinline__ float cubic_hpass(const float* row, int sw, int x0, c
     const float v2 = row[heat_clampi(x0 + 1, 0, sw - 1)];
     const float v3 = row[heat_clampi(x0 + 2, 0, sw - 1)];
     return v0 * a[0] + v1 * a[1] + v2 * a[2] + v3 * a[3];
+}
+
+// OpenCV's vertical SIMD width on the x86-64 SSE baseline (v_float32::nlanes of CV_SIMD128)
+constexpr int kCvVResizeLanes = 4;
+
+// VResizeCubic of one column: x < vec_end (= w - w % 4) is inside OpenCV's SIMD body
+__device__ __forceinline__ float cubic_vpass(const float h[4], float b0, float b1, float b2, float b3,
+                                             bool simd)
+{
+    if (simd) {
+        const float t3 = h[3] * b3;
+        const float t2 = h[2] * b2 + t3;
+        const float t1 = h[1] * b1 + t2;
+        return h[0] * b0 + t1;
+    }
+    return h[0] * b0 + h[1] * b1 + h[2] * b2 + h[3] * b3;
+}
+
+__device__ __forceinline__ bool cubic_simd_column(int x, int w)
+{
+    return x < w - w % kCvVResizeLanes;
 }
 
 // value of plane `plane` (= frame * channels + channel) at full-resolution pixel (x, y)
@@ -40,7 +64,7 @@ __device__ __forceinline__ float heat_at(const HeatMap& M, int plane, int x, int
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             h[k] = cubic_hpass(src + (size_t)heat_clampi(yb + k, 0, S.sh - 1) * S.sw, S.sw, x0, a);
-        const float v = h[0] * b.x + h[1] * b.y + h[2] * b.z + h[3] * b.w;
+        const float v = cubic_vpass(h, b.x, b.y, b.z, b.w, cubic_simd_column(x, M.w));
         acc = (n == 0) ? v : v + acc;
     }
     return M.nsrc > 1 ? acc * M.inv_n : acc;

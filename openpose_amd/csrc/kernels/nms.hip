@@ -118,6 +118,7 @@ __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ s
     const int x = xw0 + tid;
     const int y0 = blockIdx.y * LOY - 1;           // window row 0
     const bool xin = x >= 0 && x < W;
+    const bool simd_col = cubic_simd_column(x, W);   // OpenCV's vertical SIMD body (heat_dev.h)
     const int ry_lo = max(y0, 0), ry_hi = min(y0 + LWR - 1, H - 1);
     __shared__ float4 rcoef[LWR];          // vertical coefficients of the window rows
     __shared__ int4 rofs[LWR];             // their 4 source rows as offsets into hb
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ s
                     hv[2] = cubic_hpass(src + (size_t)o.z * S.sw, S.sw, xo, a);
                     hv[3] = cubic_hpass(src + (size_t)o.w * S.sw, S.sw, xo, a);
                 }
-                v = hv[0] * bq.x + hv[1] * bq.y + hv[2] * bq.z + hv[3] * bq.w;
+                v = cubic_vpass(hv, bq.x, bq.y, bq.z, bq.w, simd_col);
             }
             acc[rr] = (n == 0) ? v : v + acc[rr];
         }

@@ -73,7 +73,7 @@ __global__ __launch_bounds__(TX) void resize_merge_kernel(float* __restrict__ ds
                     h[k] = tiled ? hbuf[(r - r_lo) * TX + tx]
                                  : cubic_hpass(src + (size_t)r * S.sw, S.sw, x0, a);
                 }
-                v = h[0] * b.x + h[1] * b.y + h[2] * b.z + h[3] * b.w;
+                v = cubic_vpass(h, b.x, b.y, b.z, b.w, cubic_simd_column(x, dw));
             }
             acc[j] = (n == 0) ? v : v + acc[j];
         }

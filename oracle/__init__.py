@@ -41,6 +41,8 @@ def lib():
         L.orc_resize_cubic.argtypes = [_f32p, _f32p, _i, _i, _i, _i]
         L.orc_resize_merge.argtypes = [_f32p, ctypes.POINTER(ctypes.c_void_p), _i, _i, _i32p, _i, _i]
         L.orc_cubic_tables.argtypes = [_i, _i, _i32p, _f32p]
+        L.orc_set_resize_simd.argtypes = [_i]
+        L.orc_resize_simd.restype = _i
         L.orc_paf_score.restype = _f
         L.orc_paf_score.argtypes = [_f32p, _f32p, _f32p, _f32p, _i, _i, _f, _f, _f]
         L.orc_connect_body_parts.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _i, _f,
@@ -119,6 +121,23 @@ def resize_merge(srcs, dh, dw):
     hw = np.array([[s.shape[1], s.shape[2]] for s in srcs], np.int32).ravel()
     lib().orc_resize_merge(out, ptrs, len(srcs), c, hw, dh, dw)
     return out
+
+
+class resize_order:
+    """Context manager: the OpenCV version whose vertical summation order the resize restatement
+    follows ("4.x": SIMD body of 4 lanes, the default; "3.x": left to right; see resize.c)."""
+
+    def __init__(self, version):
+        self.lanes = {"4.x": 4, "3.x": 0}[version]
+
+    def __enter__(self):
+        self.prev = lib().orc_resize_simd()
+        lib().orc_set_resize_simd(self.lanes)
+        return self
+
+    def __exit__(self, *exc):
+        lib().orc_set_resize_simd(self.prev)
+        return False
 
 
 def cubic_tables(s, d):

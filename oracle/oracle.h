@@ -46,6 +46,10 @@ void orc_resize_cubic(float* dst, const float* src, int sh, int sw, int dh, int 
 /* multi-scale: resizeAndMergeBase.cpp:55-106 (each source to the full target, sum, average) */
 void orc_resize_merge(float* dst, const float* const* srcs, int nsrc, int channels,
                       const int* src_hw /* nsrc*2 */, int dh, int dw);
+/* vertical-pass summation order: lanes = 4 restates OpenCV 4.x's SIMD kernel (default), 0 the
+ * left-to-right order of OpenCV 3.x (see resize.c) */
+void orc_set_resize_simd(int lanes);
+int orc_resize_simd(void);
 /* the tables the cubic resize uses (for kernel cross-checks) */
 void orc_cubic_tables(int s, int d, int* ofs /* d */, float* coef /* d*4 */);
 

@@ -10,9 +10,20 @@
  *   t = f - s0;  taps s0-1 .. s0+2 clamped to the image (BORDER_REPLICATE);
  *   coefficients: Keys cubic with A = -0.75 (interpolateCubic);
  *   horizontal pass first (one row buffer per source row), then vertical.
- * Summation order: taps left to right (t0 + t1) + t2) + t3, horizontal then vertical.  OpenCV's
- * SSE vertical kernel may sum in a different order (<= 2 ulp difference): parity with OpenCV
- * itself is therefore unpinned; the HIP kernel matches THIS restatement bit for bit.
+ * Summation order (the source of every last-bit difference between OpenCV builds):
+ *   horizontal pass (HResizeCubic, scalar in every version): ((S[x0-1]a0 + S[x0]a1) + S[x0+1]a2)
+ *     + S[x0+2]a3, starting from 0 at the replicate-clamped border columns (0 + t0 == t0);
+ *   vertical pass (VResizeCubic<float,...,VResizeCubicVec_32f>): OpenCV 4.x (the reference's CI:
+ *     Ubuntu 20.04 libopencv-dev 4.2, Windows 4.5) writes the SIMD part with universal intrinsics,
+ *       dst[x] = v_fma(S0, b0, v_fma(S1, b1, v_fma(S2, b2, S3 * b3)))
+ *     for x < width rounded down to the vector width, and the scalar tail
+ *       dst[x] = S0*b0 + S1*b1 + S2*b2 + S3*b3   (left to right);
+ *     on the SSE2/SSE3 x86-64 baseline (no FMA3) v_fma is _mm_add_ps(_mm_mul_ps(a, b), c) and the
+ *     vector width is 4 floats, so the body sums S0b0 + (S1b1 + (S2b2 + S3b3)) in float.  OpenCV
+ *     3.x (Ubuntu 18.04's 3.2) used an SSE kernel that sums left to right everywhere.
+ *   orc_set_resize_simd(4) (the default) restates 4.x; orc_set_resize_simd(0) restates 3.x.
+ * Parity with OpenCV itself stays unpinned (OpenCV is absent); the HIP kernels follow the 4.x
+ * order (kernels/heat_dev.h, resize.hip, nms.hip) and match THIS restatement bit for bit.
  */
 #include <math.h>
 #include <stdlib.h>
@@ -42,6 +53,27 @@ void orc_cubic_tables(int s, int d, int* ofs, float* coef)
 
 static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
 
+/* vector width of OpenCV's vertical SIMD kernel: 4 (4.x on the x86-64 SSE baseline), 0 (3.x) */
+static int g_simd = 4;
+void orc_set_resize_simd(int lanes) { g_simd = lanes; }
+int orc_resize_simd(void) { return g_simd; }
+
+/* VResizeCubic for one output row of width dw */
+static void vresize_cubic(float* o, const float* r0, const float* r1, const float* r2,
+                          const float* r3, const float* be, int dw)
+{
+    const int vec_end = g_simd > 0 ? dw - dw % g_simd : 0;   /* whole vectors */
+    int x = 0;
+    for (; x < vec_end; ++x) {   /* v_fma nesting, each a mul then an add */
+        const float t3 = r3[x] * be[3];
+        const float t2 = r2[x] * be[2] + t3;
+        const float t1 = r1[x] * be[1] + t2;
+        o[x] = r0[x] * be[0] + t1;
+    }
+    for (; x < dw; ++x)   /* scalar tail (all of the row for 3.x) */
+        o[x] = r0[x] * be[0] + r1[x] * be[1] + r2[x] * be[2] + r3[x] * be[3];
+}
+
 void orc_resize_cubic(float* dst, const float* src, int sh, int sw, int dh, int dw)
 {
     int* xo = (int*)malloc(sizeof(int) * dw);
@@ -62,11 +94,8 @@ void orc_resize_cubic(float* dst, const float* src, int sh, int sw, int dh, int 
                      + srow[clampi(b + 2, 0, sw - 1)] * a[2] + srow[clampi(b + 3, 0, sw - 1)] * a[3];
             }
         }
-        const float* be = yb + 4 * y;
-        float* o = dst + (long)y * dw;
-        for (int x = 0; x < dw; ++x)
-            o[x] = rows[x] * be[0] + rows[dw + x] * be[1] + rows[2 * dw + x] * be[2]
-                 + rows[3 * dw + x] * be[3];
+        vresize_cubic(dst + (long)y * dw, rows, rows + dw, rows + 2 * dw, rows + 3 * dw, yb + 4 * y,
+                      dw);
     }
     free(xo); free(yo); free(xa); free(yb); free(rows);
 }

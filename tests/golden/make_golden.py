@@ -155,8 +155,15 @@ def make_resize():
     out = oracle.resize_merge([src], 80, 160)
     srcs = [rng.normal(0, 0.5, (2, h, w)).astype(np.float32) for h, w in [(10, 20), (7, 15), (5, 10)]]
     merged = oracle.resize_merge(srcs, 80, 160)
+    # a target width that is not a multiple of OpenCV's 4-float vertical SIMD vector (2 tail
+    # columns summed left to right), and the OpenCV 3.x order for comparison (resize.c)
+    rsrc = rng.normal(0, 0.5, (2, 9, 21)).astype(np.float32)
+    rout = oracle.resize_merge([rsrc], 72, 166)
+    with oracle.resize_order("3.x"):
+        out3 = oracle.resize_merge([src], 80, 160)
     np.savez_compressed(os.path.join(HERE, "resize.npz"), src=src, out=out,
-                        ms_src0=srcs[0], ms_src1=srcs[1], ms_src2=srcs[2], ms_out=merged)
+                        ms_src0=srcs[0], ms_src1=srcs[1], ms_src2=srcs[2], ms_out=merged,
+                        ragged_src=rsrc, ragged_out=rout, out_opencv3=out3)
 
 
 def make_cnn():

@@ -63,6 +63,23 @@ def test_resize_fixture():
     np.testing.assert_array_equal(oracle.resize_merge([g["src"]], 80, 160), g["out"])
     ms = oracle.resize_merge([g["ms_src0"], g["ms_src1"], g["ms_src2"]], 80, 160)
     np.testing.assert_array_equal(ms, g["ms_out"])
+    np.testing.assert_array_equal(oracle.resize_merge([g["ragged_src"]], 72, 166), g["ragged_out"])
+    with oracle.resize_order("3.x"):
+        np.testing.assert_array_equal(oracle.resize_merge([g["src"]], 80, 160), g["out_opencv3"])
+
+
+def test_resize_orders_differ_only_in_the_vertical_sum():
+    """OpenCV 4.x (SIMD body h0b0 + (h1b1 + (h2b2 + h3b3))) and 3.x (left to right) agree to a few
+    ulp, differ somewhere in the last bits, and agree exactly on the 4.x scalar tail columns."""
+    g = _load(os.path.join(GOLDEN, "resize.npz"))
+    a, b = g["out"], g["out_opencv3"]
+    assert not np.array_equal(a, b)
+    np.testing.assert_allclose(a, b, rtol=0, atol=4 * np.finfo(np.float32).eps * np.abs(a).max())
+    src = g["ragged_src"]
+    four = g["ragged_out"]
+    with oracle.resize_order("3.x"):
+        three = oracle.resize_merge([src], 72, 166)
+    np.testing.assert_array_equal(four[..., 164:], three[..., 164:])   # 166 % 4 == 2 tail columns
 
 
 def test_cnn_fixture():
