@@ -184,7 +184,8 @@ int opk_cvmat_to_input(opk_ctx* ctx, float* input_dev, const uint8_t* frames_dev
 
 /* Kernel-variant switches (no reference counterpart; A/B tests and tuning only): key = one of
  * "CONV3_SMALL", "CONV3_W16", "CONV3_PERSIST", "CONV3_WIDE", "CONV3P_ASMR", "CONV3P_WIDE",
- * "CONV3P_PRIO", "CONV1_TILE", "CONV1_N64W16", "CONV1_FUSED" (read when a launch is planned);
+ * "CONV3P_PRIO", "CONV3W", "CONV1_TILE", "CONV1_N64W16", "CONV1_FUSED" (read when a launch is
+ * planned);
  * reset != 0 removes the key (back to the product default).  Process-wide; the environment is
  * never consulted. */
 int opk_dev_set(const char* key, int value, int reset);

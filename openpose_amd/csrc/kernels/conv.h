@@ -60,6 +60,10 @@ struct Conv3Shape {
 };
 Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border = 1);
 void launch_conv3(const ConvArgs& a, hipStream_t stream);
+// conv3w.hip: the persistent 512 x {128, 96} 3x3 variant with one mid-unit barrier per K unit
+// (launched by launch_conv3 for single-n-block layers on the persistent path)
+bool conv3w_supported(const ConvArgs& a);
+void launch_conv3w(const ConvArgs& a, hipStream_t stream);
 
 // First conv (3 input channels, 3x3, cout <= 64) straight from the fp32 NCHW input [frames][3][H][W]
 // (conv_image.hip); weights [cout_pad][64], K order (ky*3 + kx)*3 + ci.

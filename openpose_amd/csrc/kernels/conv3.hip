@@ -32,23 +32,13 @@
 #include <cstdlib>
 
 #include "../common.h"
+#include "conv3_dev.h"
 
 namespace opk {
 
 namespace {
 
-typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
-typedef float float4_t __attribute__((ext_vector_type(4)));
-typedef float float2_t __attribute__((ext_vector_type(2)));
-typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ int swz64(int row, int piece) { return row * 4 + (piece ^ (((row >> 2) & 1) << 1)); }
-
-__device__ __forceinline__ uint16_t f2h_bits3(float v)
-{
-    const _Float16 h = (_Float16)v;
-    return __builtin_bit_cast(uint16_t, h);
-}
+using namespace conv3dev;
 
 #ifndef OPK3_ABLATE
 #define OPK3_ABLATE 0
@@ -68,85 +58,6 @@ __device__ unsigned long long* opk3_stamps;
 #define OPK3_STAMP(k_) do {} while (0)
 #endif
 
-template <int N>
-__device__ __forceinline__ void vm_wait()
-{
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (0..15)
-__device__ __forceinline__ void vm_wait_rt(int n)
-{
-    switch (n) {
-    case 0: vm_wait<0>(); break;
-    case 1: vm_wait<1>(); break;
-    case 2: vm_wait<2>(); break;
-    case 3: vm_wait<3>(); break;
-    case 4: vm_wait<4>(); break;
-    case 5: vm_wait<5>(); break;
-    case 6: vm_wait<6>(); break;
-    case 7: vm_wait<7>(); break;
-    case 8: vm_wait<8>(); break;
-    case 9: vm_wait<9>(); break;
-    case 10: vm_wait<10>(); break;
-    case 11: vm_wait<11>(); break;
-    case 12: vm_wait<12>(); break;
-    case 13: vm_wait<13>(); break;
-    case 14: vm_wait<14>(); break;
-    case 15: vm_wait<15>(); break;
-    default: vm_wait<0>(); break;
-    }
-}
-
-// n / d for 0 <= n < 2^24, 0 < d (float reciprocal estimate, then one correction step): a few VALU
-// instead of the ~40-instruction integer division sequence
-__device__ __forceinline__ int fdiv(int n, int d, float rd)
-{
-    int q = (int)((float)n * rd);
-    const int r = n - q * d;
-    q += (r >= d) ? 1 : 0;
-    q -= (r < 0) ? 1 : 0;
-    return q;
-}
-
-// virtual-image geometry (see the header comment)
-// B = the zero border of every activation buffer of the net (1 for BODY_25; the pad of its widest
-// convolution in general, 3 for the 7x7 stages of COCO / MPI / face / hand)
-struct Strips {
-    int H, B, Hp, Wp, sw, VW, nstrips, fposV, total;
-    float rf, rv, rs;   // reciprocals of fposV, VW, nstrips
-    __device__ Strips(const ConvArgs& a)
-        : H(a.H), B(a.border), Hp(a.H + 2 * a.border), Wp(a.W + 2 * a.border), sw(a.sw),
-          VW(a.sw + 2 * a.border), nstrips(a.nstrips), fposV((a.H + 2 * a.border) * (a.sw + 2 * a.border)),
-          total(a.frames * a.nstrips * (a.H + 2 * a.border) * (a.sw + 2 * a.border)),
-          rf(a.rcp[0]), rv(a.rcp[1]), rs(a.rcp[2])
-    {
-    }
-    // virtual position (yy, xx) of strip s is an output pixel of the image
-    __device__ bool interior(int yy, int xx, int s, int W) const
-    {
-        return yy >= B && yy < H + B && xx >= B && xx < sw + B && s * sw + xx - B < W;
-    }
-    // padded-image position of virtual position v (any v; outside the image -> -1, a zeroed guard)
-    template <bool FAST = true>
-    __device__ long map(int v, int& f, int& yy, int& xx, int& s) const
-    {
-        if (v < 0 || v >= total) {
-            f = 0;
-            yy = -1;
-            xx = -1;
-            s = 0;
-            return -1;
-        }
-        const int vf = FAST ? fdiv(v, fposV, rf) : v / fposV;
-        const int rem = v - vf * fposV;
-        yy = FAST ? fdiv(rem, VW, rv) : rem / VW;
-        xx = rem - yy * VW;
-        f = FAST ? fdiv(vf, nstrips, rs) : vf / nstrips;
-        s = vf - f * nstrips;
-        return (long)(f * Hp + yy) * Wp + s * sw + xx;
-    }
-};
 
 // TAPU: taps per K unit (3 = one ky row of taps, 1 = a single tap); MINB: workgroups per CU the
 // LDS budget allows (2 -> 80 KB: the other workgroup's MFMAs cover this one's prologue, barrier
@@ -444,27 +355,6 @@ void conv3_kernel(const ConvArgs a)
 // must know how many stores an epilogue issued: every (fragment pair, destination) issues exactly
 // one 16-byte store, plus one 8-byte store per odd last fragment (lanes of border positions write
 // to a scratch "sink"), S = MF*(NF/2 + NF%2)*ndst.
-#define OPK3_VM_CASE(n_) case n_: vm_wait<n_>(); break;
-__device__ __forceinline__ void vm_wait_rt64(int n)
-{
-    switch (n) {
-        OPK3_VM_CASE(0) OPK3_VM_CASE(1) OPK3_VM_CASE(2) OPK3_VM_CASE(3) OPK3_VM_CASE(4)
-        OPK3_VM_CASE(5) OPK3_VM_CASE(6) OPK3_VM_CASE(7) OPK3_VM_CASE(8) OPK3_VM_CASE(9)
-        OPK3_VM_CASE(10) OPK3_VM_CASE(11) OPK3_VM_CASE(12) OPK3_VM_CASE(13) OPK3_VM_CASE(14)
-        OPK3_VM_CASE(15) OPK3_VM_CASE(16) OPK3_VM_CASE(17) OPK3_VM_CASE(18) OPK3_VM_CASE(19)
-        OPK3_VM_CASE(20) OPK3_VM_CASE(21) OPK3_VM_CASE(22) OPK3_VM_CASE(23) OPK3_VM_CASE(24)
-        OPK3_VM_CASE(25) OPK3_VM_CASE(26) OPK3_VM_CASE(27) OPK3_VM_CASE(28) OPK3_VM_CASE(29)
-        OPK3_VM_CASE(30) OPK3_VM_CASE(31) OPK3_VM_CASE(32) OPK3_VM_CASE(33) OPK3_VM_CASE(34)
-        OPK3_VM_CASE(35) OPK3_VM_CASE(36) OPK3_VM_CASE(37) OPK3_VM_CASE(38) OPK3_VM_CASE(39)
-        OPK3_VM_CASE(40) OPK3_VM_CASE(41) OPK3_VM_CASE(42) OPK3_VM_CASE(43) OPK3_VM_CASE(44)
-        OPK3_VM_CASE(45) OPK3_VM_CASE(46) OPK3_VM_CASE(47) OPK3_VM_CASE(48) OPK3_VM_CASE(49)
-        OPK3_VM_CASE(50) OPK3_VM_CASE(51) OPK3_VM_CASE(52) OPK3_VM_CASE(53) OPK3_VM_CASE(54)
-        OPK3_VM_CASE(55) OPK3_VM_CASE(56) OPK3_VM_CASE(57) OPK3_VM_CASE(58) OPK3_VM_CASE(59)
-        OPK3_VM_CASE(60) OPK3_VM_CASE(61) OPK3_VM_CASE(62) OPK3_VM_CASE(63)
-    default: vm_wait<0>(); break;
-    }
-}
-#undef OPK3_VM_CASE
 
 constexpr int kP_BM = 512, kP_HR = 688, kP_NW = 16;
 
@@ -880,6 +770,11 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
         bool aligned = true;
         // 16-byte stores of 8-channel groups
         for (int d = 0; d < a.ndst; ++d) aligned = aligned && ((a.dst_coff[d] | a.dst_cs[d]) & 7) == 0;
+        // mid-unit-barrier schedule (conv3w.hip, bit-identical; CONV3W=0: conv3p_kernel)
+        if (aligned && nn == 1 && dev_switch("CONV3W", 1) != 0 && conv3w_supported(a)) {
+            launch_conv3w(a, stream);
+            return;
+        }
         if (aligned) {   // one workgroup per CU, n-blocks spread evenly over the grid
             const long per_n = std::min<long>(a.cus / nn, (ntiles + nn - 1) / nn);
             const unsigned G = (unsigned)(per_n * nn);

@@ -206,10 +206,11 @@ def test_7x7_cpm_stages_vs_oracle(ctx, concat, hw):
     assert got.shape == ref.shape and err < SMALL_TOL
 
 
-VARIANTS = {"persistent": {}, "w16": {"CONV3_PERSIST": 0},
+VARIANTS = {"persistent": {}, "persistent_conv3p": {"CONV3W": 0}, "w16": {"CONV3_PERSIST": 0},
             "w8": {"CONV3_W16": 0, "CONV1_TILE": 0}, "w8_one_per_cu": {"CONV3_W16": 0, "CONV3_SMALL": 0},
-            "persistent_compiler_frags": {"CONV3P_ASMR": 0}, "persistent_dwordx2": {"CONV3P_WIDE": 0},
-            "dwordx2": {"CONV3P_WIDE": 0, "CONV3_WIDE": 0},
+            "persistent_compiler_frags": {"CONV3W": 0, "CONV3P_ASMR": 0},
+            "persistent_dwordx2": {"CONV3W": 0, "CONV3P_WIDE": 0},
+            "dwordx2": {"CONV3W": 0, "CONV3P_WIDE": 0, "CONV3_WIDE": 0},
             "w16_dwordx2": {"CONV3_PERSIST": 0, "CONV3_WIDE": 0},
             "conv1_512x128": {"CONV1_TILE": 1}, "conv1_256x256": {"CONV1_TILE": 2},
             "conv1_512x64": {"CONV1_N64W16": 1}}
