@@ -156,6 +156,29 @@ int opk_keep_top_n_people(const float* keypoints_host, int people, int parts,
                           const float* scores_host, int max_people, float* out_keypoints_host,
                           int* out_index_host, int* out_people);
 
+/* ---- People JSON (--write_json).  One keypoint array of the reference's keypointVector
+ * (WPeopleJsonSaver::workConsumer, include/openpose/filestream/wPeopleJsonSaver.hpp:75-88):
+ * name ("person_id", "pose_keypoints_2d", ...), ndims 0 (empty op::Array), 1 ([people], e.g. the
+ * person ids as float) or 3 ([people][parts][dims]); host data. */
+typedef struct opk_json_keypoints {
+    const char* name;
+    const float* data;
+    int ndims, people, parts, dims;
+} opk_json_keypoints;
+/* opk_people_json replaces op::savePeopleJson(keypointVector, candidates, fileName, humanReadable)
+ * (src/openpose/filestream/fileStream.cpp:306-344, JsonOfstream formatting): writes the file's text
+ * (no terminating NUL counted) into out_host when *len + 1 <= capacity (out_host may be NULL to
+ * query), *len = its length.  candidates_host: n_parts lists of [x, y, score] back to back,
+ * candidate_counts_host[part] each (the Datum's poseCandidates; n_parts 0 = none, no
+ * "part_candidates" key).  opk_save_people_json writes the same text to path (PeopleJsonSaver::save,
+ * peopleJsonSaver.cpp:15-30, with the ".json" already in path). */
+int opk_people_json(const opk_json_keypoints* arrays, int n_arrays, const float* candidates_host,
+                    const int* candidate_counts_host, int n_parts, int human_readable,
+                    char* out_host, size_t capacity, size_t* len);
+int opk_save_people_json(const char* path, const opk_json_keypoints* arrays, int n_arrays,
+                         const float* candidates_host, const int* candidate_counts_host,
+                         int n_parts, int human_readable);
+
 /* Pose tables (getPoseNumberBodyParts, addBkgChannel, getPosePartPairs, getPoseMapIndex;
  * poseParameters.hpp:17-34).  Any output pointer may be NULL; pairs gets 2*npairs entries,
  * map_idx the model's map-index entries (heat_channels - parts - bkg). */

@@ -82,6 +82,8 @@ _SIGS = {
     "opk_pose_candidates": (_i, [_p, _i, _p, _ip]),
     "opk_scale_keypoints": (_i, [_p, _i, _i, _i, _d, _d, _i, _i]),
     "opk_keep_top_n_people": (_i, [_p, _i, _i, _p, _i, _p, _p, _ip]),
+    "opk_people_json": (_i, [_p, _i, _p, _p, _i, _i, _p, ctypes.c_size_t, _p]),
+    "opk_save_people_json": (_i, [ctypes.c_char_p, _p, _i, _p, _p, _i, _i]),
     "opk_face_detect": (_i, [_i, _p, _i, _i, _p]),
     "opk_hand_detect": (_i, [_i, _p, _i, _i, _p]),
     "opk_extractor_create": (_i, [_p, _p, _i, _i, _i, _c.POINTER(_p)]),

@@ -191,6 +191,70 @@ def keep_top_n_people(keypoints, scores, max_people):
     return out[:n.value], idx[:n.value]
 
 
+class _JsonKeypoints(ctypes.Structure):
+    _fields_ = [("name", ctypes.c_char_p), ("data", ctypes.c_void_p), ("ndims", ctypes.c_int),
+                ("people", ctypes.c_int), ("parts", ctypes.c_int), ("dims", ctypes.c_int)]
+
+
+def _json_args(keypoint_vector, candidates):
+    keep = []
+    arr = (_JsonKeypoints * max(len(keypoint_vector), 1))()
+    for i, (a, name) in enumerate(keypoint_vector):
+        a = np.ascontiguousarray(a if a is not None else np.zeros(0), np.float32)
+        keep.append(a)
+        shape = a.shape if a.size else ()
+        if len(shape) not in (0, 1, 3):
+            shape = (None,) * 2   # rejected by the library like the reference
+        dims = list(shape) + [0] * (3 - len(shape))
+        arr[i] = _JsonKeypoints(name.encode(), a.ctypes.data if a.size else None, len(shape),
+                                dims[0] or 0, dims[1] or 0, dims[2] or 0)
+    cands = candidates or []
+    counts = np.array([len(c) for c in cands], np.int32)
+    flat = np.ascontiguousarray(
+        np.concatenate([np.asarray(c, np.float32).reshape(-1, 3) for c in cands])
+        if cands and counts.sum() else np.zeros((0, 3)), np.float32)
+    keep += [counts, flat]
+    return arr, keep, (flat.ctypes.data if flat.size else None,
+                       counts.ctypes.data if counts.size else None, len(cands))
+
+
+def people_json(keypoint_vector, candidates=None, human_readable=False):
+    """op::savePeopleJson's file text (fileStream.cpp:306-344) for keypoint_vector = [(array, name)]
+    (arrays [people][parts][3], [people] or empty) and candidates = per-part lists of [x, y, score]."""
+    L = _lib.load()
+    arr, keep, (cp, cc, nparts) = _json_args(keypoint_vector, candidates)
+    n = ctypes.c_size_t()
+    check(L.opk_people_json(arr, len(keypoint_vector), cp, cc, nparts, int(human_readable), None,
+                            0, ctypes.byref(n)))
+    buf = ctypes.create_string_buffer(n.value + 1)
+    check(L.opk_people_json(arr, len(keypoint_vector), cp, cc, nparts, int(human_readable), buf,
+                            n.value + 1, ctypes.byref(n)))
+    del keep
+    return buf.raw[:n.value].decode()
+
+
+def save_people_json(path, keypoint_vector, candidates=None, human_readable=False):
+    """PeopleJsonSaver::save (peopleJsonSaver.cpp:15-30): the same text written to path."""
+    L = _lib.load()
+    arr, keep, (cp, cc, nparts) = _json_args(keypoint_vector, candidates)
+    check(L.opk_save_people_json(path.encode(), arr, len(keypoint_vector), cp, cc, nparts,
+                                 int(human_readable)))
+    del keep
+
+
+def datum_keypoint_vector(pose_keypoints, face_keypoints=None, hand_keypoints=(None, None)):
+    """The keypointVector WPeopleJsonSaver builds from a Datum (wPeopleJsonSaver.hpp:75-88):
+    person ids (-1 each without a person-id extractor, PoseExtractor::extractIds,
+    poseExtractor.cpp:136-151), the 2-D body / face / hand arrays and the (empty) 3-D ones."""
+    pk = np.asarray(pose_keypoints, np.float32)
+    ids = np.full(pk.shape[0], -1, np.float32) if pk.size else None
+    return [(ids, "person_id"), (pk, "pose_keypoints_2d"), (face_keypoints, "face_keypoints_2d"),
+            (hand_keypoints[0], "hand_left_keypoints_2d"),
+            (hand_keypoints[1], "hand_right_keypoints_2d"), (None, "pose_keypoints_3d"),
+            (None, "face_keypoints_3d"), (None, "hand_left_keypoints_3d"),
+            (None, "hand_right_keypoints_3d")]
+
+
 def caffemodel_blob(path, layer, index):
     """Host utility: (shape, float32 data) of a blob in a .caffemodel (opk_caffemodel_blob)."""
     L = _lib.load()

@@ -7,6 +7,7 @@
 #include "../../../include/opk.h"
 #include "connector.h"
 #include "context.h"
+#include "json.h"
 #include "output.h"
 
 namespace opk {
@@ -340,6 +341,34 @@ int opk_keep_top_n_people(const float* keypoints_host, int people, int parts,
         const int n = opk::keep_top_n_people(keypoints_host, people, parts, scores_host, max_people,
                                              out_keypoints_host, out_index_host);
         if (out_people) *out_people = n;
+    });
+}
+
+int opk_people_json(const opk_json_keypoints* arrays, int n_arrays, const float* candidates_host,
+                    const int* candidate_counts_host, int n_parts, int human_readable,
+                    char* out_host, size_t capacity, size_t* len)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(len != nullptr, "opk_people_json: NULL len");
+        const std::string t = opk::people_json(arrays, n_arrays, candidates_host,
+                                               candidate_counts_host, n_parts, human_readable != 0);
+        *len = t.size();
+        if (out_host) {
+            OPK_CHECK_ARG(capacity >= t.size() + 1, "opk_people_json: buffer too small");
+            std::memcpy(out_host, t.c_str(), t.size() + 1);
+        }
+    });
+}
+
+int opk_save_people_json(const char* path, const opk_json_keypoints* arrays, int n_arrays,
+                         const float* candidates_host, const int* candidate_counts_host,
+                         int n_parts, int human_readable)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(path != nullptr, "opk_save_people_json: NULL path");
+        opk::save_people_json(path, opk::people_json(arrays, n_arrays, candidates_host,
+                                                     candidate_counts_host, n_parts,
+                                                     human_readable != 0));
     });
 }
 

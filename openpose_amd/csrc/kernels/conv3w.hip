@@ -61,6 +61,22 @@ __device__ unsigned long long* opkw_stamps;
 #define OPKW_RTSTAMP(k_) do {} while (0)
 #endif
 
+#ifndef OPKW_STORE_MODE   // dev probe: 0 plain epilogue stores, 1 non-temporal
+#define OPKW_STORE_MODE 0
+#endif
+typedef unsigned int opkw_u4 __attribute__((ext_vector_type(4)));
+typedef unsigned int opkw_u2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void opkw_st(uint4* p, const uint4& v)
+{
+    if (OPKW_STORE_MODE == 1) __builtin_nontemporal_store((opkw_u4){v.x, v.y, v.z, v.w}, reinterpret_cast<opkw_u4*>(p));
+    else *p = v;
+}
+__device__ __forceinline__ void opkw_st(uint2* p, const uint2& v)
+{
+    if (OPKW_STORE_MODE == 1) __builtin_nontemporal_store((opkw_u2){v.x, v.y}, reinterpret_cast<opkw_u2*>(p));
+    else *p = v;
+}
+
 #define OPKW_DSR(dst_, addr_, off_)                                                           \
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst_) : "v"(addr_), "i"(off_))
 
@@ -350,16 +366,19 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
         const int nd = a.ndst;
         uint16_t* const d0 = a.dst[0] + a.dst_coff[0];
         const int cs0 = a.dst_cs[0];
+#ifndef OPKW_SINK_ONLY   // dev probe: every store to the sink (tile-transition store-burst test)
+#define OPKW_SINK_ONLY 0
+#endif
 #define OPKW_STORE(T_, sink_, ch_, i_, val_)                                                  \
     do {                                                                                      \
         if (nd == 1) {                                                                        \
             T_* p_ = reinterpret_cast<T_*>(d0 + (ch_) + (size_t)prow[i_] * cs0);              \
-            *(pok[i_] ? p_ : sink_) = val_;                                                   \
+            opkw_st(pok[i_] && !OPKW_SINK_ONLY ? p_ : sink_, val_);                           \
         } else {                                                                              \
             for (int d_ = 0; d_ < nd; ++d_) {                                                 \
                 T_* p_ = reinterpret_cast<T_*>(a.dst[d_] + a.dst_coff[d_] + (ch_) +           \
                                                (size_t)prow[i_] * a.dst_cs[d_]);              \
-                *(pok[i_] ? p_ : sink_) = val_;                                               \
+                opkw_st(pok[i_] ? p_ : sink_, val_);                                          \
             }                                                                                 \
         }                                                                                     \
     } while (0)

@@ -6,6 +6,8 @@ numpy restatements, in float32 arithmetic, of:
   KeypointScaler::scale                 src/openpose/core/keypointScaler.cpp:6-95
   KeepTopNPeople::keepTopPeople         src/openpose/core/keepTopNPeople.cpp:16-86
   getKeypointsRectangle / Area          src/openpose/utilities/keypoint.cpp:289-389
+  savePeopleJson (+ addKeypointsToJson,  src/openpose/filestream/fileStream.cpp:20-130,306-344,
+    addCandidatesToJson, JsonOfstream)   src/openpose/filestream/jsonOfstream.cpp
 Parity unpinned for keypoint.cpp-based code (it includes OpenCV, absent here); the others are
 plain float code restated line by line.
 """
@@ -144,3 +146,98 @@ def keep_top_n_people(kp, scores, max_people):
                 out[len(idx)] = kp[p]
                 idx.append(p)
     return out, np.array(idx)
+
+
+# ---- savePeopleJson ------------------------------------------------------------------------
+def _fmt(v):
+    """std::ostream << float with the default format (precision 6, %g) -- jsonOfstream.hpp:40-44."""
+    return "%g" % float(f32(v))
+
+
+def people_json(keypoint_vector, candidates=None, human_readable=False):
+    """op::savePeopleJson's file text.  keypoint_vector: [(array or None, name)], arrays of 1 or
+    3 dimensions; op::Array::getSize (array.cpp:421-437): missing dimensions count 1, empty 0."""
+    out = []
+    braces = brackets = 0
+
+    def enter():
+        if human_readable:
+            out.append("\n" + "\t" * (braces + brackets))
+
+    def size(a, i):
+        if a is None or np.asarray(a).size == 0:
+            return 0
+        a = np.asarray(a)
+        return a.shape[i] if i < a.ndim else 1
+
+    braces += 1
+    out.append("{")                                    # objectOpen
+    enter()
+    out.append('"version":')                           # version("1.3")
+    out.append("1.3")
+    out.append(",")
+    enter()
+    out.append('"people":')                            # addKeypointsToJson
+    brackets += 1
+    out.append("[")
+    enter()
+    people = max([size(a, 0) for a, _ in keypoint_vector] + [0])
+    for p in range(people):
+        braces += 1
+        out.append("{")
+        for v, (a, name) in enumerate(keypoint_vector):
+            per_row = size(a, 1) * size(a, 2)
+            enter()
+            out.append('"%s":' % name)
+            brackets += 1
+            out.append("[")
+            enter()
+            if per_row > 0:
+                row = np.asarray(a, f32).reshape(-1)[p * per_row:(p + 1) * per_row]
+                out.append(",".join(_fmt(x) for x in row))
+            brackets -= 1
+            enter()
+            out.append("]")
+            if v < len(keypoint_vector) - 1:
+                out.append(",")
+        braces -= 1
+        enter()
+        out.append("}")
+        if p < people - 1:
+            out.append(",")
+            enter()
+    brackets -= 1
+    enter()
+    out.append("]")
+    if candidates:                                      # addCandidatesToJson
+        out.append(",")
+        enter()
+        out.append('"part_candidates":')
+        brackets += 1
+        out.append("[")
+        enter()
+        braces += 1
+        out.append("{")
+        for part, cl in enumerate(candidates):
+            enter()
+            out.append('"%d":' % part)
+            brackets += 1
+            out.append("[")
+            enter()
+            out.append(",".join(_fmt(x) for c in cl for x in c[:3]))
+            brackets -= 1
+            enter()
+            out.append("]")
+            if part < len(candidates) - 1:
+                out.append(",")
+        braces -= 1
+        enter()
+        out.append("}")
+        brackets -= 1
+        enter()
+        out.append("]")
+    braces -= 1
+    enter()
+    out.append("}")
+    enter()                                             # ~JsonOfstream
+    return "".join(out)

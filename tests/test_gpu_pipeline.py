@@ -131,6 +131,73 @@ def test_end_to_end_keypoints_within_tolerance(ctx):
         assert np.abs(ks - rs).max() <= KEYPOINT_TOL
 
 
+def _peak_drift(ref_peaks, got_peaks, radius=1.0):
+    """Fraction of the reference peaks with a peak of the same part within `radius` heat-map
+    pixels, and the largest such displacement."""
+    matched, total, worst = 0, 0, 0.0
+    for c in range(ref_peaks.shape[0]):
+        r = ref_peaks[c, 1:int(ref_peaks[c, 0, 0]) + 1, :2]
+        g = got_peaks[c, 1:int(got_peaks[c, 0, 0]) + 1, :2]
+        total += len(r)
+        if len(r) == 0 or len(g) == 0:
+            continue
+        d = np.sqrt(((r[:, None, :] - g[None, :, :]) ** 2).sum(-1)).min(1)
+        ok = d <= radius
+        matched += int(ok.sum())
+        if ok.any():
+            worst = max(worst, float(d[ok].max()))
+    return (matched / total if total else 1.0), worst, total
+
+
+def test_end_to_end_unscaled_heads(ctx, record_property):
+    """Full-strength heads (out_scale 1, no overlay) at 656x368, one frame.
+
+    (1) post-processing isolated: the oracle's resize -> NMS -> connector run on the GPU's OWN net
+        output must give the GPU pipeline's peaks and keypoints bit for bit;
+    (2) fp16-vs-fp32 CNN drift, measured: the same chain on the fp32 oracle net output; the
+        fraction of fp32 peaks reproduced within 1 heat-map pixel and the largest displacement
+        are recorded (record_property) and bounded loosely.
+    poseExtractorCaffe.cpp:246-333 is the chain both sides follow."""
+    graph = body25.layers()
+    params = synth.he_weights(graph, seed=31, out_scale=1.0)
+    x = np.random.default_rng(32).uniform(-0.5, 0.5, (1, 3, 368, 656)).astype(np.float32)
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(params)
+    pose = PoseExtractor(ctx, net)
+    pose.forward(_dev(x), (1280, 720))
+    s = pose.scale_net_to_output()
+    off = float(np.float32(0.5 / np.float64(s)))
+    gpu_out = net.output_numpy()[0]
+    gpu_peaks = pose.peaks_numpy()[0]
+    kp, ks = pose.keypoints(0)
+
+    heat = oracle.resize_merge([gpu_out], 368, 656)
+    peaks = oracle.nms(heat, 0.05, 128, (off, off))
+    rk, rs = oracle.connect(heat, peaks, scale=s)
+    for c in range(25):
+        n = int(peaks[c, 0, 0])
+        assert int(gpu_peaks[c, 0, 0]) == n
+        np.testing.assert_array_equal(gpu_peaks[c, 1:n + 1], peaks[c, 1:n + 1])
+    np.testing.assert_array_equal(kp, rk)
+    np.testing.assert_array_equal(ks, rs)
+
+    ref_out = body25.forward(x, params, graph=graph)[0]
+    err = float(np.linalg.norm(gpu_out - ref_out) / np.linalg.norm(ref_out))
+    heat32 = oracle.resize_merge([ref_out], 368, 656)
+    peaks32 = oracle.nms(heat32, 0.05, 128, (off, off))
+    frac, worst, total = _peak_drift(peaks32, gpu_peaks)
+    rk32, _ = oracle.connect(heat32, peaks32, scale=s)
+    record_property("net_rel_l2", err)
+    record_property("fp32_peaks", total)
+    record_property("peaks_within_1px", frac)
+    record_property("max_peak_shift_px", worst)
+    record_property("people_fp16_fp32", (len(kp), len(rk32)))
+    print("unscaled heads: rel-L2 %.2e, %d fp32 peaks, %.4f within 1 px (max shift %.3f px), "
+          "people %d vs %d" % (err, total, frac, worst, len(kp), len(rk32)))
+    assert err < 5e-3
+    assert total > 0 and frac >= 0.9
+
+
 def test_pose_submit_collect_pipeline(ctx):
     """Two batches in flight (opk_pose_submit / opk_pose_collect) give the synchronous results."""
     def fields(seed):

@@ -90,3 +90,60 @@ def test_gpu_heatmaps_copy_rejects_bkg_without_background(ctx):
     pose.forward_net_output(field, (96, 80), (96, 80))
     with pytest.raises(api._lib.OpkError, match="heatmaps_add_bkg"):
         pose.heatmaps_copy(2, 8)
+
+
+# ---- people JSON (--write_json): savePeopleJson, fileStream.cpp:306-344 ----------------------
+def test_people_json_known_answer():
+    """Hand-derived from the reference source: JsonOfstream writes `"key":` then the values through
+    std::ostream (%g); humanReadable = false in WPeopleJsonSaver (wPeopleJsonSaver.hpp:68)."""
+    kp = np.array([[[1.5, 2.0, 0.25], [0.0, 0.0, 0.0]]], np.float32)
+    text = api.people_json(api.datum_keypoint_vector(kp))
+    assert text == ('{"version":1.3,"people":[{"person_id":[-1],"pose_keypoints_2d":[1.5,2,0.25,0,0,0],'
+                    '"face_keypoints_2d":[],"hand_left_keypoints_2d":[],"hand_right_keypoints_2d":[],'
+                    '"pose_keypoints_3d":[],"face_keypoints_3d":[],"hand_left_keypoints_3d":[],'
+                    '"hand_right_keypoints_3d":[]}]}')
+    assert api.people_json([(None, "pose_keypoints_2d")]) == \
+        '{"version":1.3,"people":[]}'
+    cand = [[[10.0, 20.0, 0.5]], [], [[1e-7, 123456789.0, 1.0], [0.1, 0.2, 0.3]]]
+    assert api.people_json([(None, "pose_keypoints_2d")], cand) == \
+        ('{"version":1.3,"people":[],"part_candidates":[{"0":[10,20,0.5],"1":[],'
+         '"2":[1e-07,1.23457e+08,1,0.1,0.2,0.3]}]}')
+
+
+@pytest.mark.parametrize("human", [False, True])
+@pytest.mark.parametrize("seed", range(4))
+def test_people_json_matches_oracle(seed, human, tmp_path):
+    rng = np.random.default_rng(seed)
+    people = [0, 1, 3, 7][seed]
+    kp = rng.uniform(0, 1280, (people, 25, 3)).astype(np.float32)
+    kp[..., 2] = rng.uniform(0, 1, (people, 25))
+    kp[:, ::4] = 0                                        # parts not found
+    face = rng.uniform(-1, 1, (people, 70, 3)).astype(np.float32) if seed % 2 else None
+    hands = (rng.normal(0, 1e3, (people, 21, 3)).astype(np.float32), None)
+    vec = api.datum_keypoint_vector(kp, face, hands)
+    cand = ([[list(rng.uniform(0, 500, 3)) for _ in range(rng.integers(0, 4))] for _ in range(25)]
+            if seed >= 2 else None)
+    text = api.people_json(vec, cand, human_readable=human)
+    assert text == O.people_json(vec, cand, human_readable=human)
+    path = str(tmp_path / ("%d_keypoints.json" % seed))
+    api.save_people_json(path, vec, cand, human_readable=human)
+    with open(path) as f:
+        saved = f.read()
+    assert saved == text
+    if not human:
+        import json
+        d = json.loads(text)
+        assert d["version"] == 1.3 and len(d["people"]) == people
+        for p in range(people):
+            np.testing.assert_allclose(d["people"][p]["pose_keypoints_2d"], kp[p].reshape(-1),
+                                       rtol=1e-5)
+
+
+def test_people_json_rejects_bad_arrays():
+    with pytest.raises(api._lib.OpkError):    # getNumberDimensions() != 1 && != 3
+        api.people_json([(np.zeros((2, 3), np.float32), "pose_keypoints_2d")])
+    with pytest.raises(api._lib.OpkError):    # fewer people than the widest array
+        api.people_json([(np.zeros((3, 25, 3), np.float32), "a"),
+                         (np.zeros((2, 25, 3), np.float32), "b")])
+    with pytest.raises(api._lib.OpkError):
+        api.save_people_json("/nonexistent_dir/x.json", [(None, "pose_keypoints_2d")])
