@@ -64,6 +64,9 @@ void launch_conv3(const ConvArgs& a, hipStream_t stream);
 // (launched by launch_conv3 for single-n-block layers on the persistent path)
 bool conv3w_supported(const ConvArgs& a);
 void launch_conv3w(const ConvArgs& a, hipStream_t stream);
+// conv3w8.hip: the same tile with 8 waves of 64 x BN (fewer LDS fragment reads per MFMA)
+bool conv3w8_supported(const ConvArgs& a);
+void launch_conv3w8(const ConvArgs& a, hipStream_t stream);
 
 // First conv (3 input channels, 3x3, cout <= 64) straight from the fp32 NCHW input [frames][3][H][W]
 // (conv_image.hip); weights [cout_pad][64], K order (ky*3 + kx)*3 + ci.

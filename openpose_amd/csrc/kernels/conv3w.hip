@@ -77,8 +77,16 @@ __device__ __forceinline__ void opkw_st(uint2* p, const uint2& v)
     else *p = v;
 }
 
+#ifndef OPKW_ABLATE   // dev probe only (tools/conv3w_probe.hip): 1 no mid-unit barrier, 2 no MFMAs,
+#define OPKW_ABLATE 0  // 3 no fragment reads, 4 no DMA after the prologue (timing only, wrong results)
+#endif
+#if OPKW_ABLATE == 3
+#define OPKW_DSR(dst_, addr_, off_)                                                           \
+    asm volatile("; no read %1" : "=v"(dst_) : "v"(addr_))
+#else
 #define OPKW_DSR(dst_, addr_, off_)                                                           \
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst_) : "v"(addr_), "i"(off_))
+#endif
 
 // DMA_END (the default): issue unit u+2's DMA after tap 2 instead of right after the mid-unit
 // barrier -- fewer registers live at the issue point (no spills), two thirds of a unit less lead
@@ -227,7 +235,8 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
                 asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(cur_));                            \
             }                                                                                 \
             _Pragma("unroll") for (int j_ = 0; j_ < NF; ++j_)                                 \
-                acc[i_][j_] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j_], cur_, acc[i_][j_], 0, 0, 0); \
+                acc[i_][j_] = OPKW_ABLATE == 2 ? acc[i_][j_] + (float)cur_[j_]                  \
+                    : __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j_], cur_, acc[i_][j_], 0, 0, 0); \
             __builtin_amdgcn_sched_barrier(0);   /* keep the issue order as written */       \
         }                                                                                     \
         if (PF_) OPKW_READ_TAP0(nab_, nbb_, nboff_);                                          \
@@ -289,15 +298,15 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
 #ifdef OPKW_STAMPS
             if (tcount == 0 && u == 3) OPKW_STAMP(9);
 #endif
-            __builtin_amdgcn_s_barrier();
+            if (OPKW_ABLATE != 1) __builtin_amdgcn_s_barrier();
 #ifdef OPKW_STAMPS
             if (tcount == 0 && u == 3) OPKW_STAMP(10);
             if (tcount == 0 && u == 4) OPKW_STAMP(11);
             if (tcount == 1 && u == 0) OPKW_STAMP(12);
 #endif
-            if (!DMA_END) OPKW_DMA_U2();
+            if (!DMA_END && (OPKW_ABLATE != 4 || u + 2 >= U)) OPKW_DMA_U2();
             OPKW_TAP(ab2, ab2, bb_u, 0, false);
-            if (DMA_END) OPKW_DMA_U2();
+            if (DMA_END && (OPKW_ABLATE != 4 || u + 2 >= U)) OPKW_DMA_U2();
 #undef OPKW_DMA_U2
         }
 

@@ -1,0 +1,393 @@
+// conv3w8.hip -- 3x3 convolution: the persistent 512 x {128, 96} halo implicit GEMM of conv3w.hip
+// with 8 waves of 64 positions x ALL output channels instead of 16 waves of 64 x 64.
+//
+// Why: the conv3w K loop is bound by LDS fragment reads, not by the MFMAs or the barrier
+// (tools/conv3w_probe.hip ablations, 64 frames x 46x82, cin 384: 197 us as built, 194 without the
+// mid-unit barrier, 174 without MFMAs, 138 without fragment reads).  With 16 waves of 64 x 64 every
+// weight (B) fragment is read by 8 waves and every halo (A) fragment by 2: 8 ds_read_b128 per 16
+// MFMAs.  Here a wave owns 64 positions x BN channels (acc 128 VGPRs at 2 waves per SIMD): per tap
+// MF = 4 A + NF = 8 B fragments for 32 MFMAs, 25 % fewer LDS reads per MFMA, and the next tap's
+// B fragments stream in during taps 0 and 1 of a K unit (fbE / fbO alternate; tap 2 re-reads the
+// next unit's tap-0 B into fbE after its last MFMAs), the A fragments two steps ahead.
+//
+// Same tile, operands, LDS layout, K order and epilogue arithmetic as conv3w_kernel / conv3p_kernel,
+// so outputs are bit-identical to them.  Schedule per K unit u = (chunk c, tap row ky), as conv3w:
+//     tap 0, tap 1, [wait own DMA of unit u+1; s_barrier], tap 2, [issue DMA of unit u+2];
+// fragments of unit u+1 are read during tap 2 (certified by the mid-unit barrier).
+//
+// lgkmcnt: per tap, step i (position fragment i) issues A(t, i+2) (for i >= 2: the next tap's A
+// fragments 0 / 1) and, in taps 0 / 1, the next tap's B fragments 2i, 2i+1; the waits (kWait) are
+// counted from that fixed issue order (no other LDS traffic inside the K loop).
+#include "conv.h"
+
+#include <algorithm>
+
+#include "../common.h"
+#include "conv3_dev.h"
+
+namespace opk {
+
+namespace {
+
+using namespace conv3dev;
+
+constexpr int k8_BM = 512, k8_HR = 688, k8_NW = 8;
+
+#ifndef OPK8_ABLATE   // dev probe only (tools/conv3w_probe.hip): 1 no mid-unit barrier, 2 no MFMAs,
+#define OPK8_ABLATE 0  // 3 no fragment reads, 4 no DMA after the prologue (timing only, wrong results)
+#endif
+#if OPK8_ABLATE == 3
+#define OPK8_DSR(dst_, addr_, off_) asm volatile("; no read %1" : "=v"(dst_) : "v"(addr_))
+#else
+#define OPK8_DSR(dst_, addr_, off_)                                                           \
+    asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst_) : "v"(addr_), "i"(off_))
+#endif
+
+template <int BN>
+__global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a)
+{
+    constexpr int NW = k8_NW, BM = k8_BM, HR = k8_HR;
+    constexpr int WROWS = BM / NW, MF = WROWS / 16, NF = BN / 16;
+    static_assert(WROWS == 64 && (NF == 8 || NF == 6), "wave tiles 64 x 128 / 64 x 96");
+    constexpr int API = HR / 16, AIW = (API + NW - 1) / NW;
+    constexpr int BROWS = 3 * BN, BPI = BROWS / 16, BIW = (BPI + NW - 1) / NW;
+    constexpr int ASLOT = HR * 4, BSLOT = BROWS * 4;   // 16-byte pieces
+    constexpr int LDS_PIECES = 2 * ASLOT + 3 * BSLOT + BN / 2;
+    static_assert(LDS_PIECES * 16 <= 160 * 1024, "LDS budget");
+    // counted lgkmcnt waits of steps 0..3 per tap kind (-1: none needed), from the issue order
+    // (see OPK8_TAP): step 0 waits for the tap's last B fragment and everything older
+    constexpr int kWait[3][4] = {
+        {3, -1, 8, NF == 8 ? 8 : 6},                                   // tap 0
+        {NF == 8 ? 3 : 4, NF == 8 ? -1 : 6, 8, NF == 8 ? 8 : 6},       // tap 1
+        {NF == 8 ? 1 : 2, NF == 8 ? -1 : 2, 2, 2}};                    // tap 2
+    __shared__ uint4 lds[LDS_PIECES];
+    float* lbias = reinterpret_cast<float*>(lds + 2 * ASLOT + 3 * BSLOT);
+    float* lmul = lbias + BN;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int r16 = lane & 15, q = lane >> 4;
+    const Strips g(a);
+    const int ntm = (g.total + BM - 1) / BM;
+    const int G = gridDim.x;
+    const int xcd = blockIdx.x & 7, qq = G >> 3, rr = G & 7;
+    const int tix = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (blockIdx.x >> 3);
+    int m = tix;
+    if (m >= ntm) return;
+
+    if (tid < BN) {
+        const float neg = a.act == 1 ? 0.f : 1.f;
+        lbias[tid] = a.bias[tid];
+        lmul[tid] = a.act == 2 ? a.slope[tid] : neg;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+    const int lrow = lane >> 2, phys = lane & 3;
+    const int cpt = a.cin_pad >> 5;
+    const int U = 3 * cpt;
+    const int bi = (BPI - wave + NW - 1) / NW;
+    // weight piece of B DMA instruction j (recomputed at each issue: registers)
+#define OPK8_BOFF(j_)                                                                         \
+    ({                                                                                        \
+        int rb_ = ((j_) * NW + wave) * 16 + lrow;                                             \
+        asm volatile("" : "+v"(rb_));                                                         \
+        rb_ * 32 + (phys ^ (((rb_ >> 2) & 1) << 1)) * 8;                                      \
+    })
+    const char* abase = reinterpret_cast<const char*>(a.in + a.in_coff - a.in_cs);
+    uint32_t aoff[AIW];
+#define OPK8_AROW1(mt_, i_)                                                                   \
+    ({                                                                                        \
+        const int hr_ = ((i_) * NW + wave) * 16 + lrow;                                       \
+        const int lp_ = phys ^ (((hr_ >> 2) & 1) << 1);                                       \
+        int f_, yy_, xx_, s_;                                                                 \
+        const long pos_ = g.map((mt_) * BM - g.VW - 1 + hr_, f_, yy_, xx_, s_);               \
+        (uint32_t)(((pos_ + 1) * a.in_cs + lp_ * 8) * 2);                                     \
+    })
+#define OPK8_AROW(dst_, mt_)                                                                  \
+    do {                                                                                      \
+        _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_) dst_[i_] = OPK8_AROW1(mt_, i_);     \
+    } while (0)
+#define OPK8_ISSUE(c_, ky_, aslot_, bslot_, nt_)                                              \
+    do {                                                                                      \
+        if ((ky_) == 0) {                                                                     \
+            const int as_ = (aslot_) * ASLOT;                                                 \
+            _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
+                if (API % NW == 0 || i_ * NW + wave < API)                                    \
+                    __builtin_amdgcn_global_load_lds(                                         \
+                        (const void*)(abase + (c_) * 64 +                                     \
+                                      ((nt_) ? OPK8_AROW1(m + G, i_) : aoff[i_])),            \
+                        (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * NW + wave) * 64]), \
+                        16, 0, 0);                                                            \
+        }                                                                                     \
+        const int bs_ = 2 * ASLOT + (bslot_) * BSLOT;                                         \
+        const uint16_t* ub_ = a.w + (size_t)((c_) * 3 + (ky_)) * BROWS * 32;                  \
+        _Pragma("unroll") for (int j_ = 0; j_ < BIW; ++j_)                                    \
+            if (BPI % NW == 0 || j_ * NW + wave < BPI) {                                      \
+                const int bo_ = OPK8_BOFF(j_);                                                \
+                __builtin_amdgcn_global_load_lds(                                             \
+                    (const void*)(ub_ + bo_),                                                 \
+                    (__attribute__((address_space(3))) void*)(&lds[bs_ + (j_ * NW + wave) * 64]), \
+                    16, 0, 0);                                                                \
+            }                                                                                 \
+    } while (0)
+
+    // fragment bases: A row wave*64 + r16 + ky*VW + kx of a halo slot; B row kx*BN + r16 of a
+    // weight slot (fragment j at +1 KiB j)
+    const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+    const int arow0 = wave * WROWS + r16;
+    const uint32_t bswz = (uint32_t)swz64(r16, q) * 16;
+#define OPK8_ABASE(slot_, ky_, kx_)                                                            \
+    ({                                                                                        \
+        int r_ = arow0 + (ky_) * g.VW + (kx_);                                                \
+        asm volatile("" : "+v"(r_));                                                          \
+        lds0 + (uint32_t)((slot_) * ASLOT * 16) + (uint32_t)swz64(r_, q) * 16;                \
+    })
+#define OPK8_BBASE(slot_)                                                                     \
+    ({                                                                                        \
+        uint32_t b_ = bswz;                                                                   \
+        asm volatile("" : "+v"(b_));                                                          \
+        lds0 + (uint32_t)((2 * ASLOT + (slot_) * BSLOT) * 16) + b_;                           \
+    })
+
+    half8_t fbE[NF], fbO[NF], fa[4];
+    float4_t acc[MF][NF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+    // B fragment j of a tap (weight base bb_ + tap offset)
+#define OPK8_RB(dst_, bb_, toff_, j_)                                                         \
+    do {                                                                                      \
+        switch (j_) {                                                                         \
+        case 0: OPK8_DSR(dst_, bb_, (toff_) + 0); break;                                      \
+        case 1: OPK8_DSR(dst_, bb_, (toff_) + 1024); break;                                   \
+        case 2: OPK8_DSR(dst_, bb_, (toff_) + 2048); break;                                   \
+        case 3: OPK8_DSR(dst_, bb_, (toff_) + 3072); break;                                   \
+        case 4: OPK8_DSR(dst_, bb_, (toff_) + 4096); break;                                   \
+        case 5: OPK8_DSR(dst_, bb_, (toff_) + 5120); break;                                   \
+        case 6: OPK8_DSR(dst_, bb_, (toff_) + 6144); break;                                   \
+        default: OPK8_DSR(dst_, bb_, (toff_) + 7168); break;                                  \
+        }                                                                                     \
+    } while (0)
+#define OPK8_RA(dst_, ab_, i_)                                                                \
+    do {                                                                                      \
+        switch (i_) {                                                                         \
+        case 0: OPK8_DSR(dst_, ab_, 0); break;                                                \
+        case 1: OPK8_DSR(dst_, ab_, 1024); break;                                             \
+        case 2: OPK8_DSR(dst_, ab_, 2048); break;                                             \
+        default: OPK8_DSR(dst_, ab_, 3072); break;                                            \
+        }                                                                                     \
+    } while (0)
+#define OPK8_WAIT(n_, cur_, ...)                                                              \
+    asm volatile("s_waitcnt lgkmcnt(%c[n])" : "+v"(cur_), ##__VA_ARGS__ : [n] "n"(n_))
+    // one tap of kind K on B fragments FC and A fragments fa[]: K 0 / 1 (a unit's taps 0 / 1)
+    // stream the next tap's B fragments into FN during the steps; K 2 (tap 2) reads the next
+    // unit's tap-0 B fragments back into FC after its last MFMAs.  A fragments of the next tap
+    // come from base nab_ (steps 2, 3), B fragments from nbb_ + nbo_.
+#define OPK8_STEP(K, I, ab_, nab_, nbb_, nbo_, FC, FN)                                        \
+    do {                                                                                      \
+        if constexpr (I < 2) OPK8_RA(fa[I + 2], ab_, I + 2);                                  \
+        else OPK8_RA(fa[I - 2], nab_, I - 2);                                                 \
+        if constexpr (K != 2)                                                                 \
+            _Pragma("unroll") for (int k_ = 0; k_ < 2; ++k_)                                  \
+                if (2 * I + k_ < NF) OPK8_RB(FN[2 * I + k_], nbb_, nbo_, 2 * I + k_);          \
+        constexpr int w_ = kWait[K][I];                                                       \
+        if constexpr (I == 0) {                                                               \
+            if constexpr (NF == 8)                                                            \
+                OPK8_WAIT(w_, fa[0], "+v"(fa[1]), "+v"(FC[0]), "+v"(FC[1]), "+v"(FC[2]),      \
+                          "+v"(FC[3]), "+v"(FC[4]), "+v"(FC[5]), "+v"(FC[6 % NF]),            \
+                          "+v"(FC[7 % NF]));                                                  \
+            else                                                                              \
+                OPK8_WAIT(w_, fa[0], "+v"(FC[0]), "+v"(FC[1]), "+v"(FC[2]), "+v"(FC[3]),      \
+                          "+v"(FC[4]), "+v"(FC[5]));                                          \
+        } else if constexpr (w_ >= 0) {                                                       \
+            OPK8_WAIT(w_ < 0 ? 0 : w_, fa[I]);                                                \
+        }                                                                                     \
+        _Pragma("unroll") for (int j_ = 0; j_ < NF; ++j_)                                     \
+            acc[I][j_] = OPK8_ABLATE == 2 ? acc[I][j_] + (float)fa[I][j_]                      \
+                : __builtin_amdgcn_mfma_f32_16x16x32_f16(FC[j_], fa[I], acc[I][j_], 0, 0, 0);   \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+    } while (0)
+#define OPK8_TAP(K, ab_, nab_, nbb_, nbo_, FC, FN)                                            \
+    do {                                                                                      \
+        OPK8_STEP(K, 0, ab_, nab_, nbb_, nbo_, FC, FN);                                       \
+        OPK8_STEP(K, 1, ab_, nab_, nbb_, nbo_, FC, FN);                                       \
+        OPK8_STEP(K, 2, ab_, nab_, nbb_, nbo_, FC, FN);                                       \
+        OPK8_STEP(K, 3, ab_, nab_, nbb_, nbo_, FC, FN);                                       \
+        if constexpr (K == 2)                                                                 \
+            _Pragma("unroll") for (int j_ = 0; j_ < NF; ++j_) OPK8_RB(FC[j_], nbb_, nbo_, j_); \
+    } while (0)
+
+    // ---- prologue: units 0 and 1 of the first tile in flight, unit 0 visible, tap 0 read ------
+    OPK8_AROW(aoff, m);
+    OPK8_ISSUE(0, 0, 0, 0, false);
+    OPK8_ISSUE(0, 1, 0, 1, false);
+    vm_wait_rt(bi);
+    __builtin_amdgcn_s_barrier();
+    {
+        const uint32_t bb0 = OPK8_BBASE(0);
+        const uint32_t ab0 = OPK8_ABASE(0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < NF; ++j) OPK8_RB(fbE[j], bb0, 0, j);
+        OPK8_RA(fa[0], ab0, 0);
+        OPK8_RA(fa[1], ab0, 1);
+    }
+
+    int gc = 0;   // running chunk index of this tile's chunk 0 (halo slot parity)
+    for (;;) {
+        const int mn = m + G;
+        const bool has_next = mn < ntm;
+        for (int u = 0; u < U; ++u) {
+            const int c = u / 3, ky = u - 3 * (u / 3);
+            const int aslot = (gc + c) & 1;
+            const uint32_t bb_u = OPK8_BBASE(u % 3);
+            const uint32_t ab0 = OPK8_ABASE(aslot, ky, 0);
+            const uint32_t ab1 = OPK8_ABASE(aslot, ky, 1);
+            const uint32_t ab2 = OPK8_ABASE(aslot, ky, 2);
+            // next unit's tap 0 (unit u+1, or the next tile's unit 0): halo slot, tap row, weights
+            const bool nt = u + 1 >= U;
+            const int u1 = nt ? 0 : u + 1;
+            const int c1 = u1 / 3, ky1 = u1 - 3 * (u1 / 3);
+            const int aslot1 = (gc + (nt ? cpt : 0) + c1) & 1;
+            const uint32_t nab = OPK8_ABASE(aslot1, ky1, 0);
+            const uint32_t nbb = OPK8_BBASE((u + 1) % 3);
+            constexpr int S1 = MF * (NF / 2);   // epilogue stores per wave
+#define OPK8_DMA_U2()                                                                         \
+    do {                                                                                      \
+        const bool nt_ = u + 2 >= U;                                                          \
+        const int u2_ = nt_ ? u + 2 - U : u + 2;                                              \
+        const int c2_ = u2_ / 3;                                                              \
+        OPK8_ISSUE(c2_, u2_ - 3 * c2_, (gc + (nt_ ? cpt : 0) + c2_) & 1, (u + 2) % 3, nt_);  \
+    } while (0)
+            OPK8_TAP(0, ab0, ab1, bb_u, BN * 64, fbE, fbO);
+            OPK8_TAP(1, ab1, ab2, bb_u, 2 * BN * 64, fbO, fbE);
+            if (u == 0 && gc > 0) vm_wait<S1>();
+            else vm_wait<0>();
+            if (OPK8_ABLATE != 1) __builtin_amdgcn_s_barrier();
+            OPK8_TAP(2, ab2, nab, nbb, 0, fbE, fbO);
+            if (OPK8_ABLATE != 4 || u + 2 >= U) OPK8_DMA_U2();
+#undef OPK8_DMA_U2
+        }
+
+        // ---- epilogue: bias + activation + fp16 pack, 16-byte stores (border lanes to the sink)
+        const int el = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        const int er16 = el & 15, eq = el >> 4;
+        const int sidx = blockIdx.x * 64 * NW + wave * 64 + el;
+        uint4* sink4 = reinterpret_cast<uint4*>(a.sink) + sidx;
+        const int cw = 16 * (eq & 1) + 8 * (eq >> 1);   // channel of a lane's 16-byte store
+        int prow[MF];
+        bool pok[MF];
+        {
+            const int pbase = m * BM + wave * WROWS + er16;
+            int f, yy, xx, s;
+            prow[0] = (int)g.map(pbase, f, yy, xx, s);
+            pok[0] = g.interior(yy, xx, s, a.W);
+#pragma unroll
+            for (int i = 1; i < MF; ++i) {
+                xx += 16;
+                if (xx >= g.VW) {
+                    xx -= g.VW;
+                    if (++yy == g.Hp) {
+                        yy = 0;
+                        if (++s == g.nstrips) {
+                            s = 0;
+                            ++f;
+                        }
+                    }
+                }
+                const bool in = pbase + i * 16 < g.total;
+                prow[i] = in ? (f * g.Hp + yy) * g.Wp + s * g.sw + xx : 0;
+                pok[i] = in && g.interior(yy, xx, s, a.W);
+            }
+        }
+        const char* lb = reinterpret_cast<const char*>(lbias) + 4 * eq * 4;
+        const int nd = a.ndst;
+        uint16_t* const d0 = a.dst[0] + a.dst_coff[0];
+        const int cs0 = a.dst_cs[0];
+#pragma unroll
+        for (int j = 0; j < NF; j += 2) {
+            float4_t bq[2], mq[2];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                bq[k] = *reinterpret_cast<const float4_t*>(lb + (j + k) * 64);
+                mq[k] = *reinterpret_cast<const float4_t*>(lb + BN * 4 + (j + k) * 64);
+            }
+#pragma unroll
+            for (int i = 0; i < MF; ++i) {
+                uint32_t pk[2][2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const float4_t t = acc[i][j + h] + bq[h];
+                    const float4_t tm = t * mq[h];
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
+                    pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+                    pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                }
+                const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+                const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+                const uint4 val = make_uint4(sl[0], sh[0], sl[1], sh[1]);
+                const int ch = cw + j * 16;
+                if (nd == 1) {
+                    uint4* p = reinterpret_cast<uint4*>(d0 + ch + (size_t)prow[i] * cs0);
+                    *(pok[i] ? p : sink4) = val;
+                } else {
+                    for (int d = 0; d < nd; ++d) {
+                        uint4* p = reinterpret_cast<uint4*>(a.dst[d] + a.dst_coff[d] + ch +
+                                                            (size_t)prow[i] * a.dst_cs[d]);
+                        *(pok[i] ? p : sink4) = val;
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+            for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+        if (!has_next) break;
+        m = mn;
+        gc += cpt;
+        OPK8_AROW(aoff, m);
+    }
+#undef OPK8_TAP
+#undef OPK8_STEP
+#undef OPK8_WAIT
+#undef OPK8_RA
+#undef OPK8_RB
+#undef OPK8_ABASE
+#undef OPK8_BBASE
+#undef OPK8_ISSUE
+#undef OPK8_AROW
+#undef OPK8_AROW1
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+
+#undef OPK8_DSR
+
+}  // namespace
+
+bool conv3w8_supported(const ConvArgs& a)
+{
+    // one 16-byte store per (fragment pair, destination): the counted vmcnt at a tile's first
+    // mid-unit assumes a single destination
+    bool aligned = a.ndst == 1;
+    for (int d = 0; d < a.ndst; ++d) aligned = aligned && ((a.dst_coff[d] | a.dst_cs[d]) & 7) == 0;
+    return a.ntaps == 9 && (a.cout == 128 || a.cout == 96) && a.sink && a.cus > 0 && !a.out32 &&
+           aligned && a.sw + 2 * a.border > 16;
+}
+
+void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
+{
+    OPK_CHECK_ARG(conv3w8_supported(a), "conv3w8: 96 / 128 output channels, 3x3, one aligned slice");
+    const long total = (long)a.frames * a.nstrips * (a.H + 2 * a.border) * (a.sw + 2 * a.border);
+    const long ntm = (total + k8_BM - 1) / k8_BM;
+    const unsigned G = (unsigned)std::min<long>(a.cus, ntm);
+    OPK_CHECK_ARG(G <= 1024, "persistent grid exceeds the sink");
+    if (a.cout == 128) hipLaunchKernelGGL((conv3w8_kernel<128>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
+    else hipLaunchKernelGGL((conv3w8_kernel<96>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
+    OPK_LAUNCH_CHECK();
+}
+
+}  // namespace opk

@@ -207,6 +207,7 @@ def test_7x7_cpm_stages_vs_oracle(ctx, concat, hw):
 
 
 VARIANTS = {"persistent": {}, "persistent_conv3p": {"CONV3W": 0}, "w16": {"CONV3_PERSIST": 0},
+            "persistent_8wave": {"CONV3W8": 2}, "persistent_no_8wave": {"CONV3W8": 0},
             "w8": {"CONV3_W16": 0, "CONV1_TILE": 0}, "w8_one_per_cu": {"CONV3_W16": 0, "CONV3_SMALL": 0},
             "persistent_compiler_frags": {"CONV3W": 0, "CONV3P_ASMR": 0},
             "persistent_dwordx2": {"CONV3W": 0, "CONV3P_WIDE": 0},

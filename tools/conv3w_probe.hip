@@ -2,11 +2,15 @@
 // of every workgroup) on one BODY_25 stage-layer shape, plus its event-timed throughput.
 //
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude -o tools/conv3w_probe_bin tools/conv3w_probe.hip
-//   conv3w_probe [frames H W cin cout iters dma_end]
+//   conv3w_probe [frames H W cin cout iters dma_end zero_operands variant]
+//   variant 1 (NOSTAMPS builds): conv3w8, checked bit for bit against conv3w
 #ifndef NOSTAMPS
 #define OPKW_STAMPS
 #endif
 #include "../openpose_amd/csrc/kernels/conv3w.hip"
+#ifdef NOSTAMPS
+#include "../openpose_amd/csrc/kernels/conv3w8.hip"
+#endif
 
 #include <algorithm>
 #include <cstdio>
@@ -40,6 +44,7 @@ int main(int argc, char** argv)
     const int cout = argc > 5 ? std::atoi(argv[5]) : 128;
     const int iters = argc > 6 ? std::atoi(argv[6]) : 20;
     g_dma_end = argc > 7 ? std::atoi(argv[7]) : 1;
+    const int variant = argc > 9 ? std::atoi(argv[9]) : 0;
     const int cin_pad = (cin + 31) / 32 * 32;
     const int Wp = W + 2;
     const long pos = (long)frames * (H + 2) * Wp;
@@ -105,18 +110,40 @@ int main(int argc, char** argv)
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
-    for (int i = 0; i < 5; ++i) launch_conv3w(a, 0);
+    auto launch = [&](const ConvArgs& x) {
+#ifdef NOSTAMPS
+        if (variant == 1) { launch_conv3w8(x, 0); return; }
+#endif
+        launch_conv3w(x, 0);
+    };
+    CK(hipMemset(dout, 0, out_elems * 2));
+    for (int i = 0; i < 5; ++i) launch(a);
     CK(hipDeviceSynchronize());
     CK(hipEventRecord(e0, 0));
-    for (int i = 0; i < iters; ++i) launch_conv3w(a, 0);
+    for (int i = 0; i < iters; ++i) launch(a);
     CK(hipEventRecord(e1, 0));
     CK(hipEventSynchronize(e1));
     float ms = 0;
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / iters;
     const double flops = 2.0 * frames * H * W * (double)cout * cin * 9;
-    std::printf("conv3w dma_end=%d frames=%d %dx%d cin=%d cout=%d tiles=%ld grid=%d: %.2f us/launch %.1f TFLOP/s\n",
-                g_dma_end, frames, H, W, cin, cout, ntm, G, us, flops / us / 1e6);
+    if (variant == 1) {   // bit-identity against conv3w
+        uint16_t* dref;
+        CK(hipMalloc(&dref, out_elems * 2));
+        CK(hipMemset(dref, 0, out_elems * 2));
+        ConvArgs b = a;
+        b.dst[0] = dref + head * cout;
+        launch_conv3w(b, 0);
+        CK(hipDeviceSynchronize());
+        std::vector<uint16_t> h1(out_elems), h2(out_elems);
+        CK(hipMemcpy(h1.data(), dout, out_elems * 2, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(h2.data(), dref, out_elems * 2, hipMemcpyDeviceToHost));
+        long diff = 0, nz = 0;
+        for (long i = 0; i < out_elems; ++i) { diff += h1[i] != h2[i]; nz += h2[i] != 0; }
+        std::printf("  variant 1 vs conv3w: %ld of %ld fp16 values differ (%ld nonzero)\n", diff, out_elems, nz);
+    }
+    std::printf("conv3w v%d dma_end=%d frames=%d %dx%d cin=%d cout=%d tiles=%ld grid=%d: %.2f us/launch %.1f TFLOP/s\n",
+                variant, g_dma_end, frames, H, W, cin, cout, ntm, G, us, flops / us / 1e6);
 #ifndef OPKW_STAMPS
     return 0;
 #endif
