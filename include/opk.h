@@ -93,6 +93,28 @@ int opk_nms(opk_ctx* ctx, float* target_dev, int* kernel_scratch_dev, const floa
             float threshold, const int target_size[4], const int source_size[4],
             float offset_x, float offset_y);
 
+/* ---- Heat-map semantics of the reference's two builds (resize + NMS).
+ * OPK_MAPS_CPU (the default everywhere): resizeAndMergeCpu + nmsCpu, as above.
+ * OPK_MAPS_CUDA: what a CUDA build of the reference computes --
+ *   resizeAndMergeGpu (src/openpose/net/resizeAndMergeBase.cu:105-162,274-495): Catmull-Rom
+ *   bicubic (cubicInterpolate/bicubicInterpolate, include/openpose_private/gpu/cuda.hu:92-145) with
+ *   the clamped base, one source only at x8 (or identity; other ratios are the reference's
+ *   "Kernel only implemented for 8x resize" error), several sources scaled by
+ *   (W/W0) / (scale_ratios[i] / scale_ratios[0]) and averaged as sum / N (scale_ratios required);
+ *   nmsGpu (src/openpose/net/nmsBase.cu:50-90,161-240): interior pixels only, strictly greater
+ *   than all 8 neighbours, centroid sums fused multiply-adds (nvcc's default contraction).
+ * The expressions are evaluated as written, each operation rounded (nvcc's exact contraction of the
+ * cubic polynomial is not reproducible without the CUDA toolchain: parity unpinned). */
+#define OPK_MAPS_CPU 0
+#define OPK_MAPS_CUDA 1
+int opk_resize_and_merge_semantics(opk_ctx* ctx, float* target_dev, const float* const* sources_dev,
+                                   int num_sources, const int target_size[4],
+                                   const int* source_sizes, const float* scale_ratios,
+                                   int semantics);
+int opk_nms_semantics(opk_ctx* ctx, float* target_dev, int* kernel_scratch_dev,
+                      const float* source_dev, float threshold, const int target_size[4],
+                      const int source_size[4], float offset_x, float offset_y, int semantics);
+
 /* ---- PAF pair scores: the pafScoreKernel stage of op::connectBodyPartsGpu
  *      (src/openpose/net/bodyPartConnectorBase.cu:107-145) computed with the CPU path's getScoreAB
  *      numerics (bodyPartConnectorBase.cpp:12-75: clamp to the map, 0 on rejection).
@@ -273,6 +295,11 @@ int opk_pose_create_model(opk_ctx* ctx, opk_net* net, int pose_model, int maximi
                           int semantics, opk_pose** out);
 int opk_pose_destroy(opk_pose* pose);
 int opk_pose_set_property(opk_pose* pose, int property, double value);
+/* heat-map semantics of the pipeline's resize + NMS (OPK_MAPS_CPU, the default, or OPK_MAPS_CUDA:
+ * what the reference's CUDA build computes, see opk_nms_semantics); the lazy heat maps, the PAF
+ * samples and opk_pose_heatmaps follow it.  Multi-scale with OPK_MAPS_CUDA needs the raw-frame
+ * path (opk_pose_submit_frames), which knows scaleInputToNetInputs. */
+int opk_pose_set_map_semantics(opk_pose* pose, int semantics);
 /* frames: [n][3][net_h][net_w] device fp32; producer_w/h: original frame size (for
  * scaleNetToOutput, poseExtractorCaffe.cpp:306-310) */
 int opk_pose_forward(opk_pose* pose, const float* frames_dev, int n, int net_h, int net_w,

@@ -17,8 +17,11 @@
 // members of op::FaceExtractorCaffe / op::HandExtractorCaffe (faceExtractorCaffe.hpp:13-45,
 // handExtractorCaffe.hpp:13-58, replace src/openpose/{face,hand}/*ExtractorCaffe.cpp): every
 // rectangle of a frame cropped, run through the face / hand net and reduced on the GPU at once.
-// Numerics are the CPU path's; errors come back through op::error, the reference's
-// convention (errorAndLog.cpp:158-233).  See INTEGRATION.md for the build lines.
+// resizeAndMergeGpu / nmsGpu compute what the CUDA objects they replace compute (OPK_MAPS_CUDA:
+// Catmull-Rom x8 resize, strict-interior NMS; include/opk.h) unless the shim is built with
+// -DOPK_SHIM_MAPS=OPK_MAPS_CPU, which gives the CPU path's numerics (resizeAndMergeCpu / nmsCpu);
+// everything else follows the CPU path.  Errors come back through op::error, the
+// reference's convention (errorAndLog.cpp:158-233).  See INTEGRATION.md for the build lines.
 #include <memory>
 #include <mutex>
 #include <string>
@@ -38,6 +41,10 @@
 
 #include "opk.h"
 #include "poseExtractorHip.hpp"
+
+#ifndef OPK_SHIM_MAPS
+#define OPK_SHIM_MAPS OPK_MAPS_CUDA
+#endif
 
 namespace op
 {
@@ -88,9 +95,10 @@ namespace op
             for (const auto& s : sourceSizes)
                 sizes.insert(sizes.end(), s.begin(), s.end());
             std::vector<float> ratios(scaleInputToNetInputs.begin(), scaleInputToNetInputs.end());
-            check(opk_resize_and_merge(threadContext(), (float*)targetPtr,
-                                       (const float* const*)sourcePtrs.data(), (int)sourcePtrs.size(),
-                                       targetSize.data(), sizes.data(), ratios.data()),
+            check(opk_resize_and_merge_semantics(threadContext(), (float*)targetPtr,
+                                                 (const float* const*)sourcePtrs.data(),
+                                                 (int)sourcePtrs.size(), targetSize.data(),
+                                                 sizes.data(), ratios.data(), OPK_SHIM_MAPS),
                   __LINE__, __FUNCTION__);
             check(opk_sync(threadContext()), __LINE__, __FUNCTION__);
         }
@@ -108,9 +116,10 @@ namespace op
         try
         {
             requireFloat<T>("nmsGpu");
-            check(opk_nms(threadContext(), (float*)targetPtr, kernelPtr, (const float*)sourcePtr,
-                          (float)threshold, targetSize.data(), sourceSize.data(), (float)offset.x,
-                          (float)offset.y),
+            check(opk_nms_semantics(threadContext(), (float*)targetPtr, kernelPtr,
+                                    (const float*)sourcePtr, (float)threshold, targetSize.data(),
+                                    sourceSize.data(), (float)offset.x, (float)offset.y,
+                                    OPK_SHIM_MAPS),
                   __LINE__, __FUNCTION__);
             check(opk_sync(threadContext()), __LINE__, __FUNCTION__);
         }

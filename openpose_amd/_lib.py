@@ -36,6 +36,9 @@ _SIGS = {
     "opk_memcpy_d2h": (_i, [_p, _p, _p, _c.c_size_t]),
     "opk_resize_and_merge": (_i, [_p, _p, _c.POINTER(_p), _i, _ip, _ip, _fp]),
     "opk_nms": (_i, [_p, _p, _p, _p, _f, _ip, _ip, _f, _f]),
+    "opk_nms_semantics": (_i, [_p, _p, _p, _p, _f, _ip, _ip, _f, _f, _i]),
+    "opk_pose_set_map_semantics": (_i, [_p, _i]),
+    "opk_resize_and_merge_semantics": (_i, [_p, _p, _c.POINTER(_p), _i, _ip, _ip, _fp, _i]),
     "opk_paf_scores": (_i, [_p, _p, _p, _p, _i, _i, _i, _i, _i, _i, _f, _f, _f]),
     "opk_connect_body_parts": (_i, [_p, _p, _p, _i, _ip, _p, _p, _i, _i, _i, _i, _i, _f, _f, _i,
                                     _f, _f, _f, _i]),

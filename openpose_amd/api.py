@@ -17,6 +17,9 @@ from .pose_tables import (BODY_25, CONNECT_CPU, CONNECT_GPU, CONNECT_INTER_MIN_A
                           CONNECT_INTER_THRESHOLD,
                           CONNECT_MIN_SUBSET_CNT, CONNECT_MIN_SUBSET_SCORE, NMS_THRESHOLD)
 
+# heat-map semantics (include/opk.h OPK_MAPS_*): the reference's CPU build or its CUDA build
+MAPS_CPU, MAPS_CUDA = 0, 1
+
 
 def _ptr(t):
     if t is None:
@@ -103,13 +106,16 @@ class Context:
         return self
 
     # ---- operators ---------------------------------------------------------------------------
-    def resize_and_merge(self, target, sources):
-        """target [N,C,H,W] fp32 CUDA; sources list of [N,C,h,w] (resizeAndMergeGpu)."""
+    def resize_and_merge(self, target, sources, semantics=MAPS_CPU, scale_ratios=None):
+        """target [N,C,H,W] fp32 CUDA; sources list of [N,C,h,w] (resizeAndMergeGpu).  semantics
+        MAPS_CPU: resizeAndMergeCpu's arithmetic; MAPS_CUDA: the CUDA build's (scale_ratios =
+        scaleInputToNetInputs, needed with several sources)."""
         n = len(sources)
         ptrs = (ctypes.c_void_p * n)(*[s.data_ptr() for s in sources])
         sizes = (ctypes.c_int * (4 * n))(*[int(v) for s in sources for v in s.shape])
-        check(self.L.opk_resize_and_merge(self.h, _ptr(target), ptrs, n, int4(target.shape), sizes,
-                                          None))
+        ratios = None if scale_ratios is None else (ctypes.c_float * n)(*[float(r) for r in scale_ratios])
+        check(self.L.opk_resize_and_merge_semantics(self.h, _ptr(target), ptrs, n,
+                                                    int4(target.shape), sizes, ratios, semantics))
 
     def cvmat_to_input(self, net_input, frames, scale, normalize=1):
         """op::CvMatToOpInput for one scale: frames [n, h, w, 3] uint8 BGR (CUDA) ->
@@ -121,10 +127,12 @@ class Context:
                                         float(scale), net_input.shape[3], net_input.shape[2],
                                         normalize))
 
-    def nms(self, peaks, heat, threshold=NMS_THRESHOLD, offset=(0.0, 0.0)):
-        """peaks [N,parts,maxPeaks+1,3]; heat [N,C,H,W] (nmsGpu)."""
-        check(self.L.opk_nms(self.h, _ptr(peaks), None, _ptr(heat), threshold, int4(peaks.shape),
-                             int4(heat.shape), offset[0], offset[1]))
+    def nms(self, peaks, heat, threshold=NMS_THRESHOLD, offset=(0.0, 0.0), semantics=MAPS_CPU):
+        """peaks [N,parts,maxPeaks+1,3]; heat [N,C,H,W] (nmsGpu; semantics MAPS_CPU: nmsCpu's
+        rules, MAPS_CUDA: nmsGpu's)."""
+        check(self.L.opk_nms_semantics(self.h, _ptr(peaks), None, _ptr(heat), threshold,
+                                       int4(peaks.shape), int4(heat.shape), offset[0], offset[1],
+                                       semantics))
 
     def paf_scores(self, scores, heat, peaks, pose_model=BODY_25, inter_th=CONNECT_INTER_THRESHOLD,
                    inter_min_above=CONNECT_INTER_MIN_ABOVE_THRESHOLD, nms_th=NMS_THRESHOLD):
@@ -429,6 +437,11 @@ class PoseExtractor:
 
     def set_property(self, prop, value):
         check(self.L.opk_pose_set_property(self.h, prop, float(value)))
+
+    def set_map_semantics(self, semantics):
+        """MAPS_CPU (default) or MAPS_CUDA: the resize + NMS arithmetic of the reference's CPU or
+        CUDA build (opk_pose_set_map_semantics)."""
+        check(self.L.opk_pose_set_map_semantics(self.h, semantics))
 
     def set_overlay(self, overlay):
         self._overlay = overlay   # keep the tensor alive

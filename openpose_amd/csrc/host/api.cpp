@@ -8,6 +8,7 @@
 #include "connector.h"
 #include "context.h"
 #include "json.h"
+#include "maps.h"
 #include "output.h"
 
 namespace opk {
@@ -176,9 +177,42 @@ int opk_resize_and_merge(opk_ctx* ctx, float* target, const float* const* source
     });
 }
 
+int opk_resize_and_merge_semantics(opk_ctx* ctx, float* target, const float* const* sources,
+                                   int nsrc, const int ts[4], const int* ss,
+                                   const float* scale_ratios, int semantics)
+{
+    if (semantics == OPK_MAPS_CPU)
+        return opk_resize_and_merge(ctx, target, sources, nsrc, ts, ss, scale_ratios);
+    return guarded([&] {
+        OPK_CHECK_ARG(semantics == OPK_MAPS_CUDA, "unknown heat-map semantics");
+        OPK_CHECK_ARG(ctx && target && sources && ts && ss, "NULL argument");
+        OPK_CHECK_ARG(nsrc >= 1, "sourceSizes cannot be empty.");
+        int sh[opk::kMaxResizeSources], sw[opk::kMaxResizeSources];
+        for (int i = 0; i < nsrc && i < opk::kMaxResizeSources; ++i) {
+            const int* s = ss + 4 * i;
+            OPK_CHECK_ARG(s[0] == ts[0] && s[1] == ts[1],
+                          "source " + std::to_string(i) + " frames/channels differ from target");
+            sh[i] = s[2];
+            sw[i] = s[3];
+        }
+        const opk::HeatMap m = opk::cuda_heat_map(sources, sh, sw, nsrc, ts[1], ts[2], ts[3],
+                                                  scale_ratios);
+        ctx->bind();
+        opk::launch_resize_merge_cuda(target, m, ts[0] * ts[1], ctx->stream);
+    });
+}
+
 // nmsCpu sanity checks (nmsBase.cpp:116-122) + the batched HIP kernel
 int opk_nms(opk_ctx* ctx, float* target, int* kernel_scratch, const float* source, float th,
             const int ts[4], const int ss[4], float offx, float offy)
+{
+    return opk_nms_semantics(ctx, target, kernel_scratch, source, th, ts, ss, offx, offy,
+                             OPK_MAPS_CPU);
+}
+
+int opk_nms_semantics(opk_ctx* ctx, float* target, int* kernel_scratch, const float* source,
+                      float th, const int ts[4], const int ss[4], float offx, float offy,
+                      int semantics)
 {
     (void)kernel_scratch;
     return guarded([&] {
@@ -188,9 +222,11 @@ int opk_nms(opk_ctx* ctx, float* target, int* kernel_scratch, const float* sourc
         OPK_CHECK_ARG(ts[3] == 3, "target peak vector must be 3 (x, y, score)");
         OPK_CHECK_ARG(ts[1] <= ss[1], "more target parts than source channels");
         ctx->bind();
+        OPK_CHECK_ARG(semantics == OPK_MAPS_CPU || semantics == OPK_MAPS_CUDA,
+                      "unknown heat-map semantics");
         opk::launch_nms(target, ctx->nms_candidates(ts[0], ts[1]),
                         opk::heat_materialised(source, ss[1], ss[2], ss[3]), ts[0], ts[1], ts[2],
-                        th, offx, offy, ctx->stream);
+                        th, offx, offy, ctx->stream, semantics == OPK_MAPS_CUDA);
     });
 }
 

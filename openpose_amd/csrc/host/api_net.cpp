@@ -154,6 +154,14 @@ int opk_pose_destroy(opk_pose* p)
     });
 }
 
+int opk_pose_set_map_semantics(opk_pose* p, int semantics)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->set_map_semantics(semantics);
+    });
+}
+
 int opk_pose_set_property(opk_pose* p, int prop, double v)
 {
     return guarded_net([&] {

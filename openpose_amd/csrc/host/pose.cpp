@@ -19,6 +19,7 @@
 
 #include "../../../include/opk.h"
 #include "input.h"
+#include "maps.h"
 
 namespace opk {
 
@@ -60,6 +61,12 @@ PoseHip::~PoseHip()
         if (s.done) (void)hipEventDestroy(s.done);
 }
 
+void PoseHip::set_map_semantics(int maps)
+{
+    OPK_CHECK_ARG(maps == kMapsCpu || maps == kMapsCuda, "unknown heat-map semantics");
+    maps_ = maps;
+}
+
 void PoseHip::set_property(int prop, double v)
 {
     OPK_CHECK_ARG(prop >= 0 && prop < 5, "unknown PoseProperty");
@@ -81,8 +88,11 @@ float* PoseHip::heatmaps(int shape[4])
     if (!heat_valid_) {
         ctx_->bind();
         float* heat = static_cast<float*>(heat_.get((size_t)n_ * s.heat.channels * hh_ * hw_ * 4));
-        launch_resize_merge(heat, s.heat.src, s.heat.nsrc, n_ * s.heat.channels, hh_, hw_,
-                            ctx_->stream);
+        if (s.heat.cuda)
+            launch_resize_merge_cuda(heat, s.heat, n_ * s.heat.channels, ctx_->stream);
+        else
+            launch_resize_merge(heat, s.heat.src, s.heat.nsrc, n_ * s.heat.channels, hh_, hw_,
+                                ctx_->stream);
         OPK_HIP(hipStreamSynchronize(ctx_->stream));
         heat_valid_ = true;
     }
@@ -207,10 +217,18 @@ void PoseHip::submit_frames(const uint8_t* frames, int n, int w, int h, size_t s
         hw[2 * i + 1] = nw;
     }
     inputs_n_ = n;
-    if (scale_number_ == 1)
-        submit(ptrs[0], n, hw[0], hw[1], w, h);
-    else
-        submit_multi(ptrs, hw, scale_number_, n, w, h);
+    for (int i = 0; i < scale_number_; ++i) map_ratios_[i] = (float)scales[i];
+    have_ratios_ = true;
+    try {
+        if (scale_number_ == 1)
+            submit(ptrs[0], n, hw[0], hw[1], w, h);
+        else
+            submit_multi(ptrs, hw, scale_number_, n, w, h);
+    } catch (...) {
+        have_ratios_ = false;
+        throw;
+    }
+    have_ratios_ = false;
 }
 
 void PoseHip::forward_frames(const uint8_t* frames, int n, int w, int h, size_t step)
@@ -277,15 +295,28 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
     //    so the 75 MB/frame heat-map stack is only written if requested
     const int H = outs[0].h * 8, W = outs[0].w * 8;
     HeatMap heat{};
-    heat.channels = C;
-    heat.h = H;
-    heat.w = W;
-    heat.nsrc = nscales;
-    heat.inv_n = (float)(1. / (double)nscales);
-    for (int i = 0; i < nscales; ++i) {
-        const auto& t = ctx_->tables(outs[i].h, outs[i].w, H, W);
-        heat.src[i] = ResizeSource{outs[i].ptr, outs[i].h, outs[i].w, t.yofs, t.ycoef, t.xofs,
-                                   t.xcoef};
+    if (maps_ == kMapsCuda) {   // resizeAndMergeGpu's arithmetic (maps.h)
+        OPK_CHECK_ARG(nscales == 1 || have_ratios_,
+                      "multi-scale CUDA map semantics needs scaleInputToNetInputs (raw-frame path)");
+        const float* ptr[kMaxResizeSources];
+        int hs[kMaxResizeSources], ws[kMaxResizeSources];
+        for (int i = 0; i < nscales; ++i) {
+            ptr[i] = outs[i].ptr;
+            hs[i] = outs[i].h;
+            ws[i] = outs[i].w;
+        }
+        heat = cuda_heat_map(ptr, hs, ws, nscales, C, H, W, have_ratios_ ? map_ratios_ : nullptr);
+    } else {
+        heat.channels = C;
+        heat.h = H;
+        heat.w = W;
+        heat.nsrc = nscales;
+        heat.inv_n = (float)(1. / (double)nscales);
+        for (int i = 0; i < nscales; ++i) {
+            const auto& t = ctx_->tables(outs[i].h, outs[i].w, H, W);
+            heat.src[i] = ResizeSource{outs[i].ptr, outs[i].h, outs[i].w, t.yofs, t.ycoef, t.xofs,
+                                       t.xcoef};
+        }
     }
 
     // 2. scale net -> output (poseExtractorCaffe.cpp:281-310), net output size == net input size
@@ -300,7 +331,8 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
     const int P1 = kMaxPeaks + 1;
     const size_t peak_floats = (size_t)m.parts * P1 * 3;
     float* peaks = static_cast<float*>(sl.peaks.get((size_t)n * peak_floats * 4));
-    launch_nms(peaks, ctx_->nms_candidates(n, m.parts), heat, n, m.parts, P1, nms_th, off, off, s);
+    launch_nms(peaks, ctx_->nms_candidates(n, m.parts), heat, n, m.parts, P1, nms_th, off, off, s,
+               maps_ == kMapsCuda);
 
     // 4. connector, device half: PAF integrals of every candidate pair into compact records
     //    sized for the worst case (every pair of every limb), so no frame ever falls back

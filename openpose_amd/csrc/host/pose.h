@@ -23,6 +23,9 @@ public:
     ~PoseHip();
 
     void set_property(int prop, double v);
+    // heat-map semantics of resize + NMS (maps.h: kMapsCpu, kMapsCuda)
+    void set_map_semantics(int maps);
+    int map_semantics() const { return maps_; }
     double property(int prop) const { return props_[prop]; }
     void set_overlay(const float* overlay) { overlay_ = overlay; }
 
@@ -102,6 +105,9 @@ private:
     int inputs_n_ = 0;
     bool maximize_positives_;
     int model_, semantics_;
+    int maps_ = 0;                              // kMapsCpu
+    float map_ratios_[kMaxResizeSources] = {};  // scaleInputToNetInputs of the raw-frame path
+    bool have_ratios_ = false;
     double props_[5];
     const float* overlay_ = nullptr;
     hipStream_t copy_ = nullptr;         // D2H of collected batches (overlaps the next batch)

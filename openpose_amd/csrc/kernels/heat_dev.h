@@ -47,10 +47,57 @@ __device__ __forceinline__ bool cubic_simd_column(int x, int w)
     return x < w - w % kCvVResizeLanes;
 }
 
+// ---- CUDA-build semantics (HeatMap::cuda) ------------------------------------------------------
+// cubicInterpolate (include/openpose_private/gpu/cuda.hu:111-123), the expression as written,
+// every operation rounded separately (-ffp-contract=off; nvcc's own contraction is not pinned)
+__device__ __forceinline__ float cuda_cubic(float v0, float v1, float v2, float v3, float dx)
+{
+    return (-0.5f * v0 + 1.5f * v1 - 1.5f * v2 + 0.5f * v3) * dx * dx * dx +
+           (v0 - 2.5f * v1 + 2.f * v2 - 0.5f * v3) * dx * dx - 0.5f * (v0 - v2) * dx + v1;
+}
+
+// bicubicInterpolate with cubicSequentialData's clamped base (cuda.hu:92-109,125-145); the x8
+// kernel resize8TimesKernel (resizeAndMergeBase.cu:105-140) reads the same four clamped rows and
+// columns through its 5x5 shared window, so one function serves both
+__device__ __forceinline__ float cuda_bicubic(const float* src, float xs, float ys, int sw, int sh)
+{
+    const int x1 = heat_clampi((int)floorf(xs), 0, sw - 1);
+    const int xi[4] = {max(0, x1 - 1), x1, min(sw - 1, x1 + 1), min(sw - 1, min(sw - 1, x1 + 1) + 1)};
+    const float dx = xs - (float)x1;
+    const int y1 = heat_clampi((int)floorf(ys), 0, sh - 1);
+    const int yi[4] = {max(0, y1 - 1), y1, min(sh - 1, y1 + 1), min(sh - 1, min(sh - 1, y1 + 1) + 1)};
+    const float dy = ys - (float)y1;
+    float t[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const float* r = src + (size_t)yi[i] * sw;
+        t[i] = cuda_cubic(r[xi[0]], r[xi[1]], r[xi[2]], r[xi[3]], dx);
+    }
+    return cuda_cubic(t[0], t[1], t[2], t[3], dy);
+}
+
+// one target pixel of resizeAndMergeGpu: x8 single source (resize8TimesKernel, source coordinate
+// (x + 0.5f) / 8 - 0.5f), identity (fillKernel) or the multi-scale resizeAndAddAndAverageKernel
+// (resizeAndMergeBase.cu:142-162: sum over sources in order, then / counter)
+__device__ __forceinline__ float heat_at_cuda(const HeatMap& M, int plane, int x, int y)
+{
+    float acc = 0.f;
+    for (int n = 0; n < M.nsrc; ++n) {
+        const ResizeSource& S = M.src[n];
+        const float* src = S.src + (size_t)plane * S.sh * S.sw;
+        if (S.sx == 1.f && S.sy == 1.f && M.nsrc == 1) return src[(size_t)y * S.sw + x];
+        const float xs = ((float)x + 0.5f) / S.sx - 0.5f;
+        const float ys = ((float)y + 0.5f) / S.sy - 0.5f;
+        acc += cuda_bicubic(src, xs, ys, S.sw, S.sh);
+    }
+    return M.nsrc > 1 ? acc / (float)M.nsrc : acc;
+}
+
 // value of plane `plane` (= frame * channels + channel) at full-resolution pixel (x, y)
 __device__ __forceinline__ float heat_at(const HeatMap& M, int plane, int x, int y)
 {
     if (M.heat) return M.heat[((size_t)plane * M.h + y) * M.w + x];
+    if (M.cuda) return heat_at_cuda(M, plane, x, y);
     float acc = 0.f;
     for (int n = 0; n < M.nsrc; ++n) {
         const ResizeSource& S = M.src[n];

@@ -15,6 +15,8 @@ struct ResizeSource {
     const float* ycoef;  // [dh][4]
     const int* xofs;     // [dw]
     const float* xcoef;  // [dw][4]
+    // CUDA-build semantics only (HeatMap::cuda): target pixel x maps to source (x + 0.5) / sx - 0.5
+    float sx, sy;
 };
 constexpr int kMaxResizeSources = 8;
 // dst [planes][dh][dw]; planes = frames * channels; all sources share the plane count.
@@ -31,7 +33,12 @@ struct HeatMap {
     int nsrc;
     float inv_n;
     ResizeSource src[kMaxResizeSources];
+    // 1: the CUDA build's resizeAndMergeGpu arithmetic (heat_dev.h: cuda_bicubic, per-source
+    // scale sx / sy, sum / N) instead of cv::resize's; the tables are then unused
+    int cuda;
 };
+// dst [planes][M.h][M.w] = the CUDA-semantics resize/merge (M.cuda) of M's sources
+void launch_resize_merge_cuda(float* dst, const HeatMap& M, int planes, hipStream_t stream);
 inline HeatMap heat_materialised(const float* heat, int channels, int h, int w)
 {
     HeatMap m{};
@@ -47,8 +54,11 @@ inline HeatMap heat_materialised(const float* heat, int channels, int h, int w)
 // ints, zeroed once before the first call (every call leaves it zeroed again).
 constexpr int kNmsCandidates = 1024;   // per plane; more peaks fall back to an ordered re-scan
 size_t nms_scratch_ints(int frames, int parts);
+// cuda: nmsGpu's rules (nmsBase.cu:50-90,161-240: strict interior, 8 strict neighbours, centroid
+// sums contracted to fma as nvcc's default --fmad does) instead of nmsCpu's
 void launch_nms(float* peaks, int* scratch, const HeatMap& heat, int frames, int parts,
-                int max_peaks1, float threshold, float offx, float offy, hipStream_t stream);
+                int max_peaks1, float threshold, float offx, float offy, hipStream_t stream,
+                bool cuda = false);
 
 // ---- PAF scores (paf.hip) --------------------------------------------------------------------
 struct PafPairTable {

@@ -32,11 +32,20 @@ constexpr int DT = 256;   // detect lanes per block
 constexpr int FT = 256;   // finalize lanes per block
 constexpr int CAP = kNmsCandidates;
 
-// peak rules of nmsCpu for pixel (x, y) of value v; get(x, y) reads an in-map neighbour
+// peak rules of nmsCpu for pixel (x, y) of value v; get(x, y) reads an in-map neighbour.
+// cuda: nmsRegisterKernel's (nmsBase.cu:50-90) -- interior pixels only (0 < x < w-1, 0 < y < h-1),
+// v > th and v > all 8 neighbours
 template <typename Get>
-__device__ __forceinline__ bool peak_at(Get get, int w, int h, float th, int x, int y, float v)
+__device__ __forceinline__ bool peak_at(Get get, int w, int h, float th, int x, int y, float v,
+                                        bool cuda = false)
 {
     if (!(v > th)) return false;
+    if (cuda) {
+        if (!(x > 0 && x < w - 1 && y > 0 && y < h - 1)) return false;
+        return v > get(x - 1, y - 1) && v > get(x, y - 1) && v > get(x + 1, y - 1) &&
+               v > get(x - 1, y) && v > get(x + 1, y) && v > get(x - 1, y + 1) &&
+               v > get(x, y + 1) && v > get(x + 1, y + 1);
+    }
     if (x > 1 && x < w - 2 && y > 1 && y < h - 2) {
         return v > get(x - 1, y - 1) && v > get(x, y - 1) && v > get(x + 1, y - 1) &&
                v > get(x - 1, y) && v > get(x + 1, y) && v > get(x - 1, y + 1) &&
@@ -68,7 +77,7 @@ __device__ __forceinline__ void push_candidate(int* plane, int idx)
 __global__ __launch_bounds__(DT) void nms_detect_kernel(int* __restrict__ scratch,
                                                         const float* __restrict__ heat,
                                                         int channels, int parts, int h, int w,
-                                                        float th)
+                                                        float th, int cuda)
 {
     const int c = blockIdx.y, b = blockIdx.z;
     const float* s = heat + ((size_t)b * channels + c) * h * w;
@@ -83,7 +92,7 @@ __global__ __launch_bounds__(DT) void nms_detect_kernel(int* __restrict__ scratc
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int x = x0 + k;
-        if (x < w && peak_at(get, w, h, th, x, y, row[x])) push_candidate(plane, y * w + x);
+        if (x < w && peak_at(get, w, h, th, x, y, row[x], cuda != 0)) push_candidate(plane, y * w + x);
     }
 }
 
@@ -125,7 +134,14 @@ __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ s
     float acc[LWR];
 #pragma unroll
     for (int rr = 0; rr < LWR; ++rr) acc[rr] = 0.f;
-    for (int n = 0; n < M.nsrc; ++n) {
+    if (M.cuda) {   // CUDA-build resize arithmetic: pixel by pixel (no shared passes)
+#pragma unroll
+        for (int rr = 0; rr < LWR; ++rr) {
+            const int y = y0 + rr;
+            win[rr * LT + tid] = (y >= 0 && y < H && xin) ? heat_at_cuda(M, plane, x, y) : th;
+        }
+    }
+    for (int n = 0; n < (M.cuda ? 0 : M.nsrc); ++n) {
         const ResizeSource& S = M.src[n];
         const float* src = S.src + (size_t)plane * S.sh * S.sw;
         const int r_lo = heat_clampi(S.yofs[ry_lo] - 1, 0, S.sh - 1);
@@ -185,10 +201,12 @@ __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ s
             acc[rr] = (n == 0) ? v : v + acc[rr];
         }
     }
+    if (!M.cuda) {
 #pragma unroll
-    for (int rr = 0; rr < LWR; ++rr) {
-        const int y = y0 + rr;
-        win[rr * LT + tid] = (y >= 0 && y < H && xin) ? (M.nsrc > 1 ? acc[rr] * M.inv_n : acc[rr]) : th;
+        for (int rr = 0; rr < LWR; ++rr) {
+            const int y = y0 + rr;
+            win[rr * LT + tid] = (y >= 0 && y < H && xin) ? (M.nsrc > 1 ? acc[rr] * M.inv_n : acc[rr]) : th;
+        }
     }
     __syncthreads();
     if (tid == 0 || tid == LT - 1 || !xin) return;
@@ -197,7 +215,7 @@ __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ s
     for (int ty = 0; ty < LOY; ++ty) {
         const int y = y0 + 1 + ty;
         if (y >= H) break;
-        if (peak_at(get, W, H, th, x, y, win[(ty + 1) * LT + tid])) push_candidate(pl, y * W + x);
+        if (peak_at(get, W, H, th, x, y, win[(ty + 1) * LT + tid], M.cuda != 0)) push_candidate(pl, y * W + x);
     }
 }
 
@@ -215,8 +233,13 @@ __device__ void refine_write(float* __restrict__ out, const HeatMap& M, int plan
             if (xx < 0 || xx >= w) continue;
             const float sc = heat_at(M, plane, xx, yy);
             if (sc > 0) {
-                xa += (float)xx * sc;
-                ya += (float)yy * sc;
+                if (M.cuda) {   // nvcc contracts xAcc += x*score (default --fmad=true)
+                    xa = fmaf((float)xx, sc, xa);
+                    ya = fmaf((float)yy, sc, ya);
+                } else {
+                    xa += (float)xx * sc;
+                    ya += (float)yy * sc;
+                }
                 sa += sc;
             }
         }
@@ -284,7 +307,7 @@ __global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ pe
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const int x = x0 + k;
-                    if (x < w && peak_at(get, w, h, th, x, y, get(x, y))) mask |= 1u << k;
+                    if (x < w && peak_at(get, w, h, th, x, y, get(x, y), M.cuda != 0)) mask |= 1u << k;
                 }
             }
             const int cnt = __popc(mask);
@@ -329,9 +352,13 @@ __global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ pe
 
 size_t nms_scratch_ints(int frames, int parts) { return (size_t)frames * parts * (CAP + 1); }
 
-void launch_nms(float* peaks, int* scratch, const HeatMap& heat, int frames, int parts,
-                int max_peaks1, float threshold, float offx, float offy, hipStream_t stream)
+void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, int parts,
+                int max_peaks1, float threshold, float offx, float offy, hipStream_t stream,
+                bool cuda)
 {
+    // the peak rules and centroid follow `cuda`; so does the resize arithmetic of a lazy map
+    HeatMap heat = heat_in;
+    heat.cuda = cuda ? 1 : 0;
     const int h = heat.h, w = heat.w;
     OPK_CHECK_ARG(frames > 0 && parts > 0 && parts <= heat.channels, "bad channel counts");
     OPK_CHECK_ARG(h > 0 && w > 0 && max_peaks1 >= 1, "bad sizes");
@@ -343,7 +370,7 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat, int frames, int
         const int quads = (w + 3) >> 2;
         dim3 g1((h * quads + DT - 1) / DT, parts, frames);
         hipLaunchKernelGGL(nms_detect_kernel, g1, dim3(DT), 0, stream, scratch, heat.heat,
-                           heat.channels, parts, h, w, threshold);
+                           heat.channels, parts, h, w, threshold, heat.cuda);
     } else {
         constexpr int loy = 16;
         hipLaunchKernelGGL(nms_detect_lazy_kernel<loy>, dim3((w + LOX - 1) / LOX, (h + loy - 1) / loy,

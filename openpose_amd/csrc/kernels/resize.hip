@@ -87,7 +87,27 @@ __global__ __launch_bounds__(TX) void resize_merge_kernel(float* __restrict__ ds
     }
 }
 
+// CUDA-build semantics (HeatMap::cuda): one lane per target pixel, heat_at_cuda
+__global__ __launch_bounds__(256) void resize_merge_cuda_kernel(float* __restrict__ dst, const HeatMap M)
+{
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    const int plane = blockIdx.z;
+    if (x >= M.w || y >= M.h) return;
+    dst[((size_t)plane * M.h + y) * M.w + x] = heat_at_cuda(M, plane, x, y);
+}
+
 }  // namespace
+
+void launch_resize_merge_cuda(float* dst, const HeatMap& M, int planes, hipStream_t stream)
+{
+    OPK_CHECK_ARG(M.cuda && !M.heat && M.nsrc >= 1 && M.nsrc <= kMaxResizeSources,
+                  "CUDA-semantics resize: 1..8 lazy sources");
+    OPK_CHECK_ARG(planes > 0 && M.h > 0 && M.w > 0, "empty target");
+    dim3 grid((M.w + 63) / 64, (M.h + 3) / 4, planes);
+    hipLaunchKernelGGL(resize_merge_cuda_kernel, grid, dim3(256), 0, stream, dst, M);
+    OPK_LAUNCH_CHECK();
+}
 
 void launch_resize_merge(float* dst, const ResizeSource* srcs, int nsrc, int planes, int dh,
                          int dw, hipStream_t stream)

@@ -38,6 +38,9 @@ def lib():
             build(ref=False)
         L = ctypes.CDLL(path)
         L.orc_nms.argtypes = [_f32p, _f32p, _f, _i, _i, _i, _i, _f, _f]
+        L.orc_nms_cuda.argtypes = [_f32p, _f32p, _f, _i, _i, _i, _i, _f, _f]
+        L.orc_resize_merge_cuda.argtypes = [_f32p, ctypes.POINTER(ctypes.c_void_p), _i, _i, _i32p,
+                                            _i, _i, ctypes.c_void_p]
         L.orc_resize_cubic.argtypes = [_f32p, _f32p, _i, _i, _i, _i]
         L.orc_resize_merge.argtypes = [_f32p, ctypes.POINTER(ctypes.c_void_p), _i, _i, _i32p, _i, _i]
         L.orc_cubic_tables.argtypes = [_i, _i, _i32p, _f32p]
@@ -96,12 +99,14 @@ def ref_lib():
 
 
 # ---- numpy front ends -------------------------------------------------------------------------
-def nms(heat, threshold, max_peaks1=128, offset=(0.0, 0.0), channels=25):
+def nms(heat, threshold, max_peaks1=128, offset=(0.0, 0.0), channels=25, cuda=False):
+    """nmsCpu (or, cuda=True, nmsGpu's rules) on one frame's heat maps [C, H, W]."""
     heat = np.ascontiguousarray(heat, np.float32)
     c, h, w = heat.shape
     channels = min(channels, c)
     out = np.zeros((channels, max_peaks1, 3), np.float32)
-    lib().orc_nms(out, heat, threshold, channels, max_peaks1, h, w, offset[0], offset[1])
+    fn = lib().orc_nms_cuda if cuda else lib().orc_nms
+    fn(out, heat, threshold, channels, max_peaks1, h, w, offset[0], offset[1])
     return out
 
 
@@ -120,6 +125,21 @@ def resize_merge(srcs, dh, dw):
     ptrs = (ctypes.c_void_p * len(srcs))(*[s.ctypes.data for s in srcs])
     hw = np.array([[s.shape[1], s.shape[2]] for s in srcs], np.int32).ravel()
     lib().orc_resize_merge(out, ptrs, len(srcs), c, hw, dh, dw)
+    return out
+
+
+def resize_merge_cuda(srcs, dh, dw, scale_ratios=None):
+    """resizeAndMergeGpu (CUDA build) of one frame: srcs list of [C, h_i, w_i] -> [C, dh, dw];
+    None where the reference raises (non-x8 single source, > 8 sources)."""
+    srcs = [np.ascontiguousarray(s, np.float32) for s in srcs]
+    c = srcs[0].shape[0]
+    out = np.empty((c, dh, dw), np.float32)
+    ptrs = (ctypes.c_void_p * len(srcs))(*[s.ctypes.data for s in srcs])
+    hw = np.array([[s.shape[1], s.shape[2]] for s in srcs], np.int32).ravel()
+    r = None if scale_ratios is None else np.ascontiguousarray(scale_ratios, np.float32)
+    rc = r.ctypes.data if r is not None else None
+    if lib().orc_resize_merge_cuda(out, ptrs, len(srcs), c, hw, dh, dw, rc) != 0:
+        return None
     return out
 
 

@@ -43,6 +43,11 @@ void orc_nms(float* peaks, const float* heat, float threshold, int channels, int
 /* ---- bicubic resize: restates cv::resize(..., INTER_CUBIC) as called by
  * op::resizeAndMergeCpu (src/openpose/net/resizeAndMergeBase.cpp:45-52) --------------------- */
 void orc_resize_cubic(float* dst, const float* src, int sh, int sw, int dh, int dw);
+/* CUDA-build semantics (resizeAndMergeBase.cu / nmsBase.cu; resize.c, nms.c) */
+int orc_resize_merge_cuda(float* dst, const float* const* srcs, int nsrc, int channels,
+                          const int* hw, int dh, int dw, const float* ratios);
+void orc_nms_cuda(float* peaks, const float* heat, float threshold, int channels, int max_peaks1,
+                  int h, int w, float offset_x, float offset_y);
 /* multi-scale: resizeAndMergeBase.cpp:55-106 (each source to the full target, sum, average) */
 void orc_resize_merge(float* dst, const float* const* srcs, int nsrc, int channels,
                       const int* src_hw /* nsrc*2 */, int dh, int dw);

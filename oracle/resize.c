@@ -128,3 +128,82 @@ void orc_resize_merge(float* dst, const float* const* srcs, int nsrc, int channe
     for (long i = 0; i < (long)channels * tplane; ++i) dst[i] = dst[i] * inv;
     free(tmp);
 }
+
+/* ---- resizeAndMergeGpu (CUDA build), src/openpose/net/resizeAndMergeBase.cu ----------------
+ * include/openpose_private/gpu/cuda.hu:92-145: cubicSequentialData (clamped base column x1 =
+ * clamp(floor(xs), 0, w-1), neighbours clamped, dx = xs - x1, possibly negative at the border),
+ * cubicInterpolate (Catmull-Rom, A = -0.5, the polynomial as written), bicubicInterpolate (rows
+ * first, then the column).  Single source: resize8TimesKernel (:105-140), source coordinate
+ * (x + 0.5f) / r - 0.5f, r = ceil(H / h) on both axes (its 5x5 shared window reads the same clamped
+ * rows and columns as bicubicInterpolate); identical sizes: fillKernel (a copy).  Several sources:
+ * resizeAndAddAndAverageKernel (:142-162) with scale (W / w0) / (ratio_i / ratio_0), the sum over
+ * sources in order, then / counter.  Compiled with -ffp-contract=off: every operation rounds (what
+ * nvcc contracts in the polynomial is not reproducible here; parity unpinned). */
+static float cuda_cubic(float v0, float v1, float v2, float v3, float dx)
+{
+    return (-0.5f * v0 + 1.5f * v1 - 1.5f * v2 + 0.5f * v3) * dx * dx * dx +
+           (v0 - 2.5f * v1 + 2.f * v2 - 0.5f * v3) * dx * dx - 0.5f * (v0 - v2) * dx + v1;
+}
+
+static int mini(int a, int b) { return a < b ? a : b; }
+static int maxi(int a, int b) { return a > b ? a : b; }
+
+static float cuda_bicubic(const float* src, float xs, float ys, int sw, int sh)
+{
+    int xi[4], yi[4];
+    xi[1] = clampi((int)floorf(xs), 0, sw - 1);
+    xi[0] = maxi(0, xi[1] - 1);
+    xi[2] = mini(sw - 1, xi[1] + 1);
+    xi[3] = mini(sw - 1, xi[2] + 1);
+    const float dx = xs - (float)xi[1];
+    yi[1] = clampi((int)floorf(ys), 0, sh - 1);
+    yi[0] = maxi(0, yi[1] - 1);
+    yi[2] = mini(sh - 1, yi[1] + 1);
+    yi[3] = mini(sh - 1, yi[2] + 1);
+    const float dy = ys - (float)yi[1];
+    float t[4];
+    for (int i = 0; i < 4; ++i) {
+        const float* r = src + (long)yi[i] * sw;
+        t[i] = cuda_cubic(r[xi[0]], r[xi[1]], r[xi[2]], r[xi[3]], dx);
+    }
+    return cuda_cubic(t[0], t[1], t[2], t[3], dy);
+}
+
+/* dst [channels][dh][dw]; srcs[i] [channels][hw[2i]][hw[2i+1]]; ratios = scaleInputToNetInputs
+ * (several sources only).  Returns 0, or -1 where the reference raises an error. */
+int orc_resize_merge_cuda(float* dst, const float* const* srcs, int nsrc, int channels,
+                          const int* hw, int dh, int dw, const float* ratios)
+{
+    float sx[8], sy[8];
+    if (nsrc < 1 || nsrc > 8) return -1;
+    if (nsrc == 1) {
+        const int sh = hw[0], sw = hw[1];
+        if (dw / sw == 1 && dh / sh == 1) {
+            if (dw != sw || dh != sh) return -1;
+            memcpy(dst, srcs[0], sizeof(float) * (size_t)channels * dh * dw);
+            return 0;
+        }
+        if (dw / sw != 8 || dh / sh != 8) return -1;
+        sx[0] = sy[0] = (float)(unsigned)ceilf(dh / (float)sh);
+    } else {
+        const float mw = dw / (float)hw[1], mh = dh / (float)hw[0];
+        for (int i = 0; i < nsrc; ++i) {
+            const float s = ratios[i] / ratios[0];
+            sx[i] = mw / s;
+            sy[i] = mh / s;
+        }
+    }
+    for (int c = 0; c < channels; ++c)
+        for (int y = 0; y < dh; ++y)
+            for (int x = 0; x < dw; ++x) {
+                float acc = 0.f;
+                for (int i = 0; i < nsrc; ++i) {
+                    const int sh = hw[2 * i], sw = hw[2 * i + 1];
+                    const float xs = ((float)x + 0.5f) / sx[i] - 0.5f;
+                    const float ys = ((float)y + 0.5f) / sy[i] - 0.5f;
+                    acc += cuda_bicubic(srcs[i] + (long)c * sh * sw, xs, ys, sw, sh);
+                }
+                dst[((long)c * dh + y) * dw + x] = nsrc > 1 ? acc / (float)nsrc : acc;
+            }
+    return 0;
+}
