@@ -229,6 +229,25 @@ void NetHip::plan(const std::vector<LayerDesc>& layers)
             a.out32_coff < 0 && b.out32_coff < 0)
             fuse1_ = {steps_[0].idx, steps_[1].idx, steps_[2].idx, abuf, bbuf};
     }
+    // Mconv6 -> Mconv7 head pairs (conv_head.hip)
+    for (size_t si = 0; si + 1 < steps_.size(); ++si) {
+        if (!steps_[si].conv || !steps_[si + 1].conv) continue;
+        ConvPlan& a = convs_[steps_[si].idx];
+        ConvPlan& b = convs_[steps_[si + 1].idx];
+        if (a.info.k != 1 || b.info.k != 1 || a.outs.size() != 1 || a.out32_coff >= 0 ||
+            a.head >= 0 || a.from_image || border_ != 1)
+            continue;
+        const int abuf = a.outs[0].buf;
+        int readers = 0;
+        for (const auto& c : convs_) readers += c.in.buf == abuf;
+        for (const auto& q : pools_) readers += q.in_buf == abuf;
+        if (readers != 1 || b.in.buf != abuf || b.in.coff != a.outs[0].coff || a.outs[0].coff != 0 ||
+            b.info.cin != a.info.cout || !conv_head_supported(a.info.cout, b.info.cout, a.cin_pad))
+            continue;
+        a.head = b.head = (int)heads_.size();
+        heads_.push_back(FuseHead{steps_[si].idx, steps_[si + 1].idx, (int)si, abuf});
+        ++si;
+    }
 }
 
 void NetHip::set_conv(const std::string& name, const float* w, const float* b, const float* slope)
@@ -272,6 +291,24 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
                     packed3[idx] = f2h(w[(((size_t)co * cin + ci) * k + t / k) * k + t % k]);
                 }
     }
+    // conv_head.hip layouts: Mconv6 [cin_pad/32][n1][32]; Mconv7 K-permuted [n2 <= 32 ? 32 : 64][n1]
+    std::vector<uint16_t> packedh;
+    if (c.head >= 0) {
+        const FuseHead& fh = heads_[c.head];
+        if (fh.a == it->second) {
+            const int n1 = c.info.cout, cpt = c.cin_pad / 32;
+            packedh.assign((size_t)cpt * n1 * 32, 0);
+            for (int co = 0; co < n1; ++co)
+                for (int ci = 0; ci < cin; ++ci)
+                    packedh[((size_t)(ci / 32) * n1 + co) * 32 + ci % 32] = f2h(w[(size_t)co * cin + ci]);
+        } else {
+            const int n1 = cin, n2 = c.info.cout;
+            std::vector<uint16_t> w7((size_t)n2 * n1);
+            for (size_t e = 0; e < w7.size(); ++e) w7[e] = f2h(w[e]);
+            packedh.assign((size_t)(n2 <= 32 ? 32 : 64) * n1, 0);
+            conv_head_pack_w7(packedh.data(), w7.data(), n1, n2);
+        }
+    }
     // bias/slope zero-padded to a multiple of 128 channels (conv3 reads whole 4-channel groups)
     const size_t cpad = (size_t)(c.info.cout + 127) / 128 * 128;
     std::vector<float> bias(cpad, 0.f), sl(cpad, 0.f);
@@ -281,6 +318,11 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
     if (!packed3.empty()) {
         void* dw3 = c.w3.get(packed3.size() * 2);
         OPK_HIP(hipMemcpyAsync(dw3, packed3.data(), packed3.size() * 2, hipMemcpyHostToDevice,
+                               ctx_->stream));
+    }
+    if (!packedh.empty()) {
+        void* dwh = c.wh.get(packedh.size() * 2);
+        OPK_HIP(hipMemcpyAsync(dwh, packedh.data(), packedh.size() * 2, hipMemcpyHostToDevice,
                                ctx_->stream));
     }
     void* db = c.bias.get(bias.size() * 4);
@@ -344,9 +386,14 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
     // CONV1_FUSED=0 (opk_dev_set, A/B tests): the three separate kernels instead of the fusion
     S.fused1 = fuse1_.a >= 0 && dev_switch("CONV1_FUSED", 1) != 0 && border_ == 1 &&
                conv1_fused_supported(h, w, 64, 64);
+    // HEAD_FUSE=0 (opk_dev_set, A/B tests): Mconv6 and Mconv7 as two conv3 launches
+    S.fusedh = !heads_.empty() && dev_switch("HEAD_FUSE", 1) != 0;
     for (size_t i = 0; i < bufs_.size(); ++i) {
         S.mem.push_back(std::make_unique<DevBuf>());
         if ((int)i == image_buf_) continue;   // conv_image reads the NCHW input itself
+        bool head_buf = false;
+        for (const auto& fh : heads_) head_buf = head_buf || fh.buf == (int)i;
+        if (S.fusedh && head_buf) continue;   // Mconv6 outputs live only inside conv_head_kernel
         if (S.fused1 && ((int)i == fuse1_.abuf || (int)i == fuse1_.bbuf))
             continue;   // conv1_1 / conv1_2 outputs live only inside conv1_fused_kernel
         // zeroed guards: the kernels read up to W+3 positions before the first frame and up to
@@ -463,6 +510,39 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
         if (s.conv) {
             const ConvPlan& c = convs_[s.idx];
             const ConvArgs& a = S.args[s.idx];
+            if (S.fusedh && c.head >= 0 && heads_[c.head].step == (int)si) {
+                const FuseHead& fh = heads_[c.head];
+                const ConvPlan& cb = convs_[fh.b];
+                const ConvArgs& b = S.args[fh.b];
+                HeadArgs h{};
+                h.in = a.in;
+                h.in_cs = a.in_cs;
+                h.in_coff = a.in_coff;
+                h.cin_pad = a.cin_pad;
+                h.w6 = static_cast<const uint16_t*>(c.wh.ptr);
+                h.b6 = a.bias;
+                h.s6 = a.slope;
+                h.act6 = a.act;
+                h.w7 = static_cast<const uint16_t*>(cb.wh.ptr);
+                h.b7 = b.bias;
+                h.n1 = c.info.cout;
+                h.n2 = cb.info.cout;
+                h.frames = n;
+                h.H = a.H;
+                h.W = a.W;
+                h.ndst = b.ndst;
+                for (int d = 0; d < b.ndst; ++d) {
+                    h.dst[d] = b.dst[d];
+                    h.dst_cs[d] = b.dst_cs[d];
+                    h.dst_coff[d] = b.dst_coff[d];
+                }
+                h.out32 = b.out32;
+                h.out32_c = b.out32_c;
+                h.out32_coff = b.out32_coff;
+                launch_conv_head(h, ctx_->stream);
+                ++si;   // Mconv7 ran inside
+                continue;
+            }
             if (c.from_image) launch_conv_image(a, input, ctx_->stream);
             else launch_conv3(a, ctx_->stream);
         } else {

@@ -63,6 +63,8 @@ private:
         int out32_coff = -1;
         DevBuf w, bias, slope;
         DevBuf w3;            // halo-kernel weight layout (3x3 convs)
+        DevBuf wh;            // conv_head.hip layout when this conv is half of a fused head pair
+        int head = -1;        // index into heads_ (as either half), -1 none
         bool loaded = false;
     };
     struct PoolPlan { int in_buf, out_buf, level_in, channels; };
@@ -77,6 +79,7 @@ private:
         DevBuf out_mem;
         float* out32 = nullptr;
         bool fused1 = false;           // conv1_fused_kernel runs for this shape
+        bool fusedh = false;           // conv_head_kernel runs the fused head pairs
         std::vector<ConvArgs> args;    // per conv
         std::vector<char> use3;        // per conv: launch conv3
     };
@@ -97,6 +100,10 @@ private:
     int image_buf_ = -1;
     struct Fuse1 { int a = -1, b = -1, p = -1, abuf = -1, bbuf = -1; };
     Fuse1 fuse1_;                 // conv1_1 -> conv1_2 -> pool1 (conv1_fused.hip) when planned
+    // Mconv6 -> Mconv7 pairs (conv_head.hip): a = 1x1 conv with 256 / 512 outputs read only by b,
+    // a 1x1 conv with <= 64 outputs, consecutive steps; buf = a's output buffer
+    struct FuseHead { int a = -1, b = -1, step = -1, buf = -1; };
+    std::vector<FuseHead> heads_;
     int cus_ = 256;               // compute units (persistent-kernel grid)
     int border_ = 1;              // zero border of every padded image (widest conv pad, >= 1)
 

@@ -68,6 +68,31 @@ void launch_conv3w(const ConvArgs& a, hipStream_t stream);
 bool conv3w8_supported(const ConvArgs& a);
 void launch_conv3w8(const ConvArgs& a, hipStream_t stream);
 
+// conv_head.hip: Mconv6 (1x1, n1 = 256 / 512 outputs, act6) -> Mconv7 (1x1, n2 <= 64 outputs) in
+// one kernel; the Mconv6 activations never leave the chip.  Input / outputs as ConvArgs (padded
+// NHWC fp16 slices, optional fp32 NCHW out32).  w6: [cin_pad/32][n1][32] fp16; w7: packed by
+// conv_head_pack_w7 ([n2 <= 32 ? 32 : 64][n1], K permuted within 32-channel blocks); b7 zero-padded
+// to 64 floats; b6 / s6 [n1].
+struct HeadArgs {
+    const uint16_t* in;
+    int in_cs, in_coff, cin_pad;
+    const uint16_t* w6;
+    const float *b6, *s6;
+    int act6;
+    const uint16_t* w7;
+    const float* b7;
+    int n1, n2;
+    int frames, H, W;
+    int ndst;
+    uint16_t* dst[kConvMaxDst];
+    int dst_cs[kConvMaxDst], dst_coff[kConvMaxDst];
+    float* out32;
+    int out32_c, out32_coff;
+};
+bool conv_head_supported(int n1, int n2, int cin_pad);
+void conv_head_pack_w7(uint16_t* dst, const uint16_t* w7 /* [n2][n1] */, int n1, int n2);
+void launch_conv_head(const HeadArgs& a, hipStream_t stream);
+
 // First conv (3 input channels, 3x3, cout <= 64) straight from the fp32 NCHW input [frames][3][H][W]
 // (conv_image.hip); weights [cout_pad][64], K order (ky*3 + kx)*3 + ci.
 void launch_conv_image(const ConvArgs& a, const float* image, hipStream_t stream);

@@ -1,0 +1,251 @@
+// conv_head.hip -- a refinement stage's 1x1 head pair in one kernel: Mconv6 (1x1, N1 = 256 / 512
+// outputs, PReLU/ReLU) -> Mconv7 (1x1, <= 64 outputs, no activation).
+//
+// Reference layers: models/pose/body_25/pose_deploy.prototxt Mconv6_stage*_L* / Mconv7_stage*_L*
+// (run by NetCaffe::forwardPass, netCaffe.cpp:248).  Unfused, Mconv6 writes its N1-channel fp16
+// output (264 MB per 64 frames at 46x82 for N1 = 512) and Mconv7 reads it back at HBM speed
+// (profiles/round2: Mconv7 0.1-0.15 TF/s, 6 % of the CNN with Mconv6).  Here the Mconv6 tile never
+// leaves the chip:
+//   phase 1  Mconv6 as the usual implicit GEMM of a 128-position tile (1x1: the tile is its own
+//            halo) x all N1 channels, 8 waves of 64 (or 32) positions x 128 channels, 32-channel K
+//            steps through a 3-slot LDS ring (global_load_lds, swizzled 64-byte rows);
+//   phase 2  bias + activation, fp16, and each wave's 64 x 128 block turned straight into MFMA
+//            B operands: v_permlane16_swap of fragment pairs (j, j+1) gives a lane the 8 channels
+//            16(q&1) + 8(q>>1) .. +7 of a 32-channel block -- a fixed permutation of the K order,
+//            which the host applies to Mconv7's weights instead (conv_head_pack_w7) -- and
+//            Mconv7's weights for the wave's 128 channels come from L2 into registers;
+//   phase 3  the N1/128 partial products of a position block (one per wave column) are summed
+//            through LDS in a fixed order (deterministic), + bias, fp16 into every concat slice and
+//            the fp32 NCHW net output when requested.
+// MFMA f32_16x16x32_f16, C^T arrangement (weights as the A operand) as in conv3.hip.
+#include "conv.h"
+
+#include <algorithm>
+
+#include "../common.h"
+#include "conv3_dev.h"
+
+namespace opk {
+
+namespace {
+
+using namespace conv3dev;
+
+constexpr int kH_BM = 128, kH_NW = 8;
+
+template <int N1, int NF2>
+__global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs a)
+{
+    constexpr int NW = kH_NW, BM = kH_BM;
+    constexpr int WN1 = N1 / 128, WM = NW / WN1, WROWS = BM / WM, MF = WROWS / 16, NF = 8;
+    constexpr int N2P = NF2 * 16;
+    constexpr int ASLOT = BM * 4, BSLOT = N1 * 4;            // 16-byte pieces per ring slot
+    constexpr int RING = 3 * (ASLOT + BSLOT);
+    constexpr int PART = NW * WROWS * N2P / 4;                // partial products (float4 pieces)
+    constexpr int MAIN = RING > PART ? RING : PART;
+    constexpr int LDS_PIECES = MAIN + N1 / 2;                 // + bias / multiplier of Mconv6
+    static_assert(LDS_PIECES * 16 <= 160 * 1024, "LDS budget");
+    static_assert(MF >= 1 && WROWS % 16 == 0, "wave tile");
+    __shared__ uint4 lds[LDS_PIECES];
+    float* lbias = reinterpret_cast<float*>(lds + MAIN);
+    float* lmul = lbias + N1;
+
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int wm = wave / WN1, wn = wave - (wave / WN1) * WN1;
+    const int r16 = lane & 15, q = lane >> 4;
+    const int Hp = a.H + 2, Wp = a.W + 2;
+    const int total = a.frames * Hp * Wp;
+    const int p0 = blockIdx.x * BM;
+
+    for (int i = tid; i < N1; i += 64 * NW) {
+        const float neg = a.act6 == 1 ? 0.f : 1.f;
+        lbias[i] = a.b6[i];
+        lmul[i] = a.act6 == 2 ? a.s6[i] : neg;
+    }
+
+    // ---- phase 1: Mconv6 K loop ------------------------------------------------------------------
+    const int lrow = lane >> 2, phys = lane & 3;
+    const int KS = a.cin_pad >> 5;
+    constexpr int BIW = N1 / 16 / NW;                         // B DMA instructions per wave per step
+    // A DMA: instruction `wave` covers tile rows wave*16 .. +15 (positions past the end read the
+    // zeroed guard after the last frame, conv.h kConvGuardTail)
+    const int arow = wave * 16 + lrow;
+    const uint16_t* asrc = a.in + a.in_coff + (size_t)(p0 + arow) * a.in_cs +
+                           (phys ^ (((arow >> 2) & 1) << 1)) * 8;
+#define OPKH_ISSUE(s_)                                                                        \
+    do {                                                                                      \
+        const int sl_ = (s_) % 3;                                                             \
+        __builtin_amdgcn_global_load_lds((const void*)(asrc + (s_) * 32),                     \
+                                         (__attribute__((address_space(3))) void*)(&lds[sl_ * ASLOT + wave * 64]), \
+                                         16, 0, 0);                                           \
+        const uint16_t* wb_ = a.w6 + (size_t)(s_) * N1 * 32;                                  \
+        _Pragma("unroll") for (int j_ = 0; j_ < BIW; ++j_) {                                  \
+            const int rb_ = (j_ * NW + wave) * 16 + lrow;                                     \
+            __builtin_amdgcn_global_load_lds(                                                 \
+                (const void*)(wb_ + rb_ * 32 + (phys ^ (((rb_ >> 2) & 1) << 1)) * 8),         \
+                (__attribute__((address_space(3))) void*)(&lds[3 * ASLOT + sl_ * BSLOT + (j_ * NW + wave) * 64]), \
+                16, 0, 0);                                                                    \
+        }                                                                                     \
+    } while (0)
+
+    float4_t acc[MF][NF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+
+    OPKH_ISSUE(0);
+    if (KS > 1) OPKH_ISSUE(1);
+    for (int s = 0; s < KS; ++s) {
+        // own DMA of step s landed once only step s+1's (1 + BIW instructions) may be in flight
+        if (s + 1 < KS) vm_wait<1 + BIW>();
+        else vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
+        if (s + 2 < KS) OPKH_ISSUE(s + 2);
+        const uint4* As = lds + (s % 3) * ASLOT;
+        const uint4* Bs = lds + 3 * ASLOT + (s % 3) * BSLOT;
+        half8_t fa[MF], fb[NF];
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+            fa[i] = __builtin_bit_cast(half8_t, As[swz64(wm * WROWS + i * 16 + r16, q)]);
+#pragma unroll
+        for (int j = 0; j < NF; ++j)
+            fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(wn * 128 + j * 16 + r16, q)]);
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+            for (int j = 0; j < NF; ++j)
+                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+#undef OPKH_ISSUE
+
+    // ---- phase 2: activated Mconv6 block -> Mconv7 partial over this wave's 128 channels -------
+    // lane (r16, q) of acc[i][j] holds channels wn*128 + 16j + 4q .. +3 of tile row
+    // wm*WROWS + 16i + r16; after the swap of pair (2kb, 2kb+1) it holds channels
+    // 32kb + 16(q&1) + 8(q>>1) .. +7 = B-operand K elements 8q .. 8q+7 of block kb
+    float4_t acc2[MF][NF2];
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int f = 0; f < NF2; ++f) acc2[i][f] = float4_t{0.f, 0.f, 0.f, 0.f};
+    const float* lb = lbias + wn * 128 + 4 * q;
+    const float* lm = lmul + wn * 128 + 4 * q;
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+        half8_t a7[NF2];
+#pragma unroll
+        for (int f = 0; f < NF2; ++f)
+            a7[f] = *reinterpret_cast<const half8_t*>(a.w7 + (size_t)(f * 16 + r16) * N1 + wn * 128 +
+                                                      kb * 32 + q * 8);
+        float4_t bq[2], mq[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            bq[h] = *reinterpret_cast<const float4_t*>(lb + (2 * kb + h) * 16);
+            mq[h] = *reinterpret_cast<const float4_t*>(lm + (2 * kb + h) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+            uint32_t pk[2][2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float4_t t = acc[i][2 * kb + h] + bq[h];
+                const float4_t tm = t * mq[h];
+                float v[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
+                pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+                pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+            }
+            const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+            const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+            const half8_t b2 = __builtin_bit_cast(half8_t, make_uint4(sl[0], sh[0], sl[1], sh[1]));
+#pragma unroll
+            for (int f = 0; f < NF2; ++f)
+                acc2[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a7[f], b2, acc2[i][f], 0, 0, 0);
+        }
+    }
+
+    // ---- phase 3: sum the wave columns' partials in order, + bias, outputs ---------------------
+    __syncthreads();   // every wave is past its last ring read
+    float4_t* part = reinterpret_cast<float4_t*>(lds);
+    // partial of wave w: [WROWS positions][N2P channels] fp32
+#pragma unroll
+    for (int i = 0; i < MF; ++i)
+#pragma unroll
+        for (int f = 0; f < NF2; ++f)
+            part[(wave * WROWS + i * 16 + r16) * (N2P / 4) + f * 4 + q] = acc2[i][f];
+    __syncthreads();
+    for (int f = wn; f < NF2; f += WN1) {
+        const int ch = f * 16 + 4 * q;   // this lane's 4 output channels
+        if (ch >= a.n2) continue;
+        const float4_t b7 = *reinterpret_cast<const float4_t*>(a.b7 + ch);   // zero-padded to N2P
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+            const int row = wm * WROWS + i * 16 + r16;
+            float4_t v = part[((wm * WN1) * WROWS + row - wm * WROWS) * (N2P / 4) + f * 4 + q];
+            for (int w = 1; w < WN1; ++w)
+                v = v + part[((wm * WN1 + w) * WROWS + row - wm * WROWS) * (N2P / 4) + f * 4 + q];
+            v = v + b7;
+            const int p = p0 + row;
+            if (p >= total) continue;
+            const int fr = p / (Hp * Wp), rem = p - fr * Hp * Wp;
+            const int yy = rem / Wp, xx = rem - yy * Wp;
+            if (yy < 1 || yy > a.H || xx < 1 || xx > a.W) continue;   // border position
+            const int nv = min(4, a.n2 - ch);
+            const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+            const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+            for (int d = 0; d < a.ndst; ++d) {
+                uint16_t* o = a.dst[d] + a.dst_coff[d] + ch + (size_t)p * a.dst_cs[d];
+                if (nv == 4 && ((a.dst_coff[d] | a.dst_cs[d]) & 3) == 0) {
+                    *reinterpret_cast<uint2*>(o) = make_uint2(lo, hi);
+                } else {
+                    for (int e = 0; e < nv; ++e) o[e] = (uint16_t)((e < 2 ? lo : hi) >> (16 * (e & 1)));
+                }
+            }
+            if (a.out32) {
+                float* o = a.out32 + (((size_t)fr * a.out32_c + a.out32_coff + ch) * a.H + yy - 1) * a.W + xx - 1;
+                for (int e = 0; e < nv; ++e) o[(size_t)e * a.H * a.W] = v[e];
+            }
+        }
+    }
+}
+
+}  // namespace
+
+bool conv_head_supported(int n1, int n2, int cin_pad)
+{
+    return (n1 == 256 || n1 == 512) && n2 >= 1 && n2 <= 64 && cin_pad >= 32 && cin_pad % 32 == 0;
+}
+
+void conv_head_pack_w7(uint16_t* dst, const uint16_t* w7, int n1, int n2)
+{
+    // dst [N2P][N1]: within each 32-channel block, K element 8q + e = channel 16(q&1) + 8(q>>1) + e
+    const int n2p = n2 <= 32 ? 32 : 64;
+    for (int o = 0; o < n2p; ++o)
+        for (int k = 0; k < n1; ++k) {
+            const int blk = k / 32, e = k % 8, qq = (k % 32) / 8;
+            const int c = blk * 32 + 16 * (qq & 1) + 8 * (qq >> 1) + e;
+            dst[(size_t)o * n1 + k] = o < n2 ? w7[(size_t)o * n1 + c] : 0;
+        }
+}
+
+void launch_conv_head(const HeadArgs& a, hipStream_t stream)
+{
+    OPK_CHECK_ARG(conv_head_supported(a.n1, a.n2, a.cin_pad), "conv_head: N1 256/512, N2 <= 64");
+    OPK_CHECK_ARG(a.ndst <= kConvMaxDst, "conv_head: too many destinations");
+    const long total = (long)a.frames * (a.H + 2) * (a.W + 2);
+    OPK_CHECK_ARG(total < (1L << 30), "conv_head: too many positions");
+    const unsigned G = (unsigned)((total + kH_BM - 1) / kH_BM);
+    const dim3 blk(64 * kH_NW);
+    if (a.n1 == 512) {
+        if (a.n2 <= 32) hipLaunchKernelGGL((conv_head_kernel<512, 2>), dim3(G), blk, 0, stream, a);
+        else hipLaunchKernelGGL((conv_head_kernel<512, 4>), dim3(G), blk, 0, stream, a);
+    } else {
+        if (a.n2 <= 32) hipLaunchKernelGGL((conv_head_kernel<256, 2>), dim3(G), blk, 0, stream, a);
+        else hipLaunchKernelGGL((conv_head_kernel<256, 4>), dim3(G), blk, 0, stream, a);
+    }
+    OPK_LAUNCH_CHECK();
+}
+
+}  // namespace opk

@@ -324,3 +324,39 @@ def test_coco_pose_pipeline_runs_on_the_net(ctx):
         np.testing.assert_array_equal(got[f][0], kp)
         np.testing.assert_array_equal(got[f][1], ks)
     assert pose.peaks_numpy().shape[1] == 18
+
+
+def test_head_fusion_matches_unfused_and_oracle(ctx):
+    """Mconv6 -> Mconv7 pairs (1x1 to 512 / 256 channels, then 1x1 to <= 64) run as one
+    conv_head_kernel: fp16 outputs into a concat read by a later conv and fp32 net-output channels.
+    Against the two conv3 launches (HEAD_FUSE=0) only the fp32 summation order of Mconv7 differs
+    (per-wave partials summed in a fixed order); against the fp32 oracle the usual tolerance."""
+    L = conv("c0", "image", 64, 3, "relu") + conv("c1", "c0", 96, 3, "prelu")
+    L += conv("m6", "c1", 512, 1, "prelu") + conv("m7", "m6", 52, 1)
+    L += conv("n6", "c1", 256, 1, "relu") + conv("n7", "n6", 26, 1)
+    L.append(dict(name="cat", type="Concat", bottom=["m7", "c1"], top=["cat"]))
+    L += conv("c2", "cat", 32, 3, "relu")
+    L.append(dict(name="net_output", type="Concat", bottom=["n7", "m7", "c2"], top=["net_output"]))
+    text = prototxt.emit(L)
+    graph = prototxt.parse(text)
+    params = synth.he_weights(graph, seed=21)
+    x = np.random.default_rng(22).uniform(-0.5, 0.5, (3, 3, 96, 160)).astype(np.float32)
+    with tempfile.NamedTemporaryFile("w", suffix=".prototxt", delete=False) as f:
+        f.write(text)
+        path = f.name
+    outs = {}
+    try:
+        for name, sw in {"fused": {}, "unfused": {"HEAD_FUSE": 0}}.items():
+            with dev_switches(**sw):
+                net = Net(ctx, path)
+                net.set_params(params)
+                net.forward(torch.from_numpy(x).cuda())
+                outs[name] = net.output_numpy()
+                net.close()
+    finally:
+        os.unlink(path)
+    assert rel_l2(outs["fused"], outs["unfused"]) < 1e-4
+    ref = body25.forward(x, params, graph=graph)
+    assert rel_l2(outs["fused"], ref) < SMALL_TOL
+    for c in range(ref.shape[1]):
+        assert rel_l2(outs["fused"][:, c], ref[:, c]) < CHANNEL_TOL, c
