@@ -10,6 +10,8 @@
 //   op::connectBodyPartsGpu<float|double> (include/openpose/net/bodyPartConnectorBase.hpp:17-24,
 //                                          replaces src/openpose/net/bodyPartConnectorBase.cu)
 // and op::NetHip, an op::Net (include/openpose/net/net.hpp:8-18) with NetCaffe's constructor shape
+// whose output blob is an op::ArrayCpuGpu on HIP memory (arrayCpuGpuHip.cpp, which replaces
+// src/openpose/core/arrayCpuGpu.cpp)
 // (netCaffe.hpp:12-13), for PoseExtractorCaffe::addCaffeNetOnThread (poseExtractorCaffe.cpp:82-86),
 // loading the .caffemodel itself; and the members of op::CvMatToOpInput
 // (include/openpose/core/cvMatToOpInput.hpp:9-28, replaces src/openpose/core/cvMatToOpInput.cpp):
@@ -40,6 +42,7 @@
 #include <openpose/pose/poseParameters.hpp>
 
 #include "opk.h"
+#include "opk_shim.hpp"
 #include "poseExtractorHip.hpp"
 
 #ifndef OPK_SHIM_MAPS
@@ -68,6 +71,15 @@ namespace op
             return ctx.get();
         }
 
+    }
+
+    opk_ctx* opkShimThreadContext()
+    {
+        return threadContext();
+    }
+
+    namespace
+    {
         void check(const int rc, const int line, const char* function)
         {
             if (rc != OPK_OK)
@@ -261,11 +273,10 @@ namespace op
         // NetCaffe returns a live wrapper of its output blob (netCaffe.cpp:263-268), and
         // addCaffeNetOnThread takes it ONCE, right after initializationOnThread and before any
         // forward (poseExtractorCaffe.cpp:94-95), then reads it after every forward.  Here: one
-        // ArrayCpuGpu per net, valid from the first call ({1, C, 1, 1} before a forward) and
-        // refreshed by every forwardPass (Reshape to the new output + host copy).  ArrayCpuGpu
-        // exists only in USE_CAFFE builds (arrayCpuGpu.cpp:23-40); without CUDA their Caffe layers
-        // run the *Cpu functions on cpu_data(), which is what this keeps current.  A Caffe-free
-        // pipeline uses op::PoseExtractorHip instead (below), which never builds this blob.
+        // ArrayCpuGpu per net (the HIP-backed one, arrayCpuGpuHip.cpp), valid from the first call
+        // ({1, C, 1, 1} before a forward) and pointed at the net's device output by every
+        // forwardPass (Reshape + set_gpu_data: gpu_data() is the live buffer, cpu_data() copies it
+        // on demand, as Caffe's SyncedMemory does).
         std::shared_ptr<ArrayCpuGpu<float>> getOutputBlobArray() const
         {
             if (!spOutput)
@@ -287,8 +298,7 @@ namespace op
             int shape[4];
             check(opk_net_output(mNet, &out, shape), __LINE__, __FUNCTION__);
             spOutput->Reshape(shape[0], shape[1], shape[2], shape[3]);
-            check(opk_memcpy_d2h(mCtx, spOutput->mutable_cpu_data(), out,
-                                 (size_t)spOutput->count() * sizeof(float)), __LINE__, __FUNCTION__);
+            spOutput->set_gpu_data(out);
         }
 
         const std::string mProto, mModel;
