@@ -417,6 +417,17 @@ int opk_extractor_set_scales(opk_extractor* ex, int number, float range);
 /* crops per net forward (default 32; batches run in power-of-two sizes) */
 int opk_extractor_set_max_batch(opk_extractor* ex, int max_batch);
 int opk_extractor_parts(opk_extractor* ex);   /* net output channels - 1; -1 for NULL */
+/* per-person heat maps (--heatmaps_add_* with --face / --hand; FaceExtractorNet::getHeatMaps,
+ * HandExtractorNet::getHeatMaps): scale_mode = op::ScaleMode of --heatmaps_scale (-1 off).  The
+ * first `parts` channels of each rectangle's x8-resized crop output, mapped as
+ * updateFaceHeatMapsForPerson / updateHandHeatMapsForPerson do (faceExtractorCaffe.cpp:42-75,
+ * handExtractorCaffe.cpp:126-160): PlusMinusOne(FixedAspect) fastTruncate(v)*2-1, UnsignedChar
+ * (float)positiveIntRound(fastTruncate(v)*255), any other mode fastTruncate(v).  With several hand
+ * scales the last scale's maps are kept (the reference copies its blob after the last net run). */
+int opk_extractor_set_heatmaps(opk_extractor* ex, int scale_mode);
+/* after opk_extractor_forward: device pointer + shape {hands (1 face / 2 hand), people, parts, H,
+ * W}; zeros for the rectangles the reference skips.  Valid until the next forward. */
+int opk_extractor_heatmaps(opk_extractor* ex, const float** heatmaps_dev, int shape[5]);
 /* frames_dev: BGR uint8 [nframes][height][step] on device (step 0: width*3); rects_host as
  * opk_face_detect / opk_hand_detect return them; frame_of_host [people] (NULL: frame 0).
  * keypoints_host: face [people][parts][3], hand [2][people][parts][3] (left hands first), in

@@ -731,12 +731,29 @@ namespace op
                     opk_free(ctx, frame);
             }
 
+            int heatMapScaleMode = -1;   // op::ScaleMode when --heatmaps_add_* asks for maps
+
             void initialize(const int kind, const Point<int>& netSize)
             {
                 ctx = threadContext(gpuId);
                 check(opk_net_create(ctx, proto.c_str(), model.c_str(), &net), __LINE__, __FUNCTION__);
                 check(opk_extractor_create(ctx, net, kind, netSize.x, netSize.y, &ex), __LINE__,
                       __FUNCTION__);
+                check(opk_extractor_set_heatmaps(ex, heatMapScaleMode), __LINE__, __FUNCTION__);
+            }
+
+            // the last forward's per-person heat maps of hand `h` (face: 0) into `heatMaps`
+            // ({people, parts, H, W}, as updateFace/HandHeatMapsForPerson fill it)
+            void copyHeatMaps(Array<float>& heatMaps, const int h)
+            {
+                const float* dev = nullptr;
+                int shape[5];
+                check(opk_extractor_heatmaps(ex, &dev, shape), __LINE__, __FUNCTION__);
+                heatMaps.reset({shape[1], shape[2], shape[3], shape[4]}, 0.f);
+                const size_t bytes = heatMaps.getVolume() * sizeof(float);
+                if (bytes > 0)
+                    check(opk_memcpy_d2h(ctx, heatMaps.getPtr(), dev + (size_t)h * heatMaps.getVolume(),
+                                         bytes), __LINE__, __FUNCTION__);
             }
 
             // inputData (BGR uint8) -> device, rectangles -> keypoints [hands][people][parts][3]
@@ -784,8 +801,8 @@ namespace op
         upImpl{new ImplFaceExtractorCaffe{}}
     {
         (void)enableGoogleLogging;
-        if (!heatMapTypes.empty())
-            error("Face heat maps are not produced by libopk_hip.", __LINE__, __FUNCTION__, __FILE__);
+        if (!heatMapTypes.empty())   // faceExtractorCaffe.cpp:196-198,290-299
+            upImpl->heatMapScaleMode = (int)heatMapScaleMode;
         upImpl->proto = modelFolder + FACE_PROTOTXT;
         upImpl->model = modelFolder + FACE_TRAINED_MODEL;
         upImpl->gpuId = gpuId;
@@ -816,6 +833,8 @@ namespace op
                 if (keypoints.size() != mFaceKeypoints.getVolume())
                     error("The face net does not have 70 parts.", __LINE__, __FUNCTION__, __FILE__);
                 std::copy(keypoints.begin(), keypoints.end(), mFaceKeypoints.getPtr());
+                if (!mHeatMapTypes.empty())
+                    upImpl->copyHeatMaps(mHeatMaps, 0);
             }
             else
                 mFaceKeypoints.reset();
@@ -837,8 +856,8 @@ namespace op
         upImpl{new ImplHandExtractorCaffe{}}
     {
         (void)enableGoogleLogging;
-        if (!heatMapTypes.empty())
-            error("Hand heat maps are not produced by libopk_hip.", __LINE__, __FUNCTION__, __FILE__);
+        if (!heatMapTypes.empty())   // handExtractorCaffe.cpp:327-332,433-441
+            upImpl->heatMapScaleMode = (int)heatMapScaleMode;
         upImpl->proto = modelFolder + HAND_PROTOTXT;
         upImpl->model = modelFolder + HAND_TRAINED_MODEL;
         upImpl->gpuId = gpuId;
@@ -878,6 +897,8 @@ namespace op
                         error("The hand net does not have 21 parts.", __LINE__, __FUNCTION__, __FILE__);
                     std::copy(keypoints.begin() + hand * half, keypoints.begin() + (hand + 1) * half,
                               mHandKeypoints[hand].getPtr());
+                    if (!mHeatMapTypes.empty())
+                        upImpl->copyHeatMaps(mHeatMaps[hand], hand);
                 }
             }
             else

@@ -93,6 +93,8 @@ _SIGS = {
     "opk_extractor_destroy": (_i, [_p]),
     "opk_extractor_set_scales": (_i, [_p, _i, _f]),
     "opk_extractor_set_max_batch": (_i, [_p, _i]),
+    "opk_extractor_set_heatmaps": (_i, [_p, _i]),
+    "opk_extractor_heatmaps": (_i, [_p, _p, _ip]),
     "opk_extractor_parts": (_i, [_p]),
     "opk_extractor_forward": (_i, [_p, _p, _i, _i, _i, _c.c_size_t, _p, _p, _i, _p]),
     "opk_extractor_crop_count": (_i, [_p]),

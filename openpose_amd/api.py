@@ -662,6 +662,22 @@ class KeypointExtractor:
     def set_max_batch(self, b):
         check(self.L.opk_extractor_set_max_batch(self.h, b))
 
+    def set_heatmaps(self, scale_mode):
+        """Per-person heat maps with op::ScaleMode scale_mode (-1 off; opk_extractor_set_heatmaps)."""
+        check(self.L.opk_extractor_set_heatmaps(self.h, scale_mode))
+
+    def heatmaps_numpy(self):
+        """The last forward's heat maps: face [people, parts, H, W], hand [2, people, parts, H, W]."""
+        p = ctypes.c_void_p()
+        shape = (ctypes.c_int * 5)()
+        check(self.L.opk_extractor_heatmaps(self.h, ctypes.byref(p), shape))
+        dims = tuple(shape)
+        out = np.zeros(dims, np.float32)
+        if out.size:
+            check(self.L.opk_memcpy_d2h(self.ctx.h, out.ctypes.data_as(ctypes.c_void_p), p,
+                                        out.nbytes))
+        return out[0] if self.kind == FACE else out
+
     def forward(self, frames, rectangles, frame_of=None):
         """frames: BGR uint8 [n, h, w, 3] CUDA tensor; rectangles [people, 4] (face) or
         [people, 2, 4] (hand); frame_of [people] or None.  Returns face [people, parts, 3] or

@@ -503,6 +503,22 @@ int opk_extractor_set_max_batch(opk_extractor* ex, int max_batch)
 
 int opk_extractor_parts(opk_extractor* ex) { return ex ? ex->ex->parts() : -1; }
 
+int opk_extractor_set_heatmaps(opk_extractor* ex, int scale_mode)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ex, "NULL extractor");
+        ex->ex->set_heatmaps(scale_mode);
+    });
+}
+
+int opk_extractor_heatmaps(opk_extractor* ex, const float** heatmaps_dev, int shape[5])
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(ex && heatmaps_dev && shape, "NULL argument");
+        *heatmaps_dev = ex->ex->heatmaps(shape);
+    });
+}
+
 int opk_extractor_forward(opk_extractor* ex, const uint8_t* frames, int nframes, int width,
                           int height, size_t step, const float* rects, const int* frame_of,
                           int people, float* keypoints)

@@ -185,6 +185,19 @@ void KeypointExtractor::set_max_batch(int b)
     max_batch_ = b;
 }
 
+void KeypointExtractor::set_heatmaps(int scale_mode)
+{
+    OPK_CHECK_ARG(scale_mode >= -1 && scale_mode <= 8, "unknown ScaleMode");
+    heat_mode_ = scale_mode;
+}
+
+const float* KeypointExtractor::heatmaps(int shape[5]) const
+{
+    OPK_CHECK_ARG(heat_mode_ >= 0, "heat maps not enabled (set_heatmaps)");
+    for (int i = 0; i < 5; ++i) shape[i] = heat_shape_[i];
+    return static_cast<const float*>(heat_out_.ptr);
+}
+
 void KeypointExtractor::extract(const uint8_t* frames, int nframes, int w, int h, size_t step,
                                 const Rect* rects, const int* frame_of, int people,
                                 float* keypoints)
@@ -199,6 +212,7 @@ void KeypointExtractor::extract(const uint8_t* frames, int nframes, int w, int h
     OPK_CHECK_ARG(P > 0, "net has no part channels");
     std::memset(keypoints, 0, sizeof(float) * (size_t)hands * people * P * 3);
     crop_m_.clear();
+    for (int i = 0; i < 5; ++i) heat_shape_[i] = 0;
     if (people == 0) return;
     OPK_CHECK_ARG(rects, "NULL rectangles");
 
@@ -265,8 +279,18 @@ void KeypointExtractor::extract(const uint8_t* frames, int nframes, int w, int h
                           tw);
 
     // 3. net on batches of crops (power-of-two sizes, so at most log2(max_batch) + 1 plans),
-    //    each followed by its resize x8 + per-part maximum (evaluated lazily, heat_dev.h)
+    //    each followed by its resize x8 + per-part maximum (evaluated lazily, heat_dev.h) and, on
+    //    request, its per-person heat maps (the last scale of each rectangle)
     float* peaks = static_cast<float*>(peaks_.get((size_t)n * P * 3 * sizeof(float)));
+    float* heat_out = nullptr;
+    int* slots = nullptr;
+    if (heat_mode_ >= 0) {
+        std::vector<int> hs(n);
+        for (int i = 0; i < n; ++i)
+            hs[i] = crops[i].scale == scales_ - 1 ? crops[i].hand * people + crops[i].person : -1;
+        slots = static_cast<int*>(heat_slots_.get((size_t)n * sizeof(int)));
+        OPK_HIP(hipMemcpyAsync(slots, hs.data(), hs.size() * sizeof(int), hipMemcpyHostToDevice, s));
+    }
     for (int done = 0; done < n;) {
         int b = 1;
         while (b * 2 <= std::min(max_batch_, n - done)) b *= 2;
@@ -281,6 +305,16 @@ void KeypointExtractor::extract(const uint8_t* frames, int nframes, int w, int h
         const auto& t = ctx_->tables(oh, ow, heat.h, heat.w);
         heat.src[0] = ResizeSource{net_->output(), oh, ow, t.yofs, t.ycoef, t.xofs, t.xcoef};
         launch_heat_argmax(peaks + (size_t)done * P * 3, heat, b, P, s);
+        if (heat_mode_ >= 0) {
+            if (!heat_out) {
+                const int sh[5] = {hands, people, P, heat.h, heat.w};
+                std::copy(sh, sh + 5, heat_shape_);
+                const size_t bytes = (size_t)hands * people * P * heat.h * heat.w * sizeof(float);
+                heat_out = static_cast<float*>(heat_out_.get(bytes));
+                OPK_HIP(hipMemsetAsync(heat_out, 0, bytes, s));
+            }
+            launch_crop_heatmaps(heat_out, heat, slots + done, b, P, heat_mode_, s);
+        }
         done += b;
     }
     float* hp = static_cast<float*>(hpeaks_.get((size_t)n * P * 3 * sizeof(float)));

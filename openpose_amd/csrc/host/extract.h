@@ -35,6 +35,12 @@ public:
     // hand multi-scale detection (--hand_scale_number, --hand_scale_range)
     void set_scales(int number, float range);
     void set_max_batch(int b);
+    // per-person heat maps (--heatmaps_add_* with --face / --hand): scale_mode = op::ScaleMode of
+    // --heatmaps_scale, -1 off.  After extract(): [hands][people][parts][H][W] on device (H, W =
+    // net output x 8); a rectangle the reference skips leaves zeros; with several hand scales the
+    // last scale's maps are kept, as the reference's blob holds the last net run
+    void set_heatmaps(int scale_mode);
+    const float* heatmaps(int shape[5]) const;
 
     // frames: BGR uint8 [nframes][h][step] on device; rects on the host: face [people],
     // hand [people][2]; frame_of[people] (NULL: all frame 0).  keypoints (host): face
@@ -63,6 +69,9 @@ private:
     DevBuf inputs_, tabs_, peaks_;
     HostBuf hpeaks_;
     std::vector<double> crop_m_;
+    int heat_mode_ = -1;
+    DevBuf heat_out_, heat_slots_;
+    int heat_shape_[5] = {0, 0, 0, 0, 0};
 };
 
 }  // namespace opk

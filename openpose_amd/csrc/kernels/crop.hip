@@ -60,6 +60,43 @@ __global__ __launch_bounds__(256) void heat_argmax_kernel(float* __restrict__ pe
 
 }  // namespace
 
+// per-crop heat maps of FaceExtractorCaffe / HandExtractorCaffe (updateFaceHeatMapsForPerson,
+// faceExtractorCaffe.cpp:42-75; updateHandHeatMapsForPerson, handExtractorCaffe.cpp:126-160): the
+// first `parts` channels of the crop's x8 resize, through the heat-map ScaleMode -- PlusMinusOne(
+// FixedAspect): fastTruncate(v) * 2 - 1; UnsignedChar: (float)positiveIntRound(fastTruncate(v) *
+// 255); any other mode: fastTruncate(v) -- into dst[slot[crop]]; crops with slot -1 are skipped
+__global__ __launch_bounds__(256) void crop_heatmaps_kernel(float* __restrict__ dst, const HeatMap M,
+                                                            const int* __restrict__ slot, int parts,
+                                                            int scale_mode)
+{
+    const int crop = blockIdx.z, part = blockIdx.y;
+    const int sl = slot[crop];
+    if (sl < 0) return;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int hw = M.h * M.w;
+    if (i >= hw) return;
+    const int y = i / M.w, x = i - y * M.w;
+    const float v = heat_at(M, crop * M.channels + part, x, y);
+    const float m = 0.f > v ? 0.f : v;           // fastTruncate(v, 0, 1) = fastMin(1, fastMax(0, v))
+    const float t = 1.f < m ? 1.f : m;
+    float o;
+    if (scale_mode == 5 || scale_mode == 6) o = t * 2.f - 1.f;
+    else if (scale_mode == 7) o = (float)(int)(t * 255.f + 0.5f);
+    else o = t;
+    dst[((size_t)sl * parts + part) * hw + i] = o;
+}
+
+void launch_crop_heatmaps(float* dst, const HeatMap& heat, const int* slot_dev, int crops, int parts,
+                          int scale_mode, hipStream_t stream)
+{
+    OPK_CHECK_ARG(crops > 0 && parts > 0 && parts <= heat.channels, "bad crops / parts");
+    const long hw = (long)heat.h * heat.w;
+    OPK_CHECK_ARG(hw < (1L << 31), "heat map too large");
+    hipLaunchKernelGGL(crop_heatmaps_kernel, dim3((unsigned)((hw + 255) / 256), parts, crops), dim3(256),
+                       0, stream, dst, heat, slot_dev, parts, scale_mode);
+    OPK_LAUNCH_CHECK();
+}
+
 void launch_heat_argmax(float* peaks, const HeatMap& heat, int crops, int parts, hipStream_t stream)
 {
     OPK_CHECK_ARG(crops > 0 && parts > 0 && parts <= heat.channels, "bad crops / parts");

@@ -95,6 +95,10 @@ void launch_cvmat_to_input(float* dst, const uint8_t* src, int n, int sh, int sw
 // peaks [crops][parts][3] = (x, y, value) of the maximum of each of the first `parts` channels of
 // `heat` (frames = crops), the first in raster order among equal values (cv::minMaxLoc)
 void launch_heat_argmax(float* peaks, const HeatMap& heat, int crops, int parts, hipStream_t stream);
+// dst[slot[c]][parts][heat.h][heat.w] = ScaleMode-mapped first `parts` channels of crop c (slot -1:
+// none), as FaceExtractorCaffe / HandExtractorCaffe store their per-person heat maps
+void launch_crop_heatmaps(float* dst, const HeatMap& heat, const int* slot_dev, int crops, int parts,
+                          int scale_mode, hipStream_t stream);
 
 // ---- elementwise helpers (misc.hip) -----------------------------------------------------------
 void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stream);

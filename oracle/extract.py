@@ -176,3 +176,19 @@ def average_score(kp):   # getAverageScore (float accumulation)
     for v in np.asarray(kp, f32)[:, 2]:
         s = f32(s + v)
     return f32(s / f32(kp.shape[0]))
+
+
+def crop_heatmaps(net_out, parts, scale_mode):
+    """updateFaceHeatMapsForPerson / updateHandHeatMapsForPerson (faceExtractorCaffe.cpp:42-75,
+    handExtractorCaffe.cpp:126-160) on one crop's net output [C, h, w]: the first `parts`
+    channels of the x8 resize, fastTruncate to [0, 1], then *2-1 (PlusMinusOne, 5 / 6),
+    (float)positiveIntRound(* 255) (UnsignedChar, 7) or as is (any other ScaleMode), in float."""
+    c, h, w = net_out.shape
+    heat = oracle.resize_merge([net_out], h * 8, w * 8)[:parts]
+    m = np.where(f32(0) > heat, f32(0), heat).astype(f32)       # fastMax(0, v)
+    t = np.where(f32(1) < m, f32(1), m).astype(f32)             # fastMin(1, .)
+    if scale_mode in (5, 6):
+        return (t * f32(2) - f32(1)).astype(f32)
+    if scale_mode == 7:
+        return np.trunc((t * f32(255)).astype(f32) + f32(0.5)).astype(f32)
+    return t

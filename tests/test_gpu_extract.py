@@ -51,9 +51,12 @@ def test_face_extractor_matches_oracle(ctx):
                       [300.75, 20.5, 97.5, 97.5],
                       [200.0, 100.0, 233.0, 233.0]], np.float32)
     frame_of = np.array([0, 1, 0, 1, 0], np.int32)
+    ex.set_heatmaps(7)   # --heatmaps_add_parts --heatmaps_scale 3 (UnsignedChar)
     kp = ex.forward(frames.cuda(), rects, frame_of)
     parts = ex.parts
     assert parts == 70 and kp.shape == (5, 70, 3)
+    hm = ex.heatmaps_numpy()
+    assert hm.shape == (5, 70, 368, 368)
     valid = [0, 1, 3, 4]   # four crops: one batch of 4, the net output holds all of them
     want_ms = [ox.face_affine(rects[i], 368) for i in valid]
     assert ox.face_affine(rects[2], 368) is None
@@ -64,7 +67,8 @@ def test_face_extractor_matches_oracle(ctx):
     for j, i in enumerate(valid):
         want = ox.keypoints_from_output(out[j], want_ms[j], parts)
         np.testing.assert_array_equal(kp[i], want)
-    assert not kp[2].any()
+        np.testing.assert_array_equal(hm[i], ox.crop_heatmaps(out[j], parts, 7))
+    assert not kp[2].any() and not hm[2].any()
 
 
 @pytest.mark.parametrize("res,scales", [((368, 368), 1), ((320, 256), 2)])
@@ -77,9 +81,13 @@ def test_hand_extractor_matches_oracle(ctx, res, scales):
     rects = np.array([[[50.5, 40.0, 80.0, 80.0], [250.25, 120.0, 61.0, 61.0]],
                       [[350.0, -20.0, 90.0, 90.0], [0.0, 0.0, 3.0, 3.0]]],   # last: area <= 10
                      np.float32)
+    mode = 5 if scales > 1 else 8   # PlusMinusOne / NoScale
+    ex.set_heatmaps(mode)
     kp = ex.forward(frames.cuda(), rects)
     parts = ex.parts
     assert parts == 21 and kp.shape == (2, 2, 21, 3)
+    hm = ex.heatmaps_numpy()
+    assert hm.shape == (2, 2, 21, res[1], res[0])
     side = min(res)
     crops, owners = [], []
     for hand in range(2):
@@ -107,7 +115,13 @@ def test_hand_extractor_matches_oracle(ctx, res, scales):
     for (hand, p), est in best.items():
         if all(owners[j] != (hand, p) for j in range(first)):   # owner's crops all in the batch
             np.testing.assert_array_equal(kp[hand, p], est)
-    assert not kp[1, 1].any()
+    # heat maps: the LAST scale's crop of each rectangle (handExtractorCaffe.cpp:433-441)
+    for j in range(first, len(crops)):
+        last = j == len(crops) - 1 or owners[j + 1] != owners[j]
+        if last:
+            hand, p = owners[j]
+            np.testing.assert_array_equal(hm[hand, p], ox.crop_heatmaps(out[j - first], parts, mode))
+    assert not kp[1, 1].any() and not hm[1, 1].any()
 
 
 def test_batches_are_independent(ctx):
