@@ -441,6 +441,60 @@ int opk_extractor_forward(opk_extractor* ex, const uint8_t* frames_dev, int nfra
 int opk_extractor_crop_count(opk_extractor* ex);
 int opk_extractor_crop(opk_extractor* ex, int i, double* matrix_host, const float** input_dev);
 
+/* ---- Renderers (enqueued on the context's stream).  frame_dev: the reference's float BGR frame
+ *      [height][width][3] (0..255), drawn in place.
+ * opk_render_pose_keypoints replaces op::renderPoseKeypointsGpu
+ *   (include/openpose/pose/renderPose.hpp:14-18; src/openpose/pose/renderPose.cu:609-748 with
+ *   renderKeypointsOld, include/openpose_private/utilities/render.hu:209-383): pose_dev
+ *   [people][parts][3] (x, y, score) in frame pixels; every PoseModel, its pairs / colors / scales
+ *   (pose/poseParametersRender.hpp), radius min(w,h)/100, line width min(w,h)/120; nothing is
+ *   drawn for people == 0 unless blend_original == 0 (then the frame is cleared).  Errors as the
+ *   reference: googly eyes with MPI, people > 127 (POSE_MAX_PEOPLE), an unknown model.  The
+ *   reference's maxPtr / minPtr / scalePtr scratch is internal here.
+ * opk_render_face_keypoints / opk_render_hand_keypoints replace op::renderFaceKeypointsGpu /
+ *   op::renderHandKeypointsGpu (face/renderFace.hpp:12-15, hand/renderHand.hpp:12-15): 70 / 21
+ *   parts, radius min/120 / min/100, line min/250 / min/80, no-op for count <= 0.
+ * Keypoint renders take up to 1024 people (faces, hands) per call.
+ * Heat-map renders (alpha outside [0, 1]: "Alpha must be in the range [0, 1]."; heat_dev
+ *   [channels][heat_h][heat_w]; frame pixel x samples (x + 0.5) / scale_to_keep_ratio - 0.5):
+ *   opk_render_pose_heat_map  = op::renderPoseHeatMapGpu  (renderPose.hpp:20-23): channel `part`,
+ *                               bicubic, getColorHeatMap;
+ *   opk_render_pose_heat_maps = op::renderPoseHeatMapsGpu (:25-28): every body part, nearest
+ *                               sample, COCO colors;
+ *   opk_render_pose_paf       = op::renderPosePAFGpu      (:30-33): PAF channels part, part + 1,
+ *                               bilinear;
+ *   opk_render_pose_pafs      = op::renderPosePAFsGpu     (:35-38): every PAF, from channel
+ *                               parts + background;
+ *   opk_render_pose_distance  = op::renderPoseDistanceGpu (:40-42): channel `part`, |bicubic|.
+ * Arithmetic follows the reference expression by expression (each operation rounded); atan2f /
+ * sinf / cosf are the HIP device library's (render parity unpinned at limb edges and for PAF
+ * colours). */
+int opk_render_pose_keypoints(opk_ctx* ctx, float* frame_dev, int pose_model, int people,
+                              unsigned width, unsigned height, const float* pose_dev,
+                              float render_threshold, int googly_eyes, int blend_original,
+                              float alpha);
+int opk_render_face_keypoints(opk_ctx* ctx, float* frame_dev, unsigned width, unsigned height,
+                              const float* face_dev, int people, float render_threshold,
+                              float alpha);
+int opk_render_hand_keypoints(opk_ctx* ctx, float* frame_dev, unsigned width, unsigned height,
+                              const float* hands_dev, int hands, float render_threshold,
+                              float alpha);
+int opk_render_pose_heat_map(opk_ctx* ctx, float* frame_dev, unsigned width, unsigned height,
+                             const float* heat_dev, int heat_w, int heat_h,
+                             float scale_to_keep_ratio, unsigned part, float alpha);
+int opk_render_pose_heat_maps(opk_ctx* ctx, float* frame_dev, int pose_model, unsigned width,
+                              unsigned height, const float* heat_dev, int heat_w, int heat_h,
+                              float scale_to_keep_ratio, float alpha);
+int opk_render_pose_paf(opk_ctx* ctx, float* frame_dev, int pose_model, unsigned width,
+                        unsigned height, const float* heat_dev, int heat_w, int heat_h,
+                        float scale_to_keep_ratio, int part, float alpha);
+int opk_render_pose_pafs(opk_ctx* ctx, float* frame_dev, int pose_model, unsigned width,
+                         unsigned height, const float* heat_dev, int heat_w, int heat_h,
+                         float scale_to_keep_ratio, float alpha);
+int opk_render_pose_distance(opk_ctx* ctx, float* frame_dev, unsigned width, unsigned height,
+                             const float* heat_dev, int heat_w, int heat_h,
+                             float scale_to_keep_ratio, unsigned part, float alpha);
+
 #ifdef __cplusplus
 }
 #endif

@@ -34,6 +34,14 @@ _SIGS = {
     "opk_memset": (_i, [_p, _p, _i, _c.c_size_t]),
     "opk_memcpy_h2d": (_i, [_p, _p, _p, _c.c_size_t]),
     "opk_memcpy_d2h": (_i, [_p, _p, _p, _c.c_size_t]),
+    "opk_render_pose_keypoints": (_i, [_p, _p, _i, _i, _c.c_uint, _c.c_uint, _p, _f, _i, _i, _f]),
+    "opk_render_face_keypoints": (_i, [_p, _p, _c.c_uint, _c.c_uint, _p, _i, _f, _f]),
+    "opk_render_hand_keypoints": (_i, [_p, _p, _c.c_uint, _c.c_uint, _p, _i, _f, _f]),
+    "opk_render_pose_heat_map": (_i, [_p, _p, _c.c_uint, _c.c_uint, _p, _i, _i, _f, _c.c_uint, _f]),
+    "opk_render_pose_heat_maps": (_i, [_p, _p, _i, _c.c_uint, _c.c_uint, _p, _i, _i, _f, _f]),
+    "opk_render_pose_paf": (_i, [_p, _p, _i, _c.c_uint, _c.c_uint, _p, _i, _i, _f, _i, _f]),
+    "opk_render_pose_pafs": (_i, [_p, _p, _i, _c.c_uint, _c.c_uint, _p, _i, _i, _f, _f]),
+    "opk_render_pose_distance": (_i, [_p, _p, _c.c_uint, _c.c_uint, _p, _i, _i, _f, _c.c_uint, _f]),
     "opk_resize_and_merge": (_i, [_p, _p, _c.POINTER(_p), _i, _ip, _ip, _fp]),
     "opk_nms": (_i, [_p, _p, _p, _p, _f, _ip, _ip, _f, _f]),
     "opk_nms_semantics": (_i, [_p, _p, _p, _p, _f, _ip, _ip, _f, _f, _i]),

@@ -134,6 +134,52 @@ class Context:
                                        int4(peaks.shape), int4(heat.shape), offset[0], offset[1],
                                        semantics))
 
+    # ---- renderers (renderPose.cu / renderFace.cu / renderHand.cu) ---------------------------
+    # frame: float32 CUDA [h, w, 3] BGR, drawn in place; keypoints float32 CUDA [people, parts, 3]
+    def render_pose_keypoints(self, frame, pose, pose_model=BODY_25, threshold=0.05,
+                              googly_eyes=False, blend_original=True, alpha=0.6):
+        """op::renderPoseKeypointsGpu (POSE_DEFAULT_ALPHA_KEYPOINT 0.6)."""
+        h, w = frame.shape[:2]
+        people = 0 if pose is None else pose.shape[0]
+        check(self.L.opk_render_pose_keypoints(self.h, _ptr(frame), pose_model, people, w, h,
+                                               None if pose is None else _ptr(pose), threshold,
+                                               int(googly_eyes), int(blend_original), alpha))
+
+    def render_face_keypoints(self, frame, face, threshold=0.4, alpha=0.6):
+        """op::renderFaceKeypointsGpu; face [people, 70, 3]."""
+        h, w = frame.shape[:2]
+        check(self.L.opk_render_face_keypoints(self.h, _ptr(frame), w, h, _ptr(face), face.shape[0],
+                                               threshold, alpha))
+
+    def render_hand_keypoints(self, frame, hands, threshold=0.2, alpha=0.6):
+        """op::renderHandKeypointsGpu; hands [n, 21, 3]."""
+        h, w = frame.shape[:2]
+        check(self.L.opk_render_hand_keypoints(self.h, _ptr(frame), w, h, _ptr(hands),
+                                               hands.shape[0], threshold, alpha))
+
+    def render_heat_map(self, frame, heat, scale, part, alpha=0.7, distance=False):
+        """op::renderPoseHeatMapGpu (distance: op::renderPoseDistanceGpu); heat [C, hh, hw]."""
+        h, w = frame.shape[:2]
+        fn = self.L.opk_render_pose_distance if distance else self.L.opk_render_pose_heat_map
+        check(fn(self.h, _ptr(frame), w, h, _ptr(heat), heat.shape[-1], heat.shape[-2], scale,
+                 part, alpha))
+
+    def render_heat_maps(self, frame, heat, scale, pose_model=BODY_25, alpha=0.7):
+        """op::renderPoseHeatMapsGpu."""
+        h, w = frame.shape[:2]
+        check(self.L.opk_render_pose_heat_maps(self.h, _ptr(frame), pose_model, w, h, _ptr(heat),
+                                               heat.shape[-1], heat.shape[-2], scale, alpha))
+
+    def render_pafs(self, frame, heat, scale, part=None, pose_model=BODY_25, alpha=0.7):
+        """op::renderPosePAFGpu (part = its x channel) or, part None, op::renderPosePAFsGpu."""
+        h, w = frame.shape[:2]
+        if part is None:
+            check(self.L.opk_render_pose_pafs(self.h, _ptr(frame), pose_model, w, h, _ptr(heat),
+                                              heat.shape[-1], heat.shape[-2], scale, alpha))
+        else:
+            check(self.L.opk_render_pose_paf(self.h, _ptr(frame), pose_model, w, h, _ptr(heat),
+                                             heat.shape[-1], heat.shape[-2], scale, part, alpha))
+
     def paf_scores(self, scores, heat, peaks, pose_model=BODY_25, inter_th=CONNECT_INTER_THRESHOLD,
                    inter_min_above=CONNECT_INTER_MIN_ABOVE_THRESHOLD, nms_th=NMS_THRESHOLD):
         n, c, h, w = heat.shape

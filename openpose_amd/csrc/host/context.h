@@ -39,6 +39,14 @@ struct Context {
     std::map<std::tuple<uint64_t, int, int>, std::unique_ptr<WarpAxes>> warp_axes;
     const WarpAxes& warp_axis_tables(double scale, int dw, int dh);
 
+    // renderers (host/render.cpp): device copies of the render tables (render_tables.inc) and the
+    // per-person geometry scratch of launch_render_keypoints
+    struct RenderDev { DevBuf buf; const unsigned* pairs; const float* scales; const float* colors;
+                       int npairs, nscales, ncolors; };
+    std::map<int, std::unique_ptr<RenderDev>> render_dev;
+    const RenderDev& render_table(int which);
+    DevBuf render_geom;
+
     DevBuf scratch_scores;   // dense pair scores for opk_connect_body_parts
     // NMS candidate lists (nms.hip), zeroed when (re)allocated; the kernels keep them zeroed
     DevBuf nms_scratch;

@@ -100,6 +100,42 @@ void launch_heat_argmax(float* peaks, const HeatMap& heat, int crops, int parts,
 void launch_crop_heatmaps(float* dst, const HeatMap& heat, const int* slot_dev, int crops, int parts,
                           int scale_mode, hipStream_t stream);
 
+// ---- renderers (render.hip) -----------------------------------------------------------------
+constexpr int kRenderMaxPeople = 1024;   // people (faces, hands) per frame one launch draws
+// One keypoint render (renderKeypointsOld / renderKeypoints, render.hu): frame float BGR [h][w][3]
+// in place; kp [people][parts][3]; pairs / colors (RGB) / scales on the device; geom scratch of
+// render_geom_floats(people, parts, npairs) floats; eye1 / eye2 the googly-eye parts or -1.
+struct RenderKeypointsArgs {
+    float* frame;
+    int w, h;
+    const float* kp;
+    int people, parts;
+    const unsigned* pairs;
+    int npairs;
+    const float* colors;
+    int ncolors;
+    const float* scales;
+    int nscales;
+    float radius, line_width, threshold, alpha;
+    int blend, eye1, eye2;
+    float* geom;
+};
+size_t render_geom_floats(int people, int parts, int npairs);
+void launch_render_keypoints(const RenderKeypointsArgs& a, hipStream_t stream);
+// heat-map renders: frame [h][w][3] BGR; heat [channels][hh][hw]; target pixel x samples the heat
+// map at (x + 0.5) / scale - 0.5
+struct RenderHeatArgs {
+    float* frame;
+    int w, h;
+    const float* heat;
+    int hw, hh;
+    float scale, alpha;
+};
+void launch_render_heat_map(const RenderHeatArgs& a, int part, bool abs_value, hipStream_t stream);
+void launch_render_heat_maps(const RenderHeatArgs& a, int parts, const float* colors, int ncolors,
+                             hipStream_t stream);
+void launch_render_pafs(const RenderHeatArgs& a, int first, int count, hipStream_t stream);
+
 // ---- elementwise helpers (misc.hip) -----------------------------------------------------------
 void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stream);
 // getHeatMapsCopy: dst [frames][nsel][hw] from heat [frames][channels][hw]; sel_dev = nsel source

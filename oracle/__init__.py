@@ -72,6 +72,11 @@ def lib():
         L.orc_warp_affine_inv.argtypes = [_f32p, _u8p, _i, _i,
                                           np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS"),
                                           _i, _i, _i]
+        L.orc_render_keypoints.argtypes = [_f32p, _i, _i, _f32p, _i, _i, _u32p, _i, _f32p, _i,
+                                           _f32p, _i, _f, _f, _f, _f, _i, _i, _i, _u8p]
+        L.orc_render_heat_map.argtypes = [_f32p, _i, _i, _f32p, _i, _i, _f, _i, _f, _i]
+        L.orc_render_heat_maps.argtypes = [_f32p, _i, _i, _f32p, _i, _i, _f, _i, _f32p, _i, _f]
+        L.orc_render_pafs.argtypes = [_f32p, _i, _i, _f32p, _i, _i, _f, _i, _i, _f]
         _LIB = L
     return _LIB
 
@@ -360,4 +365,72 @@ def maxpool(x, k=2, s=2):
     ow = -(-(w - k) // s) + 1
     out = np.empty((n, c, oh, ow), np.float32)
     lib().orc_maxpool(out, np.ascontiguousarray(x), n, c, h, w, k, s, oh, ow)
+    return out
+
+
+# ---- renderers (render.c) ---------------------------------------------------------------------
+# renderPoseKeypointsGpu's model -> (render table, scales table, parts, googly eyes)
+# (renderPose.cu:129-417, 639-741); face / hand (renderFace.cu:21-46, renderHand.cu:21-46)
+RENDER_POSE = {0: ("BODY_25", "BODY_25", 25, (15, 16)), 7: ("BODY_25", "BODY_25", 25, (15, 16)),
+               9: ("BODY_25", "BODY_25", 25, (15, 16)), 1: ("COCO", "COCO", 18, (14, 15)),
+               2: ("MPI", "COCO", 15, (-1, -1)), 3: ("MPI", "COCO", 15, (-1, -1)),
+               4: ("BODY_19", "BODY_19", 19, (15, 16)), 5: ("BODY_19", "BODY_19", 19, (15, 16)),
+               6: ("BODY_19", "BODY_19", 19, (15, 16)), 12: ("BODY_19", "BODY_19", 19, (15, 16)),
+               8: ("CAR_12", "CAR_12", 12, (4, 5)), 10: ("BODY_23", "BODY_23", 23, (13, 14)),
+               11: ("CAR_22", "CAR_22", 22, (6, 7)), 13: ("BODY_25B", "BODY_25B", 25, (1, 2)),
+               14: ("BODY_135", "BODY_135", 135, (1, 2))}
+
+
+def render_tables():
+    """The reference's GPU render tables (tests/golden/render_tables.json, written by
+    tools/gen_render_tables.py from its *_RENDER_GPU macros), by name."""
+    import json
+    with open(os.path.join(_HERE, "..", "tests", "golden", "render_tables.json")) as f:
+        return {d["name"]: d for d in json.load(f)}
+
+
+def render_keypoints(frame, kp, table, scales_table=None, parts=None, radius_div=100.0,
+                     line_div=120.0, threshold=0.05, alpha=0.6, blend=True, eyes=(-1, -1)):
+    """renderKeypointsOld on a copy of frame (float BGR [h][w][3]); kp [people][parts][3].
+    Returns (frame, ambiguous [h][w] uint8)."""
+    tabs = render_tables()
+    t = tabs[table]
+    st = tabs[scales_table or table]
+    out = np.ascontiguousarray(frame, np.float32).copy()
+    h, w = out.shape[:2]
+    kp = np.ascontiguousarray(kp, np.float32).reshape(-1, parts or kp.shape[1], 3)
+    amb = np.zeros((h, w), np.uint8)
+    m = min(w, h)
+    lib().orc_render_keypoints(out, w, h, kp, kp.shape[0], kp.shape[1],
+                               np.asarray(t["pairs"], np.uint32), len(t["pairs"]) // 2,
+                               np.asarray(t["colors"], np.float32), len(t["colors"]) // 3,
+                               np.asarray(st["scales"], np.float32), len(t["scales"]),
+                               np.float32(m) / np.float32(radius_div),
+                               np.float32(m) / np.float32(line_div), threshold, alpha,
+                               1 if blend else 0, eyes[0], eyes[1], amb)
+    return out, amb
+
+
+def render_heat_map(frame, heat, scale, part, alpha=0.7, abs_value=False):
+    out = np.ascontiguousarray(frame, np.float32).copy()
+    heat = np.ascontiguousarray(heat, np.float32)
+    lib().orc_render_heat_map(out, out.shape[1], out.shape[0], heat, heat.shape[-1],
+                              heat.shape[-2], scale, part, alpha, 1 if abs_value else 0)
+    return out
+
+
+def render_heat_maps(frame, heat, scale, parts, alpha=0.7):
+    colors = np.asarray(render_tables()["COCO"]["colors"], np.float32)
+    out = np.ascontiguousarray(frame, np.float32).copy()
+    heat = np.ascontiguousarray(heat, np.float32)
+    lib().orc_render_heat_maps(out, out.shape[1], out.shape[0], heat, heat.shape[-1],
+                               heat.shape[-2], scale, parts, colors, len(colors) // 3, alpha)
+    return out
+
+
+def render_pafs(frame, heat, scale, first, count, alpha=0.7):
+    out = np.ascontiguousarray(frame, np.float32).copy()
+    heat = np.ascontiguousarray(heat, np.float32)
+    lib().orc_render_pafs(out, out.shape[1], out.shape[0], heat, heat.shape[-1], heat.shape[-2],
+                          scale, first, count, alpha)
     return out

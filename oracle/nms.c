@@ -10,6 +10,8 @@
  * Compiled with -ffp-contract=off: the accumulations below are plain float mul/add in the
  * reference's loop order.
  */
+#include <math.h>
+
 #include "oracle.h"
 
 /* Returns 1 iff (x, y) registers as a peak (nmsBase.cpp:16-67). */

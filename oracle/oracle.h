@@ -130,6 +130,23 @@ void orc_relu(float* x, long count);
 void orc_maxpool(float* out, const float* in, int n, int c, int h, int w, int k, int s,
                  int oh, int ow);
 
+/* ---- renderers (render.c): renderKeypointsOld / renderKeypoints, renderBodyPartHeatMap(s),
+ * renderPartAffinities (render.hu, renderPose.cu).  Parity unpinned (CUDA device library
+ * transcendentals); `ambiguous` marks the pixels where that can matter. */
+#define ORC_RENDER_MAX_PEOPLE 1024
+void orc_render_keypoints(float* frame, int w, int h, const float* kp, int people, int parts,
+                          const unsigned* pairs, int npairs, const float* colors, int ncolors,
+                          const float* scales, int nscales, float radius, float line_width,
+                          float threshold, float alpha, int blend, int eye1, int eye2,
+                          unsigned char* ambiguous);
+float orc_cuda_bicubic(const float* src, float xs, float ys, int sw, int sh);
+void orc_render_heat_map(float* frame, int w, int h, const float* heat, int hw, int hh,
+                         float scale, int part, float alpha, int abs_value);
+void orc_render_heat_maps(float* frame, int w, int h, const float* heat, int hw, int hh,
+                          float scale, int parts, const float* colors, int ncolors, float alpha);
+void orc_render_pafs(float* frame, int w, int h, const float* heat, int hw, int hh, float scale,
+                     int first, int count, float alpha);
+
 #ifdef __cplusplus
 }
 #endif

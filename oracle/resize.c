@@ -148,7 +148,7 @@ static float cuda_cubic(float v0, float v1, float v2, float v3, float dx)
 static int mini(int a, int b) { return a < b ? a : b; }
 static int maxi(int a, int b) { return a > b ? a : b; }
 
-static float cuda_bicubic(const float* src, float xs, float ys, int sw, int sh)
+float orc_cuda_bicubic(const float* src, float xs, float ys, int sw, int sh)
 {
     int xi[4], yi[4];
     xi[1] = clampi((int)floorf(xs), 0, sw - 1);
@@ -201,7 +201,7 @@ int orc_resize_merge_cuda(float* dst, const float* const* srcs, int nsrc, int ch
                     const int sh = hw[2 * i], sw = hw[2 * i + 1];
                     const float xs = ((float)x + 0.5f) / sx[i] - 0.5f;
                     const float ys = ((float)y + 0.5f) / sy[i] - 0.5f;
-                    acc += cuda_bicubic(srcs[i] + (long)c * sh * sw, xs, ys, sw, sh);
+                    acc += orc_cuda_bicubic(srcs[i] + (long)c * sh * sw, xs, ys, sw, sh);
                 }
                 dst[((long)c * dh + y) * dw + x] = nsrc > 1 ? acc / (float)nsrc : acc;
             }
