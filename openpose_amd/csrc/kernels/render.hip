@@ -5,17 +5,18 @@
 // renderFaceKeypointsGpu (src/openpose/face/renderFace.cu:48-76) and renderHandKeypointsGpu
 // (src/openpose/hand/renderHand.cu:48-76).  The reference evaluates, for every pixel of the frame,
 // each person's box test and every limb's atan2f / sinf / cosf.  Here:
-//   1. render_prep_kernel (one thread per person): the person's box and scale
+//   1. render_prep_kernel (one wave per person): the person's box and scale
 //      (getBoundingBoxPerPerson, render.hu:6-59) and, per limb and per part, everything that does not
 //      depend on the pixel -- limb centre, cos / sin of its angle, the ellipse's aSqrt / bSqrt, the
 //      circle radii -- with the reference's expressions, in its operation order;
 //   2. render_keypoints_kernel (one 32x8 pixel tile per workgroup): the people whose box meets the
-//      tile are compacted in order into LDS (wave ballots), then each pixel runs the reference's
-//      per-pixel tests for those people only -- limbs, then part circles, person by person -- and
-//      blends with addColorWeighted (cuda.hu:188-201).  A limb is skipped for a pixel only when its
-//      squared distance to the limb centre exceeds 1.01 * (aSqrt + bSqrt) + 4, where the ellipse
-//      test cannot pass (judge >= dist^2 / (aSqrt + bSqrt)).  Person / limb / part records are
-//      read at wave-uniform addresses (scalar loads).
+//      tile are compacted in order into LDS (wave ballots); then, in rounds of 256, their limbs and
+//      part circles -- person-major, limbs before circles, the reference's draw order -- are culled
+//      against the tile (a limb survives if the tile reaches its squared-distance bound
+//      1.01 * (aSqrt + bSqrt) + 4, beyond which the ellipse test cannot pass since
+//      judge >= dist^2 / (aSqrt + bSqrt); a circle if the tile reaches its radius) and the survivors'
+//      records staged in LDS; each pixel then runs the reference's per-pixel tests on those only and
+//      blends with addColorWeighted (cuda.hu:188-201).
 // The frame is the reference's float BGR [h][w][3]; each pixel is read and written once: the
 // kernel is bound by those 24 bytes per pixel (HBM) plus the per-person ALU work.
 //
@@ -55,10 +56,11 @@ __device__ __forceinline__ void blend(float& r, float& g, float& b, float cr, fl
     b = (1.f - alpha) * b + alpha * cb;
 }
 
+// one wave per person: box (a lane-strided scan + wave reduction; min / max do not depend on the
+// order), then lanes take limbs and parts
 __global__ __launch_bounds__(64) void render_prep_kernel(RenderKeypointsArgs a)
 {
-    const int p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= a.people) return;
+    const int p = blockIdx.x, lane = threadIdx.x;
     const float* kp = a.kp + (size_t)p * a.parts * 3;
     float* box = a.geom + (size_t)p * 8;
     float* limb = a.geom + (size_t)a.people * 8 + (size_t)p * a.npairs * 8;
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(64) void render_prep_kernel(RenderKeypointsArgs a)
                   (size_t)p * a.parts * 8;
     // getBoundingBoxPerPerson (render.hu:6-59 / 219-260)
     float minx = (float)a.w, miny = (float)a.h, maxx = 0.f, maxy = 0.f;
-    for (int i = 0; i < a.parts; ++i) {
+    for (int i = lane; i < a.parts; i += 64) {
         const float x = kp[3 * i], y = kp[3 * i + 1], s = kp[3 * i + 2];
         if (s > a.threshold) {
             if (x < minx) minx = x;
@@ -75,8 +77,16 @@ __global__ __launch_bounds__(64) void render_prep_kernel(RenderKeypointsArgs a)
             if (y > maxy) maxy = y;
         }
     }
+    for (int o = 32; o > 0; o >>= 1) {
+        const float a0 = __shfl_xor(minx, o), a1 = __shfl_xor(miny, o);
+        const float a2 = __shfl_xor(maxx, o), a3 = __shfl_xor(maxy, o);
+        minx = a0 < minx ? a0 : minx;
+        miny = a1 < miny ? a1 : miny;
+        maxx = a2 > maxx ? a2 : maxx;
+        maxy = a3 > maxy ? a3 : maxy;
+    }
     // the box's own scale; the reference leaves it unset when a coordinate maximum is exactly 0
-    // (then only the box test below decides, which rejects every pixel of an empty person)
+    // (then only the box test decides, which rejects every pixel of an empty person)
     const float scale = truncate_ref(((maxx - minx) + (maxy - miny)) / 400.f, 0.33f, 1.f);
     if (maxx != 0.f && maxy != 0.f) {
         maxx += 50.f;
@@ -84,16 +94,18 @@ __global__ __launch_bounds__(64) void render_prep_kernel(RenderKeypointsArgs a)
         minx -= 50.f;
         miny -= 50.f;
     }
-    box[0] = minx;
-    box[1] = miny;
-    box[2] = maxx;
-    box[3] = maxy;
-    box[4] = scale;
+    if (lane == 0) {
+        box[0] = minx;
+        box[1] = miny;
+        box[2] = maxx;
+        box[3] = maxy;
+        box[4] = scale;
+    }
     const float s2 = scale * scale;
     const float lw2 = a.line_width * a.line_width;
     const float r2 = a.radius * a.radius;
     // limbs (render.hu:288-326)
-    for (int j = 0; j < a.npairs; ++j) {
+    for (int j = lane; j < a.npairs; j += 64) {
         const unsigned pa = a.pairs[2 * j], pb = a.pairs[2 * j + 1];
         const float xA = kp[3 * pa], yA = kp[3 * pa + 1], sA = kp[3 * pa + 2];
         const float xB = kp[3 * pb], yB = kp[3 * pb + 1], sB = kp[3 * pb + 2];
@@ -111,14 +123,14 @@ __global__ __launch_bounds__(64) void render_prep_kernel(RenderKeypointsArgs a)
             L[3] = sinf(angle);
             L[4] = aSqrt;
             L[5] = bSqrt;
-            L[6] = 1.01f * (aSqrt + bSqrt) + 4.f;
+            L[6] = 1.01f * (aSqrt + bSqrt) + 4.f;   // squared-distance bound of the ellipse
             L[7] = (float)((pb % a.ncolors) * 3);
         } else {
-            L[6] = -1.f;   // never drawn
+            L[6] = -1.f;   // a score at or below the threshold: never drawn
         }
     }
     // part circles (render.hu:329-377)
-    for (int i = 0; i < a.parts; ++i) {
+    for (int i = lane; i < a.parts; i += 64) {
         float* C = part + (size_t)i * 8;
         const float x = kp[3 * i], y = kp[3 * i + 1], s = kp[3 * i + 2];
         if (!(s > a.threshold)) {
@@ -143,20 +155,48 @@ __global__ __launch_bounds__(64) void render_prep_kernel(RenderKeypointsArgs a)
     }
 }
 
+// squared distance from (cx, cy) to the tile's pixel rectangle, with the per-pixel test's own
+// operations at its nearest pixel: never above any pixel's dist^2 (rounding is monotonic)
+__device__ __forceinline__ float rect_d2(float cx, float cy, float fx0, float fy0, float fx1,
+                                         float fy1)
+{
+    const float dx = cx < fx0 ? fx0 - cx : (cx > fx1 ? cx - fx1 : 0.f);
+    const float dy = cy < fy0 ? fy0 - cy : (cy > fy1 ? cy - fy1 : 0.f);
+    return dx * dx + dy * dy;
+}
+
+// ordered compaction of one 256-candidate round: returns this thread's slot (or -1) and the
+// round's total; wcount is the block's 4-entry scratch
+__device__ __forceinline__ int compact(bool hit, int* wcount, int* total)
+{
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const unsigned long long m = __ballot(hit);
+    if (lane == 0) wcount[wave] = __popcll(m);
+    __syncthreads();
+    int off = 0, tot = 0;
+    for (int i = 0; i < 4; ++i) {
+        off += i < wave ? wcount[i] : 0;
+        tot += wcount[i];
+    }
+    *total = tot;
+    return hit ? off + __popcll(m & ((1ull << lane) - 1ull)) : -1;
+}
+
 __global__ __launch_bounds__(256) void render_keypoints_kernel(RenderKeypointsArgs a)
 {
-    __shared__ unsigned short list[kRenderMaxPeople];
+    __shared__ unsigned short plist[kRenderMaxPeople];
+    // one round's drawable items in draw order: {box}, {geometry}, {geometry, type, color}
+    __shared__ float4 items[256][4];
     __shared__ int wcount[4];
     const int tx0 = blockIdx.x * kTileW, ty0 = blockIdx.y * kTileH;
     const float fx0 = (float)tx0, fy0 = (float)ty0;
     const float fx1 = (float)min(tx0 + kTileW - 1, a.w - 1), fy1 = (float)min(ty0 + kTileH - 1, a.h - 1);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const float* __restrict__ boxes = a.geom;
     const float* __restrict__ limbs = a.geom + (size_t)a.people * 8;
     const float* __restrict__ circles = limbs + (size_t)a.people * a.npairs * 8;
     const float* __restrict__ colors = a.colors;
 
-    // the people whose box meets this tile, in person order
+    // 1. the people whose box meets this tile, in person order
     int n = 0;
     for (int base = 0; base < a.people; base += 256) {
         const int p = base + threadIdx.x;
@@ -165,66 +205,106 @@ __global__ __launch_bounds__(256) void render_keypoints_kernel(RenderKeypointsAr
             const float* B = boxes + (size_t)p * 8;
             hit = B[2] >= fx0 && B[0] <= fx1 && B[3] >= fy0 && B[1] <= fy1;
         }
-        const unsigned long long m = __ballot(hit);
-        if (lane == 0) wcount[wave] = __popcll(m);
-        __syncthreads();
-        int off = n, tot = 0;
-        for (int i = 0; i < 4; ++i) {
-            off += i < wave ? wcount[i] : 0;
-            tot += wcount[i];
-        }
-        if (hit) list[off + __popcll(m & ((1ull << lane) - 1ull))] = (unsigned short)p;
+        int tot;
+        const int slot = compact(hit, wcount, &tot);
+        if (slot >= 0) plist[n + slot] = (unsigned short)p;
         __syncthreads();
         n += tot;
     }
+
     const int x = tx0 + (threadIdx.x & (kTileW - 1)), y = ty0 + threadIdx.x / kTileW;
-    if (x >= a.w || y >= a.h) return;
-    const size_t base = 3 * ((size_t)y * a.w + x);
-    float b = a.frame[base], g = a.frame[base + 1], r = a.frame[base + 2];
-    if (!a.blend) b = g = r = 0.f;
-    const float fx = (float)x, fy = (float)y;
-    for (int i = 0; i < n; ++i) {
-        const int p = __builtin_amdgcn_readfirstlane((int)list[i]);
-        const float* B = boxes + (size_t)p * 8;
-        if (!(fx <= B[2] && fx >= B[0] && fy <= B[3] && fy >= B[1])) continue;
-        const float* L = limbs + (size_t)p * a.npairs * 8;
-        for (int j = 0; j < a.npairs; ++j, L += 8) {
-            if (L[6] < 0.f) continue;   // a score at or below the threshold
-            const float dx = fx - L[0], dy = fy - L[1];
-            if (dx * dx + dy * dy > L[6]) continue;
-            const float A = L[2] * dx + L[3] * dy;
-            const float Bq = L[3] * dx - L[2] * dy;
-            const float judge = A * A / L[4] + Bq * Bq / L[5];
-            if (0.f <= judge && judge <= 1.f) {
-                const float* c = colors + (int)L[7];
-                blend(r, g, b, c[0], c[1], c[2], a.alpha);
-            }
-        }
-        const float* C = circles + (size_t)p * a.parts * 8;
-        for (int k = 0; k < a.parts; ++k, C += 8) {
-            const float kind = C[4];
-            if (kind == 0.f) continue;
-            const float dx = fx - C[0], dy = fy - C[1];
-            const float dist2 = dx * dx + dy * dy;
-            if (kind == 2.f) {   // googly eyes (render.hu:344-366)
-                if (dist2 <= C[2]) {
-                    float v = 0.f;
-                    if (dist2 <= C[3]) v = 255.f;
-                    if (dist2 <= C[3] * 0.6f) {
-                        const float ex = (float)(x - 4) - C[0], ey = fy - C[1] + 4;
-                        if (ex * ex + ey * ey > 14.0625f) v = 0.f;
-                    }
-                    blend(r, g, b, v, v, v, 0.9f);
-                }
-            } else if (0.f <= dist2 && dist2 <= C[2]) {
-                const float* c = colors + (int)C[5];
-                blend(r, g, b, c[0], c[1], c[2], a.alpha);
-            }
-        }
+    const bool inside = x < a.w && y < a.h;
+    const size_t base = 3 * ((size_t)(inside ? y : 0) * a.w + (inside ? x : 0));
+    float b = 0.f, g = 0.f, r = 0.f;
+    if (inside && a.blend) {
+        b = a.frame[base];
+        g = a.frame[base + 1];
+        r = a.frame[base + 2];
     }
-    a.frame[base] = b;
-    a.frame[base + 1] = g;
-    a.frame[base + 2] = r;
+    const float fx = (float)x, fy = (float)y;
+
+    // 2. rounds of 256 (person, limb | part) candidates, person-major, limbs before parts (the
+    //    reference's draw order); those whose ellipse bound / circle reaches the tile go to LDS
+    const int per = a.npairs + a.parts;
+    const int total = n * per;
+    for (int k0 = 0; k0 < total; k0 += 256) {
+        const int k = k0 + threadIdx.x;
+        bool hit = false;
+        float4 q0, q1, q2, q3;
+        if (k < total) {
+            const int s = k / per, j = k - s * per;
+            const int p = plist[s];
+            const float* B = boxes + (size_t)p * 8;
+            q0 = make_float4(B[0], B[1], B[2], B[3]);
+            if (j < a.npairs) {
+                const float* L = limbs + ((size_t)p * a.npairs + j) * 8;
+                const float rej = L[6];
+                if (rej >= 0.f || rej != rej) {
+                    hit = !(rect_d2(L[0], L[1], fx0, fy0, fx1, fy1) > rej);
+                    q1 = make_float4(L[0], L[1], L[2], L[3]);
+                    q2 = make_float4(L[4], L[5], rej, L[7]);
+                    q3 = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            } else {
+                const float* C = circles + ((size_t)p * a.parts + (j - a.npairs)) * 8;
+                const float kind = C[4];
+                if (kind != 0.f) {
+                    hit = !(rect_d2(C[0], C[1], fx0, fy0, fx1, fy1) > C[2]);
+                    q1 = make_float4(C[0], C[1], C[2], C[3]);
+                    q2 = make_float4(0.f, 0.f, 0.f, C[5]);
+                    q3 = make_float4(kind, 0.f, 0.f, 0.f);
+                }
+            }
+        }
+        int m;
+        const int slot = compact(hit, wcount, &m);
+        if (slot >= 0) {
+            items[slot][0] = q0;
+            items[slot][1] = q1;
+            items[slot][2] = q2;
+            items[slot][3] = q3;
+        }
+        __syncthreads();
+        if (inside) {
+            for (int i = 0; i < m; ++i) {
+                const float4 B = items[i][0];
+                if (!(fx <= B.z && fx >= B.x && fy <= B.w && fy >= B.y)) continue;
+                const float4 G = items[i][1], H = items[i][2];
+                const float type = items[i][3].x;
+                const float dx = fx - G.x, dy = fy - G.y;
+                const float d2 = dx * dx + dy * dy;
+                if (type == 0.f) {   // limb (render.hu:301-325)
+                    if (d2 > H.z) continue;
+                    const float A = G.z * dx + G.w * dy;
+                    const float Bq = G.w * dx - G.z * dy;
+                    const float judge = A * A / H.x + Bq * Bq / H.y;
+                    if (0.f <= judge && judge <= 1.f) {
+                        const float* c = colors + (int)H.w;
+                        blend(r, g, b, c[0], c[1], c[2], a.alpha);
+                    }
+                } else if (type == 2.f) {   // googly eye (render.hu:344-366)
+                    if (d2 <= G.z) {
+                        float v = 0.f;
+                        if (d2 <= G.w) v = 255.f;
+                        if (d2 <= G.w * 0.6f) {
+                            const float ex = (float)(x - 4) - G.x, ey = fy - G.y + 4;
+                            if (ex * ex + ey * ey > 14.0625f) v = 0.f;
+                        }
+                        blend(r, g, b, v, v, v, 0.9f);
+                    }
+                } else if (0.f <= d2 && d2 <= G.z) {   // part circle (render.hu:368-375)
+                    const float* c = colors + (int)H.w;
+                    blend(r, g, b, c[0], c[1], c[2], a.alpha);
+                }
+            }
+        }
+        __syncthreads();   // the next round rewrites items
+    }
+    if (inside) {
+        a.frame[base] = b;
+        a.frame[base + 1] = g;
+        a.frame[base + 2] = r;
+    }
 }
 
 // getColorHeatMap (renderPose.cu:44-80) with vmin 0, vmax 1
@@ -391,7 +471,7 @@ void launch_render_keypoints(const RenderKeypointsArgs& a, hipStream_t stream)
 {
     if (a.w <= 0 || a.h <= 0) return;
     if (a.people > 0) {
-        render_prep_kernel<<<(a.people + 63) / 64, 64, 0, stream>>>(a);
+        render_prep_kernel<<<a.people, 64, 0, stream>>>(a);
         OPK_LAUNCH_CHECK();
     }
     render_keypoints_kernel<<<tiles(a.w, a.h), kTileW * kTileH, 0, stream>>>(a);
