@@ -83,8 +83,13 @@ int main(int argc, char** argv)
         const float* dpose = static_cast<const float*>(upload(pose.data(), pose.size() * 4));
         const float* dheat = static_cast<const float*>(upload(heat.data(), heat.size() * 4));
         const float* dface = static_cast<const float*>(upload(face.data(), face.size() * 4));
-        const op::Point<unsigned int> size{(unsigned)w, (unsigned)h};
-        const op::Point<int> hsize{hw, hh};
+        // op::Point's members live in the reference's core/point.cpp, which this driver does not
+        // build (no reference code travels to the GPU box): the two plain fields are laid out as the
+        // class declares them (point.hpp:12-13) and only read through the const references
+        const unsigned size_raw[2] = {(unsigned)w, (unsigned)h};
+        const int hsize_raw[2] = {hw, hh};
+        const auto& size = *reinterpret_cast<const op::Point<unsigned int>*>(size_raw);
+        const auto& hsize = *reinterpret_cast<const op::Point<int>*>(hsize_raw);
         const float scale = (float)w / (float)hw;
         std::vector<float> out(fn);
         auto fetch = [&](const char* name) {

@@ -33,9 +33,6 @@ def build_render_driver():
            "-I" + os.path.join(ROOT, "integration"),
            os.path.join(ROOT, "integration", "renderHip.cpp"),
            os.path.join(ROOT, "tests", "render_driver.cpp"),
-           # op::Point's members, from the reference's own source where it lies (as the drop-in
-           # links them from the reference build)
-           "/root/reference/src/openpose/core/point.cpp",
            "-L" + os.path.join(ROOT, "openpose_amd"), "-lopk_hip",
            "-Wl,-rpath,$ORIGIN/../../openpose_amd", "-o", BIN]
     r = subprocess.run(cmd, capture_output=True, text=True)
