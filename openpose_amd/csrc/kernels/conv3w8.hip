@@ -34,7 +34,9 @@ using namespace conv3dev;
 constexpr int k8_BM = 512, k8_HR = 688, k8_NW = 8;
 
 #ifndef OPK8_ABLATE   // dev probe only (tools/conv3w_probe.hip): 1 no mid-unit barrier, 2 no MFMAs,
-#define OPK8_ABLATE 0  // 3 no fragment reads, 4 no DMA after the prologue (timing only, wrong results)
+#define OPK8_ABLATE 0  // 3 no fragment reads, 4 no DMA after the prologue, 5 no MFMAs in tap 1 of
+                       // each unit (a third fewer, replaced by VALU adds), 6 the same with nothing
+                       // issued in their place (timing only, wrong results)
 #endif
 #if OPK8_ABLATE == 3
 #define OPK8_DSR(dst_, addr_, off_) asm volatile("; no read %1" : "=v"(dst_) : "v"(addr_))
@@ -205,7 +207,11 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
             OPK8_WAIT(w_ < 0 ? 0 : w_, fa[I]);                                                \
         }                                                                                     \
         _Pragma("unroll") for (int j_ = 0; j_ < NF; ++j_)                                     \
-            acc[I][j_] = OPK8_ABLATE == 2 ? acc[I][j_] + (float)fa[I][j_]                      \
+            if constexpr (OPK8_ABLATE == 6 && K == 1)                                         \
+                asm volatile("; mfma skipped" : "+v"(acc[I][j_]) : "v"(FC[j_]), "v"(fa[I]));  \
+            else                                                                              \
+            acc[I][j_] = (OPK8_ABLATE == 2 || (OPK8_ABLATE == 5 && K == 1))                  \
+                ? acc[I][j_] + (float)fa[I][j_]                                               \
                 : __builtin_amdgcn_mfma_f32_16x16x32_f16(FC[j_], fa[I], acc[I][j_], 0, 0, 0);   \
         __builtin_amdgcn_sched_barrier(0);                                                    \
     } while (0)
