@@ -240,6 +240,10 @@ def rank_main(args, rank, world, local):
         net_ms = max(r[2] for r in per_rank)
         post_ms = max(r[3] for r in per_rank)
 
+    # measured ceilings of this GPU (outside the timed region): the rate the conv instruction
+    # reaches from registers on random operands is the attainable MFMA roof under this clock
+    peaks = ctx.probe_peaks()
+
     total_frames = world * B * args.steps
     if rank == 0:
         assert len(ordered) == total_frames, (len(ordered), total_frames)
@@ -296,6 +300,8 @@ def rank_main(args, rank, world, local):
             "traffic_unit": "bytes per launch (HBM, PMC)",
             "algorithmic_gflop_per_launch": round(flops_frame * B / 1e9, 2),
             "avg_launch_ms": round(net_ms, 3),
+            "measured_ceilings": peaks,
+            "frac_of_measured_random_operand_mfma": round(achieved / peaks["mfma_fp16_random_tflops"], 4),
         },
         "post_roofline": {
             "bound": "hbm",

@@ -441,6 +441,14 @@ int opk_extractor_forward(opk_extractor* ex, const uint8_t* frames_dev, int nfra
 int opk_extractor_crop_count(opk_extractor* ex);
 int opk_extractor_crop(opk_extractor* ex, int i, double* matrix_host, const float** input_dev);
 
+/* ---- Measured ceilings (no reference counterpart; SURVEY.md §8d "confirm the vendor peaks"):
+ *      dense fp16 MFMA rate of v_mfma_f32_16x16x32_f16 from registers (the conv kernels'
+ *      instruction; 4 waves per SIMD, 8 independent chains, consecutive MFMAs on different operand
+ *      pairs) on uniform random and on all-zero operands, in TFLOP/s, and the streaming HBM read
+ *      rate over 2 GiB in GB/s.  Runs ~0.1 s of device work on the context's stream; synchronous. */
+int opk_probe_peaks(opk_ctx* ctx, double* mfma_random_tflops, double* mfma_zero_tflops,
+                    double* hbm_read_gbs);
+
 /* ---- Renderers (enqueued on the context's stream).  frame_dev: the reference's float BGR frame
  *      [height][width][3] (0..255), drawn in place.
  * opk_render_pose_keypoints replaces op::renderPoseKeypointsGpu

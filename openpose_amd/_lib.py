@@ -34,6 +34,7 @@ _SIGS = {
     "opk_memset": (_i, [_p, _p, _i, _c.c_size_t]),
     "opk_memcpy_h2d": (_i, [_p, _p, _p, _c.c_size_t]),
     "opk_memcpy_d2h": (_i, [_p, _p, _p, _c.c_size_t]),
+    "opk_probe_peaks": (_i, [_p, _c.POINTER(_d), _c.POINTER(_d), _c.POINTER(_d)]),
     "opk_render_pose_keypoints": (_i, [_p, _p, _i, _i, _c.c_uint, _c.c_uint, _p, _f, _i, _i, _f]),
     "opk_render_face_keypoints": (_i, [_p, _p, _c.c_uint, _c.c_uint, _p, _i, _f, _f]),
     "opk_render_hand_keypoints": (_i, [_p, _p, _c.c_uint, _c.c_uint, _p, _i, _f, _f]),

@@ -134,6 +134,14 @@ class Context:
                                        int4(peaks.shape), int4(heat.shape), offset[0], offset[1],
                                        semantics))
 
+    def probe_peaks(self):
+        """Measured ceilings on this device (opk_probe_peaks): dense fp16 MFMA TFLOP/s on random
+        and on zero operands, streaming HBM read GB/s."""
+        r, z, h = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+        check(self.L.opk_probe_peaks(self.h, ctypes.byref(r), ctypes.byref(z), ctypes.byref(h)))
+        return {"mfma_fp16_random_tflops": round(r.value, 1), "mfma_fp16_zero_tflops": round(z.value, 1),
+                "hbm_read_gbs": round(h.value, 1)}
+
     # ---- renderers (renderPose.cu / renderFace.cu / renderHand.cu) ---------------------------
     # frame: float32 CUDA [h, w, 3] BGR, drawn in place; keypoints float32 CUDA [people, parts, 3]
     def render_pose_keypoints(self, frame, pose, pose_model=BODY_25, threshold=0.05,

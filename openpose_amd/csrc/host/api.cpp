@@ -409,3 +409,53 @@ int opk_save_people_json(const char* path, const opk_json_keypoints* arrays, int
 }
 
 }  // extern "C"
+
+extern "C" int opk_probe_peaks(opk_ctx* ctx, double* mfma_random_tflops, double* mfma_zero_tflops,
+                               double* hbm_read_gbs)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx != nullptr, "NULL argument");
+        ctx->bind();
+        int cus = 0;
+        OPK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+        const int blocks = 4 * cus, hbm_blocks = 16 * cus, iters = 20000;
+        opk::DevBuf ops, out, big;
+        void* dops = ops.get(6 * 64 * 16);   // 6 x 64 half8 operands
+        // one float per lane of the larger of the two grids
+        float* dout = static_cast<float*>(out.get((size_t)std::max(blocks, hbm_blocks) * 256 * 4));
+        hipEvent_t e0, e1;
+        OPK_HIP(hipEventCreate(&e0));
+        OPK_HIP(hipEventCreate(&e1));
+        auto timed = [&](auto&& launch, int reps) {
+            launch();
+            OPK_HIP(hipEventRecord(e0, ctx->stream));
+            for (int r = 0; r < reps; ++r) launch();
+            OPK_HIP(hipEventRecord(e1, ctx->stream));
+            OPK_HIP(hipEventSynchronize(e1));
+            float ms = 0.f;
+            OPK_HIP(hipEventElapsedTime(&ms, e0, e1));
+            return (double)ms / reps;
+        };
+        std::vector<uint16_t> h(6 * 64 * 8);
+        uint32_t lcg = 12345u;
+        for (int random = 1; random >= 0; --random) {
+            for (auto& v : h) {   // fp16 bit patterns of uniform values in (-1, 1)
+                lcg = lcg * 1664525u + 1013904223u;
+                const uint32_t mant = (lcg >> 8) & 0x3ffu, ex = 11u + ((lcg >> 18) % 4u);
+                v = random ? (uint16_t)(((lcg >> 31) << 15) | (ex << 10) | mant) : (uint16_t)0;
+            }
+            OPK_HIP(hipMemcpyAsync(dops, h.data(), h.size() * 2, hipMemcpyHostToDevice, ctx->stream));
+            const double ms = timed([&] { opk::launch_mfma_peak(dops, dout, blocks, iters, ctx->stream); }, 3);
+            const double tf = (double)blocks * 4 * iters * 8 * 16384.0 / (ms * 1e-3) / 1e12;
+            if (random && mfma_random_tflops) *mfma_random_tflops = tf;
+            if (!random && mfma_zero_tflops) *mfma_zero_tflops = tf;
+        }
+        const size_t bytes = (size_t)2 << 30;
+        void* dbig = big.get(bytes);
+        OPK_HIP(hipMemsetAsync(dbig, 0, bytes, ctx->stream));
+        const double ms = timed([&] { opk::launch_hbm_read(dbig, bytes, dout, hbm_blocks, ctx->stream); }, 5);
+        if (hbm_read_gbs) *hbm_read_gbs = bytes / (ms * 1e-3) / 1e9;
+        OPK_HIP(hipEventDestroy(e0));
+        OPK_HIP(hipEventDestroy(e1));
+    });
+}

@@ -136,6 +136,11 @@ void launch_render_heat_maps(const RenderHeatArgs& a, int parts, const float* co
                              hipStream_t stream);
 void launch_render_pafs(const RenderHeatArgs& a, int first, int count, hipStream_t stream);
 
+// ---- measured ceilings (probe.hip) ------------------------------------------------------------
+// operands: 6 x 64 half8 values; out: blocks * 256 floats; 4 waves per workgroup
+void launch_mfma_peak(const void* operands, float* out, int blocks, int iters, hipStream_t stream);
+void launch_hbm_read(const void* buf, size_t bytes, float* out, int blocks, hipStream_t stream);
+
 // ---- elementwise helpers (misc.hip) -----------------------------------------------------------
 void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stream);
 // getHeatMapsCopy: dst [frames][nsel][hw] from heat [frames][channels][hw]; sel_dev = nsel source

@@ -1,0 +1,163 @@
+// peak_bench.hip -- measured MI355X ceilings for the rooflines bench.py prices against
+// ("confirm the vendor peaks with a microbenchmark and record").
+//
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/peak_bench_bin tools/peak_bench.hip
+//   tools/peak_bench_bin [iters]    -> one line per measurement (iters 4000: ~1 ms launches)
+//
+// MFMA: v_mfma_f32_16x16x32_f16 (the conv kernels' instruction) from registers, 8 independent
+// accumulator chains per wave, every MFMA on a different operand pair (the conv loop never feeds
+// the same fragments twice in a row), 2 / 4 waves per SIMD, operands all-zero or uniform random
+// fp16: the random/zero gap is the clock the chip holds under switching load.
+// HBM: float4 streaming read (sum kept), write, and copy over 4 GiB buffers.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                    \
+    do {                                                                         \
+        hipError_t e_ = (x);                                                     \
+        if (e_ != hipSuccess) {                                                  \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e_));         \
+            std::exit(1);                                                        \
+        }                                                                        \
+    } while (0)
+
+typedef _Float16 half8_t __attribute__((ext_vector_type(8)));
+typedef float float4_t __attribute__((ext_vector_type(4)));
+typedef float vf4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(256) void mfma_peak(const half8_t* __restrict__ in,
+                                                 float* __restrict__ out, int iters)
+{
+    const int lane = threadIdx.x & 63;
+    half8_t a[4], b[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = in[(k * 64 + lane) % 512];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) b[k] = in[((4 + k) * 64 + lane) % 512];
+    float4_t acc[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc[k] = float4_t{0.f, 0.f, 0.f, 0.f};
+    // hand-placed so the loop is the MFMAs and the branch only (the compiler's version rotates the
+    // accumulators through AGPR moves every iteration)
+    for (int i = 0; i < iters; i += 2) {
+        asm volatile(
+            "v_mfma_f32_16x16x32_f16 %0, %8, %12, %0\n"
+            "v_mfma_f32_16x16x32_f16 %1, %9, %12, %1\n"
+            "v_mfma_f32_16x16x32_f16 %2, %10, %12, %2\n"
+            "v_mfma_f32_16x16x32_f16 %3, %11, %12, %3\n"
+            "v_mfma_f32_16x16x32_f16 %4, %8, %13, %4\n"
+            "v_mfma_f32_16x16x32_f16 %5, %9, %13, %5\n"
+            "v_mfma_f32_16x16x32_f16 %6, %10, %13, %6\n"
+            "v_mfma_f32_16x16x32_f16 %7, %11, %13, %7\n"
+            "v_mfma_f32_16x16x32_f16 %0, %9, %13, %0\n"
+            "v_mfma_f32_16x16x32_f16 %1, %10, %13, %1\n"
+            "v_mfma_f32_16x16x32_f16 %2, %11, %13, %2\n"
+            "v_mfma_f32_16x16x32_f16 %3, %8, %13, %3\n"
+            "v_mfma_f32_16x16x32_f16 %4, %9, %12, %4\n"
+            "v_mfma_f32_16x16x32_f16 %5, %10, %12, %5\n"
+            "v_mfma_f32_16x16x32_f16 %6, %11, %12, %6\n"
+            "v_mfma_f32_16x16x32_f16 %7, %8, %12, %7\n"
+            : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3]), "+v"(acc[4]), "+v"(acc[5]),
+              "+v"(acc[6]), "+v"(acc[7])
+            : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(b[0]), "v"(b[1]));
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) s += acc[k][0] + acc[k][1] + acc[k][2] + acc[k][3];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
+__global__ __launch_bounds__(256) void hbm_read(const vf4* __restrict__ p, size_t n,
+                                                float* __restrict__ out)
+{
+    vf4 s = {0.f, 0.f, 0.f, 0.f};
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x) {
+        s += __builtin_nontemporal_load(p + i);
+    }
+    if (s.x + s.y + s.z + s.w == 12345.f) out[0] = s.x;   // keeps the loads
+}
+
+__global__ __launch_bounds__(256) void hbm_write(vf4* __restrict__ p, size_t n)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store(vf4{1.f, 2.f, 3.f, 4.f}, p + i);
+}
+
+__global__ __launch_bounds__(256) void hbm_copy(const vf4* __restrict__ s, vf4* __restrict__ d,
+                                                size_t n)
+{
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+         i += (size_t)gridDim.x * blockDim.x)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(s + i), d + i);
+}
+
+template <class F>
+static float time_ms(F f, int reps)
+{
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    f();
+    CK(hipDeviceSynchronize());
+    CK(hipEventRecord(a));
+    for (int r = 0; r < reps; ++r) f();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main(int argc, char** argv)
+{
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, 0));
+    const int cus = prop.multiProcessorCount;
+    std::printf("device %s, %d CUs, clock %d MHz\n", prop.gcnArchName, cus, prop.clockRate / 1000);
+
+    // ---- MFMA ------------------------------------------------------------------------------------
+    std::vector<_Float16> h(512 * 8);
+    srand(1);
+    half8_t* din;
+    float* dout;
+    CK(hipMalloc(&din, h.size() * 2));
+    CK(hipMalloc(&dout, (size_t)cus * 16 * 256 * 4));
+    const int iters = argc > 1 ? std::atoi(argv[1]) : 4000;   // per wave (x 8 MFMAs)
+    for (int random = 0; random < 2; ++random) {
+        for (auto& v : h) v = random ? (_Float16)((rand() / (float)RAND_MAX) * 2.f - 1.f) : (_Float16)0.f;
+        CK(hipMemcpy(din, h.data(), h.size() * 2, hipMemcpyHostToDevice));
+        for (int wps = 2; wps <= 4; wps += 2) {   // waves per SIMD: workgroups of 4 waves per CU
+            const int blocks = cus * wps;
+            const float ms = time_ms([&] { hipLaunchKernelGGL(mfma_peak, dim3(blocks), dim3(256), 0, 0,
+                                                              din, dout, iters); }, 5);
+            const double flop = (double)blocks * 4 * iters * 8 * 16384.0;
+            std::printf("mfma_f32_16x16x32_f16 %s operands, %d waves/SIMD: %.1f TFLOP/s (%.3f ms)\n",
+                        random ? "random" : "zero", wps, flop / ms / 1e9, ms);
+        }
+    }
+    CK(hipFree(din));
+
+    // ---- HBM -------------------------------------------------------------------------------------
+    const size_t bytes = (size_t)4 << 30, n = bytes / 16;
+    vf4 *a, *b;
+    CK(hipMalloc(&a, bytes));
+    CK(hipMalloc(&b, bytes));
+    CK(hipMemset(a, 0, bytes));
+    CK(hipMemset(b, 0, bytes));
+    const dim3 grid(cus * 16), block(256);
+    float ms = time_ms([&] { hipLaunchKernelGGL(hbm_read, grid, block, 0, 0, a, n, dout); }, 10);
+    std::printf("HBM read  %.0f GB/s (4 GiB, %.3f ms)\n", bytes / ms / 1e6, ms);
+    ms = time_ms([&] { hipLaunchKernelGGL(hbm_write, grid, block, 0, 0, b, n); }, 10);
+    std::printf("HBM write %.0f GB/s (4 GiB, %.3f ms)\n", bytes / ms / 1e6, ms);
+    ms = time_ms([&] { hipLaunchKernelGGL(hbm_copy, grid, block, 0, 0, a, b, n); }, 10);
+    std::printf("HBM copy  %.0f GB/s read+write (2 x 4 GiB, %.3f ms)\n", 2.0 * bytes / ms / 1e6, ms);
+    CK(hipFree(a));
+    CK(hipFree(b));
+    CK(hipFree(dout));
+    return 0;
+}
