@@ -9,7 +9,10 @@ PoseExtractorCaffe::forwardPass):
     accumulate) -> + people overlay -> resize x8 (78 maps) -> NMS (25 parts) -> PAF line integrals
     -> host people assembly -> per-frame keypoint records -> ordered gather to rank 0.
 `--config multiscale` runs BASELINE configs[3] instead (--scale_number 4 --scale_gap 0.25: nets at
-656x368, 480x272, 320x176, 160x80 per frame, their x8 resizes averaged).
+656x368, 480x272, 320x176, 160x80 per frame, their x8 resizes averaged).  `--config body135` runs
+configs[4]: BODY_135 through the poseNetOutput injection path (the reference has no BODY_135
+prototxt): synthetic 439 x 46 x 82 net outputs with 20 people per frame -> resize x8 (439 maps) ->
+NMS (135 parts) -> PAF integrals (152 pairs) -> connectBodyPartsGpu's global-sort assembly.
 Inputs are resident in HBM before timing: uint8 frames (uniform random pixels) and per-frame
 5-person overlays (synthetic weights carry no meaning, so a deterministic people field is added to
 the net output -- its cost is counted).
@@ -54,8 +57,9 @@ def parse():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=64,
                     help="frames per step per GPU (throughput mode; DESIGN.md §5 lists 16 too)")
-    ap.add_argument("--config", choices=["body25", "multiscale"], default="body25",
-                    help="body25: BASELINE configs[1]/[2]; multiscale: configs[3] (4 scales)")
+    ap.add_argument("--config", choices=["body25", "multiscale", "body135"], default="body25",
+                    help="body25: BASELINE configs[1]/[2]; multiscale: configs[3] (4 scales); "
+                         "body135: configs[4] (BODY_135 net-output injection, 20 people)")
     ap.add_argument("--people", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
@@ -326,6 +330,152 @@ def rank_main(args, rank, world, local):
         dist.destroy_process_group()
 
 
+def rank_main_body135(args, rank, world, local):
+    """BASELINE configs[4]: post-processing stress through the injection path (no CNN: the
+    reference has no BODY_135 network); frames/s and the post-processing HBM roofline."""
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    from openpose_amd import synth
+    from openpose_amd.api import Context, PoseExtractor, pose_model_info
+    from openpose_amd.pose_tables import BODY_135, CONNECT_GPU
+
+    people = 20 if args.people == 5 else args.people
+    t = pose_model_info(BODY_135)   # the library's tables (generated from poseParameters.cpp)
+    C = t["parts"] + int(t["bkg"]) + len(t["map_idx"])   # 439
+    H8, W8 = NET_H // 8, NET_W // 8
+    B = args.batch
+    distinct = 8
+    fields = np.stack([synth.overlay(people, H8, W8, seed=7000 * rank + k, table=t) +
+                       np.random.default_rng(k).normal(0, 0.01, (C, H8, W8)).astype(np.float32)
+                       for k in range(distinct)]).astype(np.float32)
+    net_out = [torch.from_numpy(fields[np.arange(B) % distinct]).cuda(),
+               torch.from_numpy(fields[(np.arange(B) + 3) % distinct]).cuda()]
+    ctx = Context(local)
+    pose = PoseExtractor(ctx, None, pose_model=BODY_135, semantics=CONNECT_GPU)
+    parts = t["parts"]
+    cap = B * (1 + (4 * people + 8) * (parts * 3 + 1))
+    gather = parallel.RecordGather(world, rank, cap, args.steps, "cuda")
+    rec_buf = np.empty(cap, np.float32)
+    collected = [0]
+
+    def collect(timed):
+        pose.collect()
+        if timed:
+            i = collected[0]
+            gather.push(i, (i * world + rank) * B, B, pose.records(rec_buf))
+            collected[0] += 1
+
+    def step(i, timed):
+        pose.submit_net_output(net_out[i % 2], (NET_W, NET_H), PRODUCER)
+        if pose.pending() > 1:
+            collect(timed)
+
+    def drain(timed):
+        while pose.pending() > 0:
+            collect(timed)
+
+    for i in range(args.warmup):
+        step(i, False)
+    drain(False)
+    torch.cuda.synchronize()
+    found = [pose.num_people(f) for f in range(min(B, 4))]
+    pose.set_timing(True)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i, True)
+    drain(True)
+    ordered = gather.finish(parts)
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    npost, post_ms = pose.read_timing()
+    pose.set_timing(False)
+    post_ms /= max(npost, 1)
+    if dist is not None:
+        tt = torch.tensor([elapsed, post_ms], device="cuda", dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, post_ms = float(tt[0]), float(tt[1])
+    total_frames = world * B * args.steps
+    if rank == 0:
+        assert len(ordered) == total_frames, (len(ordered), total_frames)
+    # what the reference's post-processing moves per frame (SURVEY.md §8d, config 5): the x8 resize
+    # of all 439 maps (read + write) and the NMS read of the 135 part planes (+ its peaks)
+    post_bytes = (4 * C * H8 * W8 + 4 * C * NET_H * NET_W + 4 * parts * NET_H * NET_W +
+                  4 * parts * 128 * 3)
+    gbs = post_bytes * B / (post_ms * 1e-3) / 1e9
+    result = {
+        "metric": METRIC,
+        "value": round(total_frames / elapsed, 2),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic BODY_135 net outputs (%d-person fields + N(0, 0.01) noise), resident "
+                "in HBM" % people,
+        "config": {
+            "workload": "BODY_135 (135 keypoints) poseNetOutput injection, 439x46x82 net output "
+                        "per frame for a 1280x720 producer, %d people per frame; resize x8 + NMS "
+                        "+ PAF integrals + connectBodyPartsGpu assembly + ordered gather" % people,
+            "frames_per_step_per_gpu": B,
+            "heatmaps": [C, NET_H, NET_W],
+            "parallelism": "frame-parallel replicas x%d (one process per GPU)" % world,
+            "people_per_frame_found": found,
+            "frames_gathered_in_order": total_frames,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "kernel": "post-processing per step (lazy resize/NMS detect + NMS finalize + PAF "
+                      "integrals), HIP events on the context stream",
+            "achieved": round(gbs, 1),
+            "peak": PEAK_HBM_GBS,
+            "unit": "GB/s",
+            "frac": round(gbs / PEAK_HBM_GBS, 4),
+            "traffic": None,
+            "algorithmic_bytes_per_frame": post_bytes,
+            "note": "effective rate: the reference's resize + NMS bytes per frame over the measured "
+                    "time; the lazy heat maps never move those bytes (DESIGN.md §4.2)",
+            "avg_launch_ms": round(post_ms, 3),
+        },
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle   # the CPU baseline leg only
+        t_orc = oracle.pose_tables()[BODY_135]
+        t1 = time.perf_counter()
+        done = 0
+        while True:
+            heat = oracle.resize_merge([fields[done % distinct]], NET_H, NET_W)
+            scale = 1.959128
+            off = 0.5 / scale
+            peaks = oracle.nms(heat, 0.05, 128, (off, off), channels=parts)
+            ps = oracle.pair_scores_table(heat, peaks, t_orc)
+            oracle.connect_gpu_semantics(ps, peaks, t_orc, scale=scale)
+            done += 1
+            el = time.perf_counter() - t1
+            if el >= min(args.cpu_seconds, 10.0):
+                break
+        result["cpu_baseline"] = {
+            "value": done / el, "unit": "frames/s", "cores": 1, "kind": "port",
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": "%d frame(s): oracle/ resize (439 maps) + NMS + pair scores + GPU-path "
+                      "assembly, %.1f s, single-threaded" % (done, el)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -336,7 +486,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
-    rank_main(args, rank, world, local)
+    if args.config == "body135":
+        rank_main_body135(args, rank, world, local)
+    else:
+        rank_main(args, rank, world, local)
 
 
 if __name__ == "__main__":

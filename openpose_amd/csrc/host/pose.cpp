@@ -15,7 +15,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <exception>
 #include <string>
+#include <thread>
 
 #include "../../../include/opk.h"
 #include "input.h"
@@ -380,25 +382,59 @@ int PoseHip::collect()
     people_.assign(n, 0);
     kp_.assign(n, {});
     ks_.assign(n, {});
-    std::vector<int> offsets;
+    // per-frame compact-record offsets; records longer than the eagerly copied head are fetched
+    // whole, all of them in one round of copies (many-people / BODY_135 frames)
+    std::vector<std::vector<int>> offsets(n);
+    std::vector<size_t> over_at(n, (size_t)-1);
+    size_t over_total = 0;
     for (int f = 0; f < n; ++f) {
-        const float* fp = hp + (size_t)f * peak_floats;
-        const float* fr = hr + (size_t)f * K;
-        const int total = compact_offsets(m, fp, kMaxPeaks, offsets);
-        OPK_CHECK_ARG((int)fr[0] == total, "PAF record count differs from the peak counts");
-        if ((size_t)total + 1 > K) {   // long record: fetch it whole
-            overflow_.resize((size_t)total + 1);
-            OPK_HIP(hipMemcpyAsync(overflow_.data(),
-                                   static_cast<const float*>(sl.records.ptr) + (size_t)f * rf,
-                                   ((size_t)total + 1) * 4, hipMemcpyDeviceToHost, copy_));
-            OPK_HIP(hipStreamSynchronize(copy_));
-            fr = overflow_.data();
+        const int total = compact_offsets(m, hp + (size_t)f * peak_floats, kMaxPeaks, offsets[f]);
+        OPK_CHECK_ARG((int)hr[(size_t)f * K] == total, "PAF record count differs from the peak counts");
+        if ((size_t)total + 1 > K) {
+            over_at[f] = over_total;
+            over_total += (size_t)total + 1;
         }
+    }
+    if (over_total > 0) {
+        float* ho = static_cast<float*>(overflow_.get(over_total * 4));
+        for (int f = 0; f < n; ++f)
+            if (over_at[f] != (size_t)-1)
+                OPK_HIP(hipMemcpyAsync(ho + over_at[f],
+                                       static_cast<const float*>(sl.records.ptr) + (size_t)f * rf,
+                                       ((size_t)hr[(size_t)f * K] + 1) * 4, hipMemcpyDeviceToHost,
+                                       copy_));
+        OPK_HIP(hipStreamSynchronize(copy_));
+    }
+    // people assembly: frames are independent (connectBodyParts* per frame), so they run on up
+    // to kAssemblyThreads host threads; every frame's result is the single-threaded one
+    const float* ho = static_cast<const float*>(overflow_.ptr);
+    auto frame = [&](int f) {
         PairScores ps;
-        ps.data = fr + 1;
+        ps.data = (over_at[f] != (size_t)-1 ? ho + over_at[f] : hr + (size_t)f * K) + 1;
         ps.compact = true;
-        ps.offsets = offsets.data();
-        people_[f] = assemble_people(m, fp, kMaxPeaks, ps, cp, kp_[f], ks_[f]);
+        ps.offsets = offsets[f].data();
+        people_[f] = assemble_people(m, hp + (size_t)f * peak_floats, kMaxPeaks, ps, cp, kp_[f],
+                                     ks_[f]);
+    };
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    const int T = (int)std::min<unsigned>({(unsigned)n, (unsigned)kAssemblyThreads, hw});
+    if (T <= 1) {
+        for (int f = 0; f < n; ++f) frame(f);
+    } else {
+        std::vector<std::exception_ptr> err(T);
+        std::vector<std::thread> pool;
+        pool.reserve(T);
+        for (int t = 0; t < T; ++t)
+            pool.emplace_back([&, t] {
+                try {
+                    for (int f = t; f < n; f += T) frame(f);
+                } catch (...) {
+                    err[t] = std::current_exception();
+                }
+            });
+        for (auto& th : pool) th.join();
+        for (auto& e : err)
+            if (e) std::rethrow_exception(e);
     }
     head_ = (head_ + 1) & 1;
     --count_;

@@ -76,6 +76,7 @@ public:
 
     static constexpr int kMaxPeaks = kPoseMaxPeople;   // peaks blob [parts][128][3]
     static constexpr int kRecordHead = 16384;          // record floats copied eagerly per frame
+    static constexpr int kAssemblyThreads = 16;        // host threads assembling a batch's people
 
 private:
     struct Slot {
@@ -115,7 +116,7 @@ private:
 
     Slot slots_[2];
     int head_ = 0, count_ = 0, last_ = -1;
-    std::vector<float> overflow_;        // records longer than kRecordHead
+    HostBuf overflow_;                   // records longer than kRecordHead (pinned)
 
     float scale_net_to_output_ = 1.f;
     int n_ = 0, hh_ = 0, hw_ = 0;
