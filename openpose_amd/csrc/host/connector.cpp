@@ -240,8 +240,10 @@ void people_global_sort(People& people, const PoseModelInfo& m, const float* pea
             people.found[p1] += people.found[p2];
             people.score[p1] += people.score[p2] + c.paf;
             dead.push_back(p2);
-            for (int& o : owner)
-                if (o == p2) o = p1;
+            // the (part, peak) slots p2 owned are exactly the parts of its row (a slot's owner
+            // is set when, and only when, the slot enters a row): re-point those to p1
+            for (int k = 0; k < P; ++k)
+                if (r2[k] > 0) owner[(size_t)k * max_peaks + (r2[k] - k * stride - 2) / 3 - 1] = p1;
         }
     }
     if (!dead.empty()) {   // erase merged-away people, keeping the order of the others
