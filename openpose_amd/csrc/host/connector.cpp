@@ -350,6 +350,10 @@ void select_people(std::vector<int>& keep, People& people, const float* peaks,
                                "). Bug in this function if this happens.");
     }
     if (!keep.empty()) {   // face-only fragments join the best-overlapping valid face
+        // each valid face's box, recomputed only after a fragment merged into it (the reference
+        // recomputes it for every comparison; between merges it cannot change)
+        std::vector<Roi> vroi(face_valid.size());
+        std::vector<char> vstale(face_valid.size(), 1);
         for (int bad : face_invalid) {
             Roi rb;
             int fb, lb;
@@ -357,10 +361,12 @@ void select_people(std::vector<int>& keep, People& people, const float* peaks,
             float best = 0.f;
             int besti = -1;
             for (int v = 0; v < (int)face_valid.size(); ++v) {
-                Roi rv;
-                int fv, lv;
-                roi_and_bounds(rv, fv, lv, people.row(face_valid[v]), peaks, 65, 135, 0.1f);
-                const float o = roi_overlap(rv, rb);
+                if (vstale[v]) {
+                    int fv, lv;
+                    roi_and_bounds(vroi[v], fv, lv, people.row(face_valid[v]), peaks, 65, 135, 0.1f);
+                    vstale[v] = 0;
+                }
+                const float o = roi_overlap(vroi[v], rb);
                 if (best < o) {
                     best = o;
                     besti = v;
@@ -368,6 +374,7 @@ void select_people(std::vector<int>& keep, People& people, const float* peaks,
             }
             if (!(best > 0.3f || (best > 0.01f && face_valid.size() < 3))) continue;
             const int good = face_valid[besti];
+            vstale[besti] = 1;
             int* g = people.row(good);
             const int* src = people.row(bad);
             for (int k = fb; k < lb; ++k) {
