@@ -464,17 +464,29 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
 
 void NetHip::forward(const float* input, int n, int h, int w)
 {
+    forward_on(input, n, h, w, ctx_->stream, true);
+}
+
+void NetHip::prepare(int n, int h, int w)
+{
+    OPK_CHECK_ARG(n > 0 && h > 0 && w > 0, "empty input");
+    ctx_->bind();
+    (void)shape_plan(n, h, w);
+}
+
+void NetHip::forward_on(const float* input, int n, int h, int w, hipStream_t st, bool timed)
+{
     OPK_CHECK_ARG(input && n > 0 && h > 0 && w > 0, "empty input");
     OPK_CHECK_ARG(ready(), "weights not loaded for every convolution");
     ctx_->bind();
     ShapePlan& S = *shape_plan(n, h, w);
     cur_ = &S;
-    timer_.begin(ctx_->stream);
-    forward_launches(S, input, n, h, w);
-    timer_.end(ctx_->stream);
+    if (timed) timer_.begin(st);
+    forward_launches(S, input, n, h, w, st);
+    if (timed) timer_.end(st);
 }
 
-void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, int w)
+void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, int w, hipStream_t st)
 {
     const std::vector<uint16_t*>& ptr = S.base;
     const std::vector<int>& lh_ = S.lh;
@@ -502,7 +514,7 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
         fa.out_coff = 0;
         fa.OH = lh_[1];
         fa.OW = lw_[1];
-        launch_conv1_fused(fa, cus_, ctx_->stream);
+        launch_conv1_fused(fa, cus_, st);
         first = 3;
     }
     for (size_t si = first; si < steps_.size(); ++si) {
@@ -539,17 +551,17 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
                 h.out32 = b.out32;
                 h.out32_c = b.out32_c;
                 h.out32_coff = b.out32_coff;
-                launch_conv_head(h, ctx_->stream);
+                launch_conv_head(h, st);
                 ++si;   // Mconv7 ran inside
                 continue;
             }
-            if (c.from_image) launch_conv_image(a, input, ctx_->stream);
-            else launch_conv3(a, ctx_->stream);
+            if (c.from_image) launch_conv_image(a, input, st);
+            else launch_conv3(a, st);
         } else {
             const PoolPlan& p = pools_[s.idx];
             const int L = p.level_in;
             launch_maxpool2(ptr[p.out_buf], ptr[p.in_buf], n, lh_[L], lw_[L],
-                            bufs_[p.in_buf].cs, lh_[L + 1], lw_[L + 1], ctx_->stream, border_);
+                            bufs_[p.in_buf].cs, lh_[L + 1], lw_[L + 1], st, border_);
         }
     }
 }

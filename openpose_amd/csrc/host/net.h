@@ -32,6 +32,12 @@ public:
     // buffers with zeroed guards, launch arguments, net output), kept across forwards, so the
     // scales of a multi-scale pass alternate without re-planning and their outputs coexist.
     void forward(const float* input, int n, int h, int w);
+    // the same on another stream, optionally untimed (concurrent scales, PoseHip::submit_multi);
+    // prepare() plans a shape ahead (its buffers are zeroed on the context stream)
+    void forward_on(const float* input, int n, int h, int w, hipStream_t stream, bool timed);
+    void prepare(int n, int h, int w);
+    void time_begin(hipStream_t s) { timer_.begin(s); }
+    void time_end(hipStream_t s) { timer_.end(s); }
     // net output of the last forward ([n][out_channels][out_h][out_w] fp32, stays valid until
     // set_conv or until more than kMaxShapes other shapes have been planned)
     float* output() const { return cur_ ? cur_->out32 : nullptr; }
@@ -85,7 +91,7 @@ private:
     };
 
     void plan(const std::vector<LayerDesc>& layers);
-    void forward_launches(ShapePlan& S, const float* input, int n, int h, int w);
+    void forward_launches(ShapePlan& S, const float* input, int n, int h, int w, hipStream_t st);
     ShapePlan* shape_plan(int n, int h, int w);
 
     Context* ctx_;

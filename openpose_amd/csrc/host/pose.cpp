@@ -61,6 +61,11 @@ PoseHip::~PoseHip()
     }
     for (auto& s : slots_)
         if (s.done) (void)hipEventDestroy(s.done);
+    for (auto& st : scale_streams_)
+        if (st) (void)hipStreamDestroy(st);
+    for (auto& e : join_)
+        if (e) (void)hipEventDestroy(e);
+    if (fork_) (void)hipEventDestroy(fork_);
 }
 
 void PoseHip::set_map_semantics(int maps)
@@ -258,10 +263,43 @@ void PoseHip::submit_multi(const float* const* frames, const int* net_hw, int ns
     // one net pass per scale (poseExtractorCaffe.cpp:240-245); every input shape keeps its own
     // plan and output buffer in NetHip, so the outputs coexist until the merge reads them
     std::vector<NetOutput> outs(nscales);
-    for (int i = 0; i < nscales; ++i) {
-        OPK_CHECK_ARG(frames[i] != nullptr, "NULL scale input");
-        net_->forward(frames[i], n, net_hw[2 * i], net_hw[2 * i + 1]);
-        outs[i] = NetOutput{net_->output(), net_->out_h(), net_->out_w()};
+    for (int i = 0; i < nscales; ++i) OPK_CHECK_ARG(frames[i] != nullptr, "NULL scale input");
+    // the scales' nets are independent until the merge: scales 1.. run on streams of their own
+    // beside scale 0 (small nets leave most CUs idle on their own), each shape with its own plan
+    // and buffers; the context stream waits for all of them before the merge.  Shapes that repeat
+    // would share a plan, so those run in order.
+    bool distinct = dev_switch("MULTISCALE_STREAMS", 1) != 0;
+    for (int i = 0; i < nscales && distinct; ++i)
+        for (int j = 0; j < i; ++j)
+            distinct = distinct && !(net_hw[2 * i] == net_hw[2 * j] && net_hw[2 * i + 1] == net_hw[2 * j + 1]);
+    if (nscales == 1 || !distinct) {
+        for (int i = 0; i < nscales; ++i) {
+            net_->forward(frames[i], n, net_hw[2 * i], net_hw[2 * i + 1]);
+            outs[i] = NetOutput{net_->output(), net_->out_h(), net_->out_w()};
+        }
+    } else {
+        if (!fork_) {
+            OPK_HIP(hipEventCreateWithFlags(&fork_, hipEventDisableTiming));
+            for (int i = 0; i < kMaxResizeSources - 1; ++i) {
+                OPK_HIP(hipStreamCreateWithFlags(&scale_streams_[i], hipStreamNonBlocking));
+                OPK_HIP(hipEventCreateWithFlags(&join_[i], hipEventDisableTiming));
+            }
+        }
+        for (int i = 0; i < nscales; ++i) net_->prepare(n, net_hw[2 * i], net_hw[2 * i + 1]);
+        hipStream_t s = ctx_->stream;
+        net_->time_begin(s);   // one timed region for all the scales' nets of the batch
+        OPK_HIP(hipEventRecord(fork_, s));   // inputs warped, new plans zeroed
+        net_->forward_on(frames[0], n, net_hw[0], net_hw[1], s, false);
+        outs[0] = NetOutput{net_->output(), net_->out_h(), net_->out_w()};
+        for (int i = 1; i < nscales; ++i) {
+            OPK_HIP(hipStreamWaitEvent(scale_streams_[i - 1], fork_, 0));
+            net_->forward_on(frames[i], n, net_hw[2 * i], net_hw[2 * i + 1], scale_streams_[i - 1],
+                             false);
+            outs[i] = NetOutput{net_->output(), net_->out_h(), net_->out_w()};
+            OPK_HIP(hipEventRecord(join_[i - 1], scale_streams_[i - 1]));
+        }
+        for (int i = 1; i < nscales; ++i) OPK_HIP(hipStreamWaitEvent(s, join_[i - 1], 0));
+        net_->time_end(s);
     }
     submit_outputs(outs.data(), nscales, n, net_hw[0], net_hw[1], prod_w, prod_h);
 }

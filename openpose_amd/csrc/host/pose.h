@@ -112,6 +112,9 @@ private:
     double props_[5];
     const float* overlay_ = nullptr;
     hipStream_t copy_ = nullptr;         // D2H of collected batches (overlaps the next batch)
+    // multi-scale: the nets of scales 1.. run on their own streams beside scale 0's
+    hipStream_t scale_streams_[kMaxResizeSources - 1] = {};
+    hipEvent_t fork_ = nullptr, join_[kMaxResizeSources - 1] = {};
     EventTimer timer_;
 
     Slot slots_[2];
