@@ -96,27 +96,26 @@ __global__ __launch_bounds__(DT) void nms_detect_kernel(int* __restrict__ scratc
     }
 }
 
-// Lazy heat map: a workgroup of LT lanes owns LT consecutive columns (x0-1 .. x0+LT-2) of a
+// Lazy heat map: a workgroup of LT lanes (one wave) owns LT consecutive columns (x0-1 .. x0+LT-2) of a
 // (LOY+2)-row window of the resized plane (tile + 1-pixel halo; pixels outside the map = th).
 // Each lane runs resize.hip's two passes down its own column -- horizontal pass of the window's
 // source rows into its LDS column, vertical combinations with the row's (block-uniform, scalar)
 // coefficients -- then the LT-2 x LOY tile pixels are tested from LDS.  The full-resolution stack
 // is never written.
-constexpr int LT = 256;           // lanes = window columns
-constexpr int LOX = LT - 2;       // tile columns
 constexpr int LMAXR = 16;         // source rows per window kept in LDS (x8 upsampling of a
                                   // 34-row window needs 9)
 
 // LOY = tile rows (window rows LOY + 2).  Measured per 64-frame launch (round 1): 16 rows 638 us,
 // 32 rows 774 us, 48 rows 938 us (more, shorter workgroups win); 16 is the one compiled
-template <int LOY>
+template <int LOY, int LT>
 __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ scratch,
                                                              const HeatMap M, int parts, float th)
 {
+    constexpr int LOX = LT - 2;       // tile columns
     constexpr int LWR = LOY + 2;      // window rows
     // hb (horizontal-pass rows) and win (window values) share LDS: a lane only ever touches its
     // own column of either before the barrier, and win is written after the last hb read
-    static_assert(LMAXR <= LWR, "hb fits in win");
+    constexpr int HBR = LWR < LMAXR ? LWR : LMAXR;   // horizontal-pass rows that fit in win
     __shared__ float win[LWR * LT];
     float* hb = win;
     const int tid = threadIdx.x;
@@ -147,7 +146,7 @@ __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ s
         const int r_lo = heat_clampi(S.yofs[ry_lo] - 1, 0, S.sh - 1);
         const int r_hi = heat_clampi(S.yofs[ry_hi] + 2, 0, S.sh - 1);
         const int nrows = r_hi - r_lo + 1;
-        const bool tiled = nrows <= LMAXR;   // block-uniform
+        const bool tiled = nrows <= HBR;     // block-uniform
         if (n > 0) __syncthreads();          // previous source's row tables fully read
         if (tid < LWR) {
             const int y = heat_clampi(y0 + tid, 0, H - 1);
@@ -373,8 +372,12 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
                            heat.channels, parts, h, w, threshold, heat.cuda);
     } else {
         constexpr int loy = 16;
-        hipLaunchKernelGGL(nms_detect_lazy_kernel<loy>, dim3((w + LOX - 1) / LOX, (h + loy - 1) / loy,
-                           frames * parts), dim3(LT), 0, stream, scratch, heat, parts, threshold);
+        // one-wave workgroups (64 columns, 62 tested): no workgroup barrier holds four waves on
+        // each other and a CU keeps ~4x more windows' loads in flight (measured 752 -> 650-672 us
+        // per 64-frame launch against 256-lane workgroups; 8 / 32-row windows 711 / 700 us)
+        hipLaunchKernelGGL((nms_detect_lazy_kernel<loy, 64>),
+                           dim3((w + 61) / 62, (h + loy - 1) / loy, frames * parts), dim3(64), 0,
+                           stream, scratch, heat, parts, threshold);
     }
     OPK_LAUNCH_CHECK();
     dim3 g2(parts, frames);
