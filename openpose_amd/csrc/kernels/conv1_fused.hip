@@ -34,6 +34,10 @@ typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
 typedef float float4_t __attribute__((ext_vector_type(4)));
 typedef float float2_t __attribute__((ext_vector_type(2)));
 
+#ifndef OPK1_ABLATE   // dev probe only (variant builds): 1 no conv1_1 gather / MFMAs, 2 no conv1_2
+#define OPK1_ABLATE 0  // MFMAs, 3 no epilogue + pooling (timing only, wrong results)
+#endif
+
 constexpr int TR = 6, TC = 62, VW = 64;       // tile rows / columns; virtual row width
 constexpr int MT = TR * VW;                   // GEMM rows per tile (384)
 constexpr int HROWS = (TR + 2) * VW + 8;      // halo rows (+ overflow of the last taps)
@@ -102,13 +106,16 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
         const float4_t s2 = *reinterpret_cast<const float4_t*>(a.s2 + ch);
         m2[g] = a.act2 == 2 ? s2 : float4_t{neg2, neg2, neg2, neg2};
     }
-    // this lane's 8 conv1_1 K values: patch offset of (ci, ky, kx) for k = 8q + e, -1 past 26
+    // this lane's 8 conv1_1 K values: patch offset of (ci, ky, kx) for k = 8q + e; K padding
+    // (k > 26) reads offset 0 and is zeroed after the read, so the eight reads issue back to back
     int off[8];
+    unsigned kvalid = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const int k = 8 * q + e;
         const int t = k / 3, ci = k - 3 * (k / 3);
-        off[e] = k < 27 ? (ci * PR + t / 3) * PC + (t - 3 * (t / 3)) : -1;
+        off[e] = k < 27 ? (ci * PR + t / 3) * PC + (t - 3 * (t / 3)) : 0;
+        kvalid |= (k < 27 ? 1u : 0u) << e;
     }
 
 #define OPK1_ORIGIN(tile_, f_, y0_, x0_)                                                       \
@@ -154,26 +161,48 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
         __syncthreads();
 
         // ---- conv1_1 over the (TR+2) x 64 halo: 32 groups of 16 positions, 4 per wave ------
+        // all 32 patch reads of the wave's 4 groups first (one LDS round trip), then the MFMAs
+        float xv[4][8];
+#pragma unroll
+        for (int gi = 0; gi < 4; ++gi) {
+            const int mh = (wave * 4 + gi) * 16 + r16;
+            const int base = (mh >> 6) * PC + (mh & 63);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) xv[gi][e] = patch[off[e] + base];
+        }
+        // the 16 MFMAs of the wave's 4 groups, then their epilogues (no MFMA result is waited
+        // for right after its issue)
+        float4_t c1[4][4];
+#pragma unroll
+        for (int gi = 0; gi < 4; ++gi) {
+            half8_t xf;
+#pragma unroll
+            for (int e = 0; e < 8; ++e)
+                xf[e] = OPK1_ABLATE == 1 ? (_Float16)0.f
+                        : ((kvalid >> e) & 1u) ? (_Float16)xv[gi][e] : (_Float16)0.f;
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                c1[gi][g] = OPK1_ABLATE == 1 ? float4_t{(float)xf[0], 0.f, 0.f, 0.f}
+                    : __builtin_amdgcn_mfma_f32_16x16x32_f16(w1f[g], xf, float4_t{0.f, 0.f, 0.f, 0.f},
+                                                             0, 0, 0);
+        }
 #pragma unroll
         for (int gi = 0; gi < 4; ++gi) {
             const int mh = (wave * 4 + gi) * 16 + r16;       // halo position
             const int hr = mh >> 6, hc = mh & 63;
-            half8_t xf;
-#pragma unroll
-            for (int e = 0; e < 8; ++e)
-                xf[e] = off[e] >= 0 ? (_Float16)patch[off[e] + hr * PC + hc] : (_Float16)0.f;
             const int y = y0 - 1 + hr, x = x0 - 1 + hc;
             const bool in = y >= 0 && y < H && x >= 0 && x < W;
             uint32_t pk[4][2];
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
-                float4_t c1 = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1f[g], xf, float4_t{0.f, 0.f, 0.f, 0.f},
-                                                                     0, 0, 0);
-                const float4_t t = c1 + b1[g];
+                const float4_t t = c1[gi][g] + b1[g];
                 const float4_t tm = t * m1[g];
                 float v[4];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = in ? (t[r] > 0.f ? t[r] : tm[r]) : 0.f;
+                for (int r = 0; r < 4; ++r) {
+                    const float a_ = t[r] > 0.f ? t[r] : tm[r];
+                    v[r] = in ? a_ : 0.f;
+                }
                 pk[g][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
                 pk[g][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
             }
@@ -197,29 +226,48 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
         for (int i = 0; i < 3; ++i)
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+        // 18 K steps (2 channel chunks x 9 taps); step s+1's fragments are read while step s's
+        // MFMAs issue (two register sets, the issue order pinned by sched_barrier)
+        half8_t fa[2][3], fb[2][4];
+#define OPK1_READ(buf_, st_)                                                                  \
+    do {                                                                                      \
+        const int c_ = (st_) / 9, tap_ = (st_) - 9 * ((st_) / 9);                             \
+        const int ky_ = tap_ / 3, kx_ = tap_ - 3 * (tap_ / 3);                                \
+        const uint4* As_ = HALO + c_ * HROWS * 4;                                             \
+        const uint4* Bs_ = W2 + (c_ * 9 + tap_) * 256;                                        \
+        _Pragma("unroll") for (int i_ = 0; i_ < 3; ++i_)                                      \
+            fa[buf_][i_] = __builtin_bit_cast(                                                \
+                half8_t, As_[swz64(wave * 48 + i_ * 16 + r16 + ky_ * VW + kx_, q)]);            \
+        _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_)                                      \
+            fb[buf_][j_] = __builtin_bit_cast(half8_t, Bs_[swz64(j_ * 16 + r16, q)]);           \
+    } while (0)
+        OPK1_READ(0, 0);
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
-            const uint4* As = HALO + c * HROWS * 4;
+        for (int st = 0; st < 18; ++st) {
+            const int cur = st & 1;
+            if (st + 1 < 18) OPK1_READ(cur ^ 1, st + 1);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int tap = 0; tap < 9; ++tap) {
-                const int ky = tap / 3, kx = tap - 3 * (tap / 3);
-                const uint4* Bs = W2 + (c * 9 + tap) * 256;
-                half8_t fa[3], fb[4];
-#pragma unroll
-                for (int i = 0; i < 3; ++i)
-                    fa[i] = __builtin_bit_cast(half8_t, As[swz64(wave * 48 + i * 16 + r16 + ky * VW + kx, q)]);
+            for (int i = 0; i < 3; ++i)
 #pragma unroll
                 for (int j = 0; j < 4; ++j)
-                    fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(j * 16 + r16, q)]);
-#pragma unroll
-                for (int i = 0; i < 3; ++i)
-#pragma unroll
-                    for (int j = 0; j < 4; ++j)
-                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-            }
+                    if (OPK1_ABLATE == 2)
+                        asm volatile("; mfma skipped" : "+v"(acc[i][j]) : "v"(fb[cur][j]), "v"(fa[cur][i]));
+                    else
+                        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[cur][j], fa[cur][i],
+                                                                           acc[i][j], 0, 0, 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
+#undef OPK1_READ
         __syncthreads();   // every wave is done reading the halo: T may overwrite it
 
+        if (OPK1_ABLATE == 3) {   // keep the accumulators alive, skip epilogue and pooling
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 4; ++j) asm volatile("" :: "v"(acc[i][j]));
+            continue;
+        }
         // ---- bias + activation -> fp16 tile [m][64 ch] -----------------------------------------
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
