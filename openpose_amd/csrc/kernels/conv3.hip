@@ -764,6 +764,13 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     const int nn = (a.cout + s.bn - 1) / s.bn;
     const long ntiles = ((total + s.bm - 1) / s.bm) * nn;
     dim3 grid((unsigned)ntiles);
+    // several 128-channel n-blocks (the VGG 256 / 512-channel layers): conv3w8 with one n-block
+    // per persistent block (bit-identical; CONV3W8N=0: the 16-wave conv3_kernel)
+    if (s.nw == 16 && s.persist && nn > 1 && s.bn == 128 && a.sink && !a.out32 && VW > 16 &&
+        dev_switch("CONV3W8N", 1) != 0 && conv3w8_supported(a)) {
+        launch_conv3w8(a, stream);
+        return;
+    }
     // measured: +3-10 % on the single-n-block layers, 3-8 % slower with 2-4 n-blocks (kept 16-wave)
     if (s.nw == 16 && s.persist && nn == 1 && a.sink && a.cus >= nn && a.cout % s.bn == 0 && !a.out32 &&
         VW > 16) {

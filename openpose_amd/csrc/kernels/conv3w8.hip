@@ -45,7 +45,7 @@ constexpr int k8_BM = 512, k8_HR = 688, k8_NW = 8;
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst_) : "v"(addr_), "i"(off_))
 #endif
 
-template <int BN>
+template <int BN, int NB>
 __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a)
 {
     constexpr int NW = k8_NW, BM = k8_BM, HR = k8_HR;
@@ -71,22 +71,30 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     const int r16 = lane & 15, q = lane >> 4;
     const Strips g(a);
     const int ntm = (g.total + BM - 1) / BM;
-    const int G = gridDim.x;
+    // output-channel blocks of BN: tile t = (m-tile t / NB, n-block t % NB);
+    // the grid is a multiple
+    // of NB (host), so a block keeps one n-block -- its weights and bias -- for the whole launch
+    // and walks the m-tiles m0, m0 + G / NB, ...; the NB n-blocks of one m-tile sit on one XCD
+    static_assert(NB == 1 || NB == 2 || NB == 4, "1, 2 or 4 n-blocks");
+    constexpr int LGNB = NB == 4 ? 2 : NB - 1;
+    const int G = gridDim.x, GM = G >> LGNB;
     const int xcd = blockIdx.x & 7, qq = G >> 3, rr = G & 7;
     const int tix = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (blockIdx.x >> 3);
-    int m = tix;
+    const int nblk = tix & (NB - 1);
+    int m = tix >> LGNB;
     if (m >= ntm) return;
 
     if (tid < BN) {
         const float neg = a.act == 1 ? 0.f : 1.f;
-        lbias[tid] = a.bias[tid];
-        lmul[tid] = a.act == 2 ? a.slope[tid] : neg;
+        lbias[tid] = a.bias[nblk * BN + tid];
+        lmul[tid] = a.act == 2 ? a.slope[nblk * BN + tid] : neg;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     const int lrow = lane >> 2, phys = lane & 3;
     const int cpt = a.cin_pad >> 5;
     const int U = 3 * cpt;
+    const int ublk = nblk * U;   // the n-block's first K unit in the packed weights
     const int bi = (BPI - wave + NW - 1) / NW;
     // weight piece of B DMA instruction j (recomputed at each issue: registers)
 #define OPK8_BOFF(j_)                                                                         \
@@ -117,12 +125,12 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                 if (API % NW == 0 || i_ * NW + wave < API)                                    \
                     __builtin_amdgcn_global_load_lds(                                         \
                         (const void*)(abase + (c_) * 64 +                                     \
-                                      ((nt_) ? OPK8_AROW1(m + G, i_) : aoff[i_])),            \
+                                      ((nt_) ? OPK8_AROW1(m + GM, i_) : aoff[i_])),            \
                         (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * NW + wave) * 64]), \
                         16, 0, 0);                                                            \
         }                                                                                     \
         const int bs_ = 2 * ASLOT + (bslot_) * BSLOT;                                         \
-        const uint16_t* ub_ = a.w + (size_t)((c_) * 3 + (ky_)) * BROWS * 32;                  \
+        const uint16_t* ub_ = a.w + (size_t)(ublk + (c_) * 3 + (ky_)) * BROWS * 32;                  \
         _Pragma("unroll") for (int j_ = 0; j_ < BIW; ++j_)                                    \
             if (BPI % NW == 0 || j_ * NW + wave < BPI) {                                      \
                 const int bo_ = OPK8_BOFF(j_);                                                \
@@ -242,7 +250,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
 
     int gc = 0;   // running chunk index of this tile's chunk 0 (halo slot parity)
     for (;;) {
-        const int mn = m + G;
+        const int mn = m + GM;
         const bool has_next = mn < ntm;
         for (int u = 0; u < U; ++u) {
             const int c = u / 3, ky = u - 3 * (u / 3);
@@ -277,7 +285,8 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         }
 
         // ---- epilogue: bias + activation + fp16 pack, 16-byte stores (border lanes to the sink)
-        const int el = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        int el = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        asm volatile("" : "+v"(el));   // recomputed per tile: nothing lane-dependent kept (spilled)
         const int er16 = el & 15, eq = el >> 4;
         const int sidx = blockIdx.x * 64 * NW + wave * 64 + el;
         uint4* sink4 = reinterpret_cast<uint4*>(a.sink) + sidx;
@@ -309,7 +318,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         }
         const char* lb = reinterpret_cast<const char*>(lbias) + 4 * eq * 4;
         const int nd = a.ndst;
-        uint16_t* const d0 = a.dst[0] + a.dst_coff[0];
+        uint16_t* const d0 = a.dst[0] + a.dst_coff[0] + nblk * BN;
         const int cs0 = a.dst_cs[0];
 #pragma unroll
         for (int j = 0; j < NF; j += 2) {
@@ -341,7 +350,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                     *(pok[i] ? p : sink4) = val;
                 } else {
                     for (int d = 0; d < nd; ++d) {
-                        uint4* p = reinterpret_cast<uint4*>(a.dst[d] + a.dst_coff[d] + ch +
+                        uint4* p = reinterpret_cast<uint4*>(a.dst[d] + a.dst_coff[d] + nblk * BN + ch +
                                                             (size_t)prow[i] * a.dst_cs[d]);
                         *(pok[i] ? p : sink4) = val;
                     }
@@ -380,19 +389,25 @@ bool conv3w8_supported(const ConvArgs& a)
     // mid-unit assumes a single destination
     bool aligned = a.ndst == 1;
     for (int d = 0; d < a.ndst; ++d) aligned = aligned && ((a.dst_coff[d] | a.dst_cs[d]) & 7) == 0;
-    return a.ntaps == 9 && (a.cout == 128 || a.cout == 96) && a.sink && a.cus > 0 && !a.out32 &&
-           aligned && a.sw + 2 * a.border > 16;
+    // 96 or 128 channels, or several 128-channel blocks (the VGG 256 / 512-channel layers)
+    const bool nb_ok = a.cout == 96 || a.cout == 128 || a.cout == 256 || a.cout == 512;
+    return a.ntaps == 9 && nb_ok && a.sink && a.cus > 0 && !a.out32 && aligned &&
+           a.sw + 2 * a.border > 16;
 }
 
 void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
 {
-    OPK_CHECK_ARG(conv3w8_supported(a), "conv3w8: 96 / 128 output channels, 3x3, one aligned slice");
+    OPK_CHECK_ARG(conv3w8_supported(a), "conv3w8: 96 or k x 128 output channels, 3x3, one aligned slice");
     const long total = (long)a.frames * a.nstrips * (a.H + 2 * a.border) * (a.sw + 2 * a.border);
     const long ntm = (total + k8_BM - 1) / k8_BM;
-    const unsigned G = (unsigned)std::min<long>(a.cus, ntm);
-    OPK_CHECK_ARG(G <= 1024, "persistent grid exceeds the sink");
-    if (a.cout == 128) hipLaunchKernelGGL((conv3w8_kernel<128>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
-    else hipLaunchKernelGGL((conv3w8_kernel<96>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
+    const int nb = a.cout == 96 ? 1 : a.cout / 128;
+    // a multiple of the n-block count (each block keeps one n-block)
+    const unsigned G = (unsigned)(std::min<long>(a.cus / nb, ntm) * nb);
+    OPK_CHECK_ARG(G >= 1 && G <= 1024, "persistent grid exceeds the sink");
+    if (nb == 4) hipLaunchKernelGGL((conv3w8_kernel<128, 4>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
+    else if (nb == 2) hipLaunchKernelGGL((conv3w8_kernel<128, 2>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
+    else if (a.cout == 128) hipLaunchKernelGGL((conv3w8_kernel<128, 1>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
+    else hipLaunchKernelGGL((conv3w8_kernel<96, 1>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
     OPK_LAUNCH_CHECK();
 }
 

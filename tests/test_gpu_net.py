@@ -214,7 +214,8 @@ VARIANTS = {"persistent": {}, "persistent_conv3p": {"CONV3W": 0}, "w16": {"CONV3
             "dwordx2": {"CONV3W": 0, "CONV3P_WIDE": 0, "CONV3_WIDE": 0},
             "w16_dwordx2": {"CONV3_PERSIST": 0, "CONV3_WIDE": 0},
             "conv1_512x128": {"CONV1_TILE": 1}, "conv1_256x256": {"CONV1_TILE": 2},
-            "conv1_512x64": {"CONV1_N64W16": 1}}
+            "conv1_512x64": {"CONV1_N64W16": 1},
+            "nblocks_16wave": {"CONV3W8N": 0}}
 ROUNDING_VARIANTS = set()   # variants with another MFMA shape (another fp32 summation order)
 
 
@@ -228,7 +229,8 @@ def test_conv3_tile_variants_bit_identical(ctx):
     L += conv("c5", "c4", 96, 3, "relu")
     L.append(dict(name="cat", type="Concat", bottom=["c3", "c5"], top=["cat"]))
     L += conv("c6", "cat", 128, 3, "prelu") + conv("c6b", "c6", 256, 3, "relu")
-    L += conv("c6c", "c6b", 512, 1, "prelu") + conv("c7", "c6c", 52, 1)
+    L += conv("c6d", "c6b", 512, 3, "prelu")   # 2 and 4 n-blocks of 128 (conv3w8 n-block grid)
+    L += conv("c6c", "c6d", 512, 1, "prelu") + conv("c7", "c6c", 52, 1)
     L.append(dict(name="net_output", type="Concat", bottom=["c7"], top=["net_output"]))
     text = prototxt.emit(L)
     graph = prototxt.parse(text)
