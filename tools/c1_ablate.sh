@@ -1,3 +1,10 @@
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/c1 && \
-timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c1/base -o run -- python bench.py --steps 6 --warmup 2 --no-cpu-baseline > gpurun_out/c1/base.log 2>&1 && \
-for v in 1 2 3; do OPK_LIB_PATH=$GRAFT_REPO_ROOT/openpose_amd/variants/libopk_c1a$v.so timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/c1/a$v -o run -- python bench.py --steps 6 --warmup 2 --no-cpu-baseline > gpurun_out/c1/a$v.log 2>&1 || exit 1; done
+#!/bin/bash
+# dev: conv1_fused ablation / A-B builds (openpose_amd/variants/libopk_<name>.so) under a short
+# profiled bench each, one GPU call:   c1_ablate.sh OUTDIR name ...   ("base" = the product build)
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+out=gpurun_out/$1; shift
+mkdir -p $out
+for v in "$@"; do
+  lib=""; [ "$v" != "base" ] && lib=$GRAFT_REPO_ROOT/openpose_amd/variants/libopk_$v.so
+  OPK_LIB_PATH=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d $out/$v -o run -- python bench.py --steps 6 --warmup 2 --no-cpu-baseline > $out/$v.log 2>&1 || exit 1
+done
