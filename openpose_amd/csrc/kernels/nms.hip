@@ -32,39 +32,53 @@ constexpr int DT = 256;   // detect lanes per block
 constexpr int FT = 256;   // finalize lanes per block
 constexpr int CAP = kNmsCandidates;
 
-// peak rules of nmsCpu for pixel (x, y) of value v; get(x, y) reads an in-map neighbour.
+// peak rules of nmsCpu for pixel (x, y) of value v; GET_(x, y) reads an in-map neighbour.
 // cuda: nmsRegisterKernel's (nmsBase.cu:50-90) -- interior pixels only (0 < x < w-1, 0 < y < h-1),
 // v > th and v > all 8 neighbours
+#define OPK_PEAK_RULES(GET_)                                                                  \
+    do {                                                                                      \
+        if (!(v > th)) return false;                                                          \
+        if (cuda) {                                                                           \
+            if (!(x > 0 && x < w - 1 && y > 0 && y < h - 1)) return false;                    \
+            return v > GET_(x - 1, y - 1) && v > GET_(x, y - 1) && v > GET_(x + 1, y - 1) &&  \
+                   v > GET_(x - 1, y) && v > GET_(x + 1, y) && v > GET_(x - 1, y + 1) &&      \
+                   v > GET_(x, y + 1) && v > GET_(x + 1, y + 1);                              \
+        }                                                                                     \
+        if (x > 1 && x < w - 2 && y > 1 && y < h - 2) {                                       \
+            return v > GET_(x - 1, y - 1) && v > GET_(x, y - 1) && v > GET_(x + 1, y - 1) &&  \
+                   v > GET_(x - 1, y) && v > GET_(x + 1, y) && v > GET_(x - 1, y + 1) &&      \
+                   v > GET_(x, y + 1) && v > GET_(x + 1, y + 1);                              \
+        }                                                                                     \
+        if (x == 1 || x == w - 2 || y == 1 || y == h - 2) {                                   \
+            bool ok = true;                                                                   \
+            _Pragma("unroll") for (int dy = -1; dy <= 1; ++dy)                                \
+            _Pragma("unroll") for (int dx = -1; dx <= 1; ++dx) {                              \
+                if (dx == 0 && dy == 0) continue;                                             \
+                const int xx = x + dx, yy = y + dy;                                           \
+                const float nb = (xx >= 0 && xx < w && yy >= 0 && yy < h) ? GET_(xx, yy) : th; \
+                ok = ok && (v >= nb);                                                         \
+            }                                                                                 \
+            return ok;                                                                        \
+        }                                                                                     \
+        return false;                                                                         \
+    } while (0)
+
 template <typename Get>
 __device__ __forceinline__ bool peak_at(Get get, int w, int h, float th, int x, int y, float v,
                                         bool cuda = false)
 {
-    if (!(v > th)) return false;
-    if (cuda) {
-        if (!(x > 0 && x < w - 1 && y > 0 && y < h - 1)) return false;
-        return v > get(x - 1, y - 1) && v > get(x, y - 1) && v > get(x + 1, y - 1) &&
-               v > get(x - 1, y) && v > get(x + 1, y) && v > get(x - 1, y + 1) &&
-               v > get(x, y + 1) && v > get(x + 1, y + 1);
-    }
-    if (x > 1 && x < w - 2 && y > 1 && y < h - 2) {
-        return v > get(x - 1, y - 1) && v > get(x, y - 1) && v > get(x + 1, y - 1) &&
-               v > get(x - 1, y) && v > get(x + 1, y) && v > get(x - 1, y + 1) &&
-               v > get(x, y + 1) && v > get(x + 1, y + 1);
-    }
-    if (x == 1 || x == w - 2 || y == 1 || y == h - 2) {
-        bool ok = true;
-#pragma unroll
-        for (int dy = -1; dy <= 1; ++dy)
-#pragma unroll
-            for (int dx = -1; dx <= 1; ++dx) {
-                if (dx == 0 && dy == 0) continue;
-                const int xx = x + dx, yy = y + dy;
-                const float nb = (xx >= 0 && xx < w && yy >= 0 && yy < h) ? get(xx, yy) : th;
-                ok = ok && (v >= nb);
-            }
-        return ok;
-    }
-    return false;
+    OPK_PEAK_RULES(get);
+}
+
+// the same rules on the lazily evaluated heat map itself.  Not a lambda over M: a closure holding
+// a reference to the by-value kernel argument made the compiler copy the whole HeatMap to scratch
+// at every nms_finalize_kernel start (496 B per lane, 203 MB of writes per 64-frame launch)
+__device__ __forceinline__ bool peak_at_heat(const HeatMap& M, int pln, int w, int h, float th, int x,
+                                             int y, float v, bool cuda)
+{
+#define OPK_HEAT_GET(xx_, yy_) heat_at(M, pln, xx_, yy_)
+    OPK_PEAK_RULES(OPK_HEAT_GET);
+#undef OPK_HEAT_GET
 }
 
 __device__ __forceinline__ void push_candidate(int* plane, int idx)
@@ -218,7 +232,7 @@ __global__ __launch_bounds__(LT) void nms_detect_lazy_kernel(int* __restrict__ s
     }
 }
 
-__device__ void refine_write(float* __restrict__ out, const HeatMap& M, int plane, int idx,
+__device__ __forceinline__ void refine_write(float* __restrict__ out, const HeatMap& M, int plane, int idx,
                              int rank, float offx, float offy)
 {
     const int w = M.w, h = M.h;
@@ -260,7 +274,6 @@ __global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ pe
     const int c = blockIdx.x, b = blockIdx.y;
     const int pln = b * M.channels + c;
     const int h = M.h, w = M.w;
-    auto get = [&M, pln](int xx, int yy) { return heat_at(M, pln, xx, yy); };
     float* out = peaks + ((size_t)b * parts + c) * max_peaks1 * 3;
     int* plane = scratch + ((size_t)b * parts + c) * (CAP + 1);
     const int tid = threadIdx.x;
@@ -306,7 +319,8 @@ __global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ pe
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
                     const int x = x0 + k;
-                    if (x < w && peak_at(get, w, h, th, x, y, get(x, y), M.cuda != 0)) mask |= 1u << k;
+                    if (x < w && peak_at_heat(M, pln, w, h, th, x, y, heat_at(M, pln, x, y), M.cuda != 0))
+                        mask |= 1u << k;
                 }
             }
             const int cnt = __popc(mask);
