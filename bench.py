@@ -140,12 +140,26 @@ def pmc_traffic(batch):
     return None
 
 
-def rank_main(args, rank, world, local):
-    torch.cuda.set_device(local)
+def dist_setup(world, local):
+    """Device and process group of this rank: its own GPU and RCCL.  OPK_BENCH_REHEARSE=1 (dev, a
+    1-GPU box): every rank on GPU 0 with gloo, to run the N-rank launcher, the ordered gather in
+    the timed loop and the max-over-ranks timing on real hardware (the ranks share the GPU, so the
+    throughput of such a run means nothing)."""
+    rehearse = os.environ.get("OPK_BENCH_REHEARSE") == "1"
+    dev = 0 if rehearse else local
+    torch.cuda.set_device(dev)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return dev, dist, "cpu" if rehearse else "cuda"
+
+
+def rank_main(args, rank, world, local):
+    local, dist, comm_dev = dist_setup(world, local)
 
     from openpose_amd import synth
     from openpose_amd.api import Context, Net, PoseExtractor, dev_switches, scale_and_size
@@ -181,7 +195,7 @@ def rank_main(args, rank, world, local):
 
     # per-step ordered gather of the per-frame records (capacity: 4x the synthetic people + 8)
     cap = B * (1 + (4 * args.people + 8) * (PARTS * 3 + 1))
-    gather = parallel.RecordGather(world, rank, cap, args.steps, "cuda")
+    gather = parallel.RecordGather(world, rank, cap, args.steps, comm_dev)
 
     # Two-stage pipeline (opk_pose_submit / opk_pose_collect): the device work of batch i+1 is
     # enqueued before the host assembly of batch i, which then overlaps it.
@@ -237,7 +251,7 @@ def rank_main(args, rank, world, local):
     post_ms /= npost
     per_rank = [[rank, elapsed, net_ms, post_ms]]
     if dist is not None:
-        t = torch.tensor([rank, elapsed, net_ms, post_ms], device="cuda", dtype=torch.float64)
+        t = torch.tensor([rank, elapsed, net_ms, post_ms], device=comm_dev, dtype=torch.float64)
         allr = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(allr, t)
         per_rank = [x.tolist() for x in allr]
@@ -283,8 +297,9 @@ def rank_main(args, rank, world, local):
             "net_input": [NET_H, NET_W],
             "net_inputs_all_scales": [[h, w] for (w, h) in net_sizes],
             "heatmaps": [78, NET_H, NET_W],
-            "parallelism": "frame-parallel replicas x%d (one process per GPU, RCCL ordered "
-                           "gather of per-frame records to rank 0)" % world,
+            "parallelism": ("frame-parallel replicas x%d (one process per GPU, RCCL ordered "
+                            "gather of per-frame records to rank 0)" % world) if comm_dev == "cuda"
+                           else "REHEARSAL x%d: every rank on GPU 0, gloo gather" % world,
             "compute": "warp u8 fixed-point; conv fp16 x fp16 -> fp32 MFMA; resize/NMS/PAF fp32",
             "people_per_frame_found": people,
             "net_output_std_before_overlay": None if out_std is None else round(out_std, 5),
@@ -334,11 +349,7 @@ def rank_main(args, rank, world, local):
 def rank_main_body135(args, rank, world, local):
     """BASELINE configs[4]: post-processing stress through the injection path (no CNN: the
     reference has no BODY_135 network); frames/s and the post-processing HBM roofline."""
-    torch.cuda.set_device(local)
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    local, dist, comm_dev = dist_setup(world, local)
     from openpose_amd import synth
     from openpose_amd.api import Context, PoseExtractor, pose_model_info
     from openpose_amd.pose_tables import BODY_135, CONNECT_GPU
@@ -358,7 +369,7 @@ def rank_main_body135(args, rank, world, local):
     pose = PoseExtractor(ctx, None, pose_model=BODY_135, semantics=CONNECT_GPU)
     parts = t["parts"]
     cap = B * (1 + (4 * people + 8) * (parts * 3 + 1))
-    gather = parallel.RecordGather(world, rank, cap, args.steps, "cuda")
+    gather = parallel.RecordGather(world, rank, cap, args.steps, comm_dev)
     rec_buf = np.empty(cap, np.float32)
     collected = [0]
 
@@ -400,7 +411,7 @@ def rank_main_body135(args, rank, world, local):
     pose.set_timing(False)
     post_ms /= max(npost, 1)
     if dist is not None:
-        tt = torch.tensor([elapsed, post_ms], device="cuda", dtype=torch.float64)
+        tt = torch.tensor([elapsed, post_ms], device=comm_dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, post_ms = float(tt[0]), float(tt[1])
     total_frames = world * B * args.steps
