@@ -41,7 +41,10 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     constexpr int N2P = NF2 * 16;
     constexpr int ASLOT = BM * 4, BSLOT = N1 * 4;            // 16-byte pieces per ring slot
     constexpr int RING = 3 * (ASLOT + BSLOT);
-    constexpr int PART = NW * WROWS * N2P / 4;                // partial products (float4 pieces)
+    // partial products (float4 pieces), rows padded by one piece: at N2P / 4 pieces a row, the 16
+    // rows of a fragment fall on the same banks (PMC: 60 % of the LDS cycles were bank conflicts)
+    constexpr int PSTRIDE = N2P / 4 + 1;
+    constexpr int PART = NW * WROWS * PSTRIDE;
     constexpr int MAIN = RING > PART ? RING : PART;
     constexpr int LDS_PIECES = MAIN + N1 / 2;                 // + bias / multiplier of Mconv6
     static_assert(LDS_PIECES * 16 <= 160 * 1024, "LDS budget");
@@ -174,7 +177,7 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     for (int i = 0; i < MF; ++i)
 #pragma unroll
         for (int f = 0; f < NF2; ++f)
-            part[(wave * WROWS + i * 16 + r16) * (N2P / 4) + f * 4 + q] = acc2[i][f];
+            part[(wave * WROWS + i * 16 + r16) * PSTRIDE + f * 4 + q] = acc2[i][f];
     __syncthreads();
     for (int f = wn; f < NF2; f += WN1) {
         const int ch = f * 16 + 4 * q;   // this lane's 4 output channels
@@ -183,9 +186,9 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
             const int row = wm * WROWS + i * 16 + r16;
-            float4_t v = part[((wm * WN1) * WROWS + row - wm * WROWS) * (N2P / 4) + f * 4 + q];
+            float4_t v = part[((wm * WN1) * WROWS + row - wm * WROWS) * PSTRIDE + f * 4 + q];
             for (int w = 1; w < WN1; ++w)
-                v = v + part[((wm * WN1 + w) * WROWS + row - wm * WROWS) * (N2P / 4) + f * 4 + q];
+                v = v + part[((wm * WN1 + w) * WROWS + row - wm * WROWS) * PSTRIDE + f * 4 + q];
             v = v + b7;
             const int p = p0 + row;
             if (p >= total) continue;
