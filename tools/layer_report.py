@@ -3,7 +3,8 @@
     python tools/layer_report.py <kernel_trace.csv> <frames_per_step> [--layers]
 
 Maps the kernels of one forward (the second to last) onto the BODY_25 conv/pool layers; a
-conv1_fused_kernel launch stands for conv1_1 + conv1_2 + pool1_stage1.
+conv1_fused_kernel launch stands for conv1_1 + conv1_2 + pool1_stage1, a conv_head_kernel launch for a
+stage's Mconv6 + Mconv7.
 """
 import csv
 import sys
@@ -42,6 +43,14 @@ for r in fw:
         lvl = 1
         if per_layer:
             print('%-28s %8.1f us %7.1f TF/s' % (key[0], d, fl / d / 1e6))
+    elif 'conv_head' in name:   # Mconv6 (1x1, PReLU) + Mconv7 (1x1) of one stage
+        l6, l7 = L[li], L[li + 1]
+        li += 2
+        fl = flops(l6, lvl) + flops(l7, lvl)
+        key = ('Mconv6+Mconv7 N1=%d' % l6['num_output'], 1, lvl)
+        if per_layer:
+            print('%-28s cin=%4d mid=%4d cout=%4d k=1 lvl=%d %8.1f us %7.1f TF/s' %
+                  (l6['name'] + '+7', l6['cin'], l6['num_output'], l7['num_output'], lvl, d, fl / d / 1e6))
     else:
         l = L[li]
         li += 1

@@ -70,6 +70,44 @@ __global__ __launch_bounds__(256) void mfma_peak(const half8_t* __restrict__ in,
     out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
+// the 32x32x16 shape: twice the MACs per operand register read, four times the accumulator
+// registers per instruction (4 chains of 16 floats)
+typedef float float16_t __attribute__((ext_vector_type(16)));
+__global__ __launch_bounds__(256) void mfma_peak32(const half8_t* __restrict__ in,
+                                                   float* __restrict__ out, int iters)
+{
+    const int lane = threadIdx.x & 63;
+    half8_t a[4], b[2];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) a[k] = in[(k * 64 + lane) % 512];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) b[k] = in[((4 + k) * 64 + lane) % 512];
+    float16_t acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[k][e] = 0.f;
+    for (int i = 0; i < iters; i += 2) {
+        asm volatile(
+            "v_mfma_f32_32x32x16_f16 %0, %4, %8, %0\n"
+            "v_mfma_f32_32x32x16_f16 %1, %5, %8, %1\n"
+            "v_mfma_f32_32x32x16_f16 %2, %6, %9, %2\n"
+            "v_mfma_f32_32x32x16_f16 %3, %7, %9, %3\n"
+            "v_mfma_f32_32x32x16_f16 %0, %5, %9, %0\n"
+            "v_mfma_f32_32x32x16_f16 %1, %6, %9, %1\n"
+            "v_mfma_f32_32x32x16_f16 %2, %7, %8, %2\n"
+            "v_mfma_f32_32x32x16_f16 %3, %4, %8, %3\n"
+            : "+v"(acc[0]), "+v"(acc[1]), "+v"(acc[2]), "+v"(acc[3])
+            : "v"(a[0]), "v"(a[1]), "v"(a[2]), "v"(a[3]), "v"(b[0]), "v"(b[1]));
+    }
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) s += acc[k][e];
+    out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+
 __global__ __launch_bounds__(256) void hbm_read(const vf4* __restrict__ p, size_t n,
                                                 float* __restrict__ out)
 {
@@ -138,6 +176,11 @@ int main(int argc, char** argv)
             const double flop = (double)blocks * 4 * iters * 8 * 16384.0;
             std::printf("mfma_f32_16x16x32_f16 %s operands, %d waves/SIMD: %.1f TFLOP/s (%.3f ms)\n",
                         random ? "random" : "zero", wps, flop / ms / 1e9, ms);
+            const float ms32 = time_ms([&] { hipLaunchKernelGGL(mfma_peak32, dim3(blocks), dim3(256), 0, 0,
+                                                                din, dout, iters); }, 5);
+            const double flop32 = (double)blocks * 4 * iters * 4 * 32768.0;
+            std::printf("mfma_f32_32x32x16_f16 %s operands, %d waves/SIMD: %.1f TFLOP/s (%.3f ms)\n",
+                        random ? "random" : "zero", wps, flop32 / ms32 / 1e9, ms32);
         }
     }
     CK(hipFree(din));
