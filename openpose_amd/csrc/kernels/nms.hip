@@ -481,7 +481,9 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
         dim3 g1((h * quads + DT - 1) / DT, parts, frames);
         hipLaunchKernelGGL(nms_detect_kernel, g1, dim3(DT), 0, stream, scratch, heat.heat,
                            heat.channels, parts, h, w, threshold, heat.cuda);
-    } else if (!cuda && heat.nsrc == 1) {
+    } else if (!cuda && heat.nsrc == 1 && dev_switch("NMS_STREAM", 1) != 0) {   // 0: dev A/B
+        // 62 x 62 walks, one wave (measured: 30-row walks, two-wave 126 / 46-row walks 4-10 %
+        // slower; loading the taps two advances ahead instead of one: no change)
         constexpr int lt = 64, rc = 62;
         hipLaunchKernelGGL((nms_detect_stream_kernel<lt, rc>),
                            dim3((w + lt - 3) / (lt - 2), (h + rc - 1) / rc, frames * parts),
