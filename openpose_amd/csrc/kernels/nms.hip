@@ -361,24 +361,25 @@ __global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ pe
     }
 }
 
-// Single-source lazy map, CPU semantics (the pose pipeline's default): one wave owns LT columns
-// (x0-1 .. x0+LT-2, LT-2 tested) of RC consecutive map rows and walks down them once.  The
-// horizontal passes of the source rows are kept as a rolling register window h0..h3 (source rows
+// Lazy map of NS sources (1..4), CPU semantics (the pose pipeline's maps): one wave owns LT
+// columns (x0-1 .. x0+LT-2, LT-2 tested) of RC consecutive map rows and walks down them once.
+// Per source, the horizontal passes are kept as a rolling register window h0..h3 (source rows
 // yofs[y]-1 .. yofs[y]+2, clamped) that advances one source row at a time, with the next source
-// row's four taps loaded one advance ahead; each map row is one vertical combination, written
-// into a 4-row LDS ring, and the row above it is tested once the ring holds its lower
-// neighbours.  Against the windowed kernel above, every source row's horizontal pass is computed
-// once per column instead of once per 16-row window it touches (2.5x at x8), and the row tables
-// are read from LDS.  Same hpass/vpass arithmetic and peak rules, so the candidate set is
-// identical (the finalize kernel orders it).
-template <int LT, int RC>
+// row's four taps loaded one advance ahead; each map row is one vertical combination per source
+// (summed in source order, then * 1/NS as resize_merge does), written into a 4-row LDS ring, and
+// the row above it is tested once the ring holds its lower neighbours.  Against the windowed
+// kernel above, every source row's horizontal pass is computed once per column instead of once
+// per 16-row window it touches (2.5x at x8), and the row tables are read from LDS.  Same
+// hpass/vpass arithmetic and peak rules, so the candidate set is identical (the finalize kernel
+// orders it).
+template <int LT, int RC, int NS>
 __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__ scratch,
                                                                const HeatMap M, int parts, float th)
 {
     static_assert(RC + 2 <= LT, "one lane per window row loads the row tables");
     __shared__ float ring[4 * LT];
-    __shared__ float4 rcoef[RC + 2];
-    __shared__ int rsrc[RC + 2];
+    __shared__ float4 rcoef[NS][RC + 2];
+    __shared__ int rsrc[NS][RC + 2];
     const int tid = threadIdx.x;
     const int c = blockIdx.z % parts, b = blockIdx.z / parts;
     const int plane = b * M.channels + c;
@@ -387,64 +388,83 @@ __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__
     const int x = xw0 + tid;
     const bool xin = x >= 0 && x < W;
     const bool simd_col = cubic_simd_column(x, W);
-    const ResizeSource& S = M.src[0];
-    const float* src = S.src + (size_t)plane * S.sh * S.sw;
+    const float inv_n = M.inv_n;
     const int ys = blockIdx.y * RC, ye = min(ys + RC, H);   // tested rows [ys, ye)
     const int wy0 = ys - 1;                                  // window row of table entry 0
-    if (tid < RC + 2) {
-        const int y = heat_clampi(wy0 + tid, 0, H - 1);
-        rcoef[tid] = *reinterpret_cast<const float4*>(S.ycoef + 4 * y);
-        rsrc[tid] = S.yofs[y];
+    // per source: locals only in the closures (one referring to the by-value kernel argument
+    // makes the compiler copy the HeatMap to scratch, see peak_at_heat)
+    const float* src[NS];
+    int ssh[NS], ssw[NS], t[NS][4];
+    float a[NS][4];
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+        const ResizeSource& S = M.src[n];
+        if (tid < RC + 2) {
+            const int y = heat_clampi(wy0 + tid, 0, H - 1);
+            rcoef[n][tid] = *reinterpret_cast<const float4*>(S.ycoef + 4 * y);
+            rsrc[n][tid] = S.yofs[y];
+        }
+        src[n] = S.src + (size_t)plane * S.sh * S.sw;
+        ssh[n] = S.sh;
+        ssw[n] = S.sw;
+        int xo = 0;
+        a[n][0] = a[n][1] = a[n][2] = a[n][3] = 0.f;
+        if (xin) {
+            xo = S.xofs[x];
+            const float4 cf = *reinterpret_cast<const float4*>(S.xcoef + 4 * x);
+            a[n][0] = cf.x; a[n][1] = cf.y; a[n][2] = cf.z; a[n][3] = cf.w;
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) t[n][k] = heat_clampi(xo - 1 + k, 0, ssw[n] - 1);
     }
-    int xo = 0;
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-    if (xin) {
-        xo = S.xofs[x];
-        const float4 cf = *reinterpret_cast<const float4*>(S.xcoef + 4 * x);
-        a[0] = cf.x; a[1] = cf.y; a[2] = cf.z; a[3] = cf.w;
-    }
-    // locals only in the closures: one referring to the by-value kernel argument makes the
-    // compiler copy the HeatMap to scratch (see peak_at_heat)
-    const int ssh = S.sh, ssw = S.sw;
-    const float a0 = a[0], a1 = a[1], a2 = a[2], a3 = a[3];
-    const int t0 = heat_clampi(xo - 1, 0, ssw - 1), t1 = heat_clampi(xo, 0, ssw - 1);
-    const int t2 = heat_clampi(xo + 1, 0, ssw - 1), t3 = heat_clampi(xo + 2, 0, ssw - 1);
-    auto taps = [src, ssh, ssw, t0, t1, t2, t3](int r, float v[4]) {   // source row r's taps
-        const float* row = src + (size_t)heat_clampi(r, 0, ssh - 1) * ssw;
-        v[0] = row[t0]; v[1] = row[t1]; v[2] = row[t2]; v[3] = row[t3];
+    auto taps = [&src, &ssh, &ssw, &t](int n, int r, float v[4]) {   // source row r's taps
+        const float* row = src[n] + (size_t)heat_clampi(r, 0, ssh[n] - 1) * ssw[n];
+        v[0] = row[t[n][0]]; v[1] = row[t[n][1]]; v[2] = row[t[n][2]]; v[3] = row[t[n][3]];
     };
     // cubic_hpass's sum, in its order
-    auto hsum = [a0, a1, a2, a3](const float v[4]) { return v[0] * a0 + v[1] * a1 + v[2] * a2 + v[3] * a3; };
+    auto hsum = [&a](int n, const float v[4]) {
+        return v[0] * a[n][0] + v[1] * a[n][1] + v[2] * a[n][2] + v[3] * a[n][3];
+    };
     __syncthreads();                                         // row tables
-    int cur = rsrc[wy0 < 0 ? 1 : 0];                         // source row of the first map row
-    float h0 = 0.f, h1 = 0.f, h2 = 0.f, h3 = 0.f, nv[4] = {0.f, 0.f, 0.f, 0.f};
-    if (xin) {
-        float v[4];
-        taps(cur - 1, v); h0 = hsum(v);
-        taps(cur, v); h1 = hsum(v);
-        taps(cur + 1, v); h2 = hsum(v);
-        taps(cur + 2, v); h3 = hsum(v);
-        taps(cur + 3, nv);                                   // next advance's row, in flight
+    int cur[NS];
+    float h[NS][4], nv[NS][4];
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+        cur[n] = rsrc[n][wy0 < 0 ? 1 : 0];                   // source row of the first map row
+#pragma unroll
+        for (int k = 0; k < 4; ++k) h[n][k] = nv[n][k] = 0.f;
+        if (xin) {
+            float v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                taps(n, cur[n] - 1 + k, v);
+                h[n][k] = hsum(n, v);
+            }
+            taps(n, cur[n] + 3, nv[n]);                      // next advance's row, in flight
+        }
     }
     int* pl = scratch + ((size_t)b * parts + c) * (CAP + 1);
     float vprev = th;
     for (int y = wy0; y <= ye; ++y) {
         float v = th;
         if (y >= 0 && y < H) {
-            const int t = rsrc[y - wy0];
-            while (cur < t) {                                // block-uniform
-                h0 = h1; h1 = h2; h2 = h3;
-                ++cur;
-                if (xin) {
-                    h3 = hsum(nv);
-                    taps(cur + 3, nv);
+            float acc = 0.f;
+#pragma unroll
+            for (int n = 0; n < NS; ++n) {
+                const int tr = rsrc[n][y - wy0];
+                while (cur[n] < tr) {                        // block-uniform
+                    h[n][0] = h[n][1]; h[n][1] = h[n][2]; h[n][2] = h[n][3];
+                    ++cur[n];
+                    if (xin) {
+                        h[n][3] = hsum(n, nv[n]);
+                        taps(n, cur[n] + 3, nv[n]);
+                    }
                 }
+                const float4 bq = rcoef[n][y - wy0];
+                const float vn = cubic_vpass(h[n], bq.x, bq.y, bq.z, bq.w, simd_col);
+                acc = (n == 0) ? vn : vn + acc;
             }
-            if (xin) {
-                const float4 bq = rcoef[y - wy0];
-                const float hv[4] = {h0, h1, h2, h3};
-                v = cubic_vpass(hv, bq.x, bq.y, bq.z, bq.w, simd_col);
-            }
+            if (xin) v = NS > 1 ? acc * inv_n : acc;
         }
         ring[(y & 3) * LT + tid] = v;                        // y >= -1: (y & 3) is y mod 4
         __syncthreads();                                     // rows y-2 .. y visible
@@ -481,13 +501,21 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
         dim3 g1((h * quads + DT - 1) / DT, parts, frames);
         hipLaunchKernelGGL(nms_detect_kernel, g1, dim3(DT), 0, stream, scratch, heat.heat,
                            heat.channels, parts, h, w, threshold, heat.cuda);
-    } else if (!cuda && heat.nsrc == 1 && dev_switch("NMS_STREAM", 1) != 0) {   // 0: dev A/B
+    } else if (!cuda && heat.nsrc <= 4 && dev_switch("NMS_STREAM", 1) != 0) {   // 0: dev A/B
         // 62 x 62 walks, one wave (measured: 30-row walks, two-wave 126 / 46-row walks 4-10 %
         // slower; loading the taps two advances ahead instead of one: no change)
         constexpr int lt = 64, rc = 62;
-        hipLaunchKernelGGL((nms_detect_stream_kernel<lt, rc>),
-                           dim3((w + lt - 3) / (lt - 2), (h + rc - 1) / rc, frames * parts),
-                           dim3(lt), 0, stream, scratch, heat, parts, threshold);
+        const dim3 grid((w + lt - 3) / (lt - 2), (h + rc - 1) / rc, frames * parts);
+#define OPK_NMS_STREAM(NS_)                                                                    \
+    hipLaunchKernelGGL((nms_detect_stream_kernel<lt, rc, NS_>), grid, dim3(lt), 0, stream,     \
+                       scratch, heat, parts, threshold)
+        switch (heat.nsrc) {
+        case 1: OPK_NMS_STREAM(1); break;
+        case 2: OPK_NMS_STREAM(2); break;
+        case 3: OPK_NMS_STREAM(3); break;
+        default: OPK_NMS_STREAM(4); break;
+        }
+#undef OPK_NMS_STREAM
     } else {
         constexpr int loy = 16;
         // one-wave workgroups (64 columns, 62 tested): no workgroup barrier holds four waves on
