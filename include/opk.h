@@ -300,6 +300,13 @@ int opk_pose_set_property(opk_pose* pose, int property, double value);
  * samples and opk_pose_heatmaps follow it.  Multi-scale with OPK_MAPS_CUDA needs the raw-frame
  * path (opk_pose_submit_frames), which knows scaleInputToNetInputs. */
 int opk_pose_set_map_semantics(opk_pose* pose, int semantics);
+/* --upsampling_ratio (include/openpose/flags.hpp:136; PoseExtractorCaffe's upsamplingRatio):
+ * heat maps of round((out_h * ratio - 1)) + 1 rows (likewise columns) of the scale-0 net output,
+ * resizeAndMergeCaffe.cpp:77-81, instead of the net input size; scaleNetToOutput then uses
+ * mNetOutputSize = round(ratio / 8 x net input size) (poseExtractorCaffe.cpp:281-310).  ratio <= 0
+ * (the default) = the net's decrease factor (8; 4 for BODY_19_X2).  CPU map semantics; the CUDA
+ * build's resize accepts x8 only for one source (resizeAndMergeBase.cu) and so does OPK_MAPS_CUDA. */
+int opk_pose_set_upsampling_ratio(opk_pose* pose, float ratio);
 /* frames: [n][3][net_h][net_w] device fp32; producer_w/h: original frame size (for
  * scaleNetToOutput, poseExtractorCaffe.cpp:306-310) */
 int opk_pose_forward(opk_pose* pose, const float* frames_dev, int n, int net_h, int net_w,

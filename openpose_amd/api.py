@@ -497,6 +497,11 @@ class PoseExtractor:
         CUDA build (opk_pose_set_map_semantics)."""
         check(self.L.opk_pose_set_map_semantics(self.h, semantics))
 
+    def set_upsampling_ratio(self, ratio):
+        """--upsampling_ratio (PoseExtractorCaffe's upsamplingRatio): heat maps at
+        round(out * ratio - 1) + 1 instead of the net input size; <= 0 restores the default."""
+        check(self.L.opk_pose_set_upsampling_ratio(self.h, float(ratio)))
+
     def set_overlay(self, overlay):
         self._overlay = overlay   # keep the tensor alive
         check(self.L.opk_pose_set_overlay(self.h, _ptr(overlay) if overlay is not None else None))

@@ -235,6 +235,14 @@ int opk_pose_collect(opk_pose* p, int* frames)
 
 int opk_pose_pending(opk_pose* p) { return p ? p->pose->pending() : -1; }
 
+int opk_pose_set_upsampling_ratio(opk_pose* p, float ratio)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->set_upsampling_ratio(ratio);
+    });
+}
+
 int opk_pose_set_overlay(opk_pose* p, const float* overlay)
 {
     return guarded_net([&] {

@@ -361,11 +361,21 @@ double NetHip::flops_per_frame(int h, int w) const
     return f;
 }
 
-NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
+NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stream)
 {
-    for (auto& sp : shapes_)
-        if (sp->n == n && sp->h == h && sp->w == w) return sp.get();
-    if ((int)shapes_.size() >= kMaxShapes) shapes_.erase(shapes_.begin());
+    // least recently used first: a lookup moves its plan to the back, so the plans of the scales
+    // of one multi-scale batch (<= kMaxShapes, prepared before it is submitted) stay resident
+    for (size_t i = 0; i < shapes_.size(); ++i)
+        if (shapes_[i]->n == n && shapes_[i]->h == h && shapes_[i]->w == w) {
+            std::unique_ptr<ShapePlan> sp = std::move(shapes_[i]);
+            shapes_.erase(shapes_.begin() + i);
+            shapes_.push_back(std::move(sp));
+            return shapes_.back().get();
+        }
+    if ((int)shapes_.size() >= kMaxShapes) {
+        if (cur_ == shapes_.front().get()) cur_ = nullptr;
+        shapes_.erase(shapes_.begin());
+    }
     shapes_.push_back(std::make_unique<ShapePlan>());
     ShapePlan& S = *shapes_.back();
     S.n = n;
@@ -404,7 +414,8 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w)
         const size_t bytes = pos * bufs_[i].cs * 2;
         OPK_CHECK_ARG(pos * bufs_[i].cs < (size_t)1 << 31, "activation buffer exceeds 2^31 elements");
         uint16_t* raw = static_cast<uint16_t*>(S.mem.back()->get(bytes));
-        OPK_HIP(hipMemsetAsync(raw, 0, bytes, ctx_->stream));
+        // zeroed on the stream whose kernels read the plan first
+        OPK_HIP(hipMemsetAsync(raw, 0, bytes, zero_stream ? zero_stream : ctx_->stream));
         ptr[i] = raw + head * bufs_[i].cs;
     }
     const size_t out_bytes = (size_t)n * out_c_ * lh_[out_level_] * lw_[out_level_] * 4;
@@ -471,7 +482,7 @@ void NetHip::prepare(int n, int h, int w)
 {
     OPK_CHECK_ARG(n > 0 && h > 0 && w > 0, "empty input");
     ctx_->bind();
-    (void)shape_plan(n, h, w);
+    (void)shape_plan(n, h, w, ctx_->stream);
 }
 
 void NetHip::forward_on(const float* input, int n, int h, int w, hipStream_t st, bool timed)
@@ -479,7 +490,7 @@ void NetHip::forward_on(const float* input, int n, int h, int w, hipStream_t st,
     OPK_CHECK_ARG(input && n > 0 && h > 0 && w > 0, "empty input");
     OPK_CHECK_ARG(ready(), "weights not loaded for every convolution");
     ctx_->bind();
-    ShapePlan& S = *shape_plan(n, h, w);
+    ShapePlan& S = *shape_plan(n, h, w, st);
     cur_ = &S;
     if (timed) timer_.begin(st);
     forward_launches(S, input, n, h, w, st);

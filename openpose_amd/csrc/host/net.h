@@ -92,7 +92,7 @@ private:
 
     void plan(const std::vector<LayerDesc>& layers);
     void forward_launches(ShapePlan& S, const float* input, int n, int h, int w, hipStream_t st);
-    ShapePlan* shape_plan(int n, int h, int w);
+    ShapePlan* shape_plan(int n, int h, int w, hipStream_t zero_stream = nullptr);
 
     Context* ctx_;
     std::string output_blob_;

@@ -68,6 +68,15 @@ PoseHip::~PoseHip()
     if (fork_) (void)hipEventDestroy(fork_);
 }
 
+void PoseHip::set_upsampling_ratio(float ratio)
+{
+    OPK_CHECK_ARG(std::isfinite(ratio), "upsampling ratio must be finite");
+    upsampling_ = ratio;
+}
+
+// getPoseNetDecreaseFactor (poseParameters.cpp:630-641)
+static float net_decrease_factor(int model) { return model == 5 /* BODY_19_X2 */ ? 4.f : 8.f; }
+
 void PoseHip::set_map_semantics(int maps)
 {
     OPK_CHECK_ARG(maps == kMapsCpu || maps == kMapsCuda, "unknown heat-map semantics");
@@ -329,11 +338,17 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
         launch_add_inplace(const_cast<float*>(outs[0].ptr), overlay_, out_elems, s);
     }
 
-    // 1. resize x8 of the first scale's size (ResizeAndMergeCaffe::Reshape: (h*8 - 1)*1 + 1) and
-    //    average of the scales (resizeAndMergeBase.cpp:55-106), evaluated lazily: NMS and the PAF
-    //    scorer compute the merged values they touch with resize.hip's arithmetic (bit-identical),
-    //    so the 75 MB/frame heat-map stack is only written if requested
-    const int H = outs[0].h * 8, W = outs[0].w * 8;
+    // 1. resize of the first scale's size (ResizeAndMergeCaffe::Reshape, resizeAndMergeCaffe.cpp:
+    //    77-81: round((h * netFactor - 1) * 1) + 1, netFactor = --upsampling_ratio or the net's
+    //    decrease factor, reshapePoseExtractorCaffe poseExtractorCaffe.cpp:47-54) and average of the
+    //    scales (resizeAndMergeBase.cpp:55-106), evaluated lazily: NMS and the PAF scorer compute
+    //    the merged values they touch with resize.hip's arithmetic (bit-identical), so the
+    //    75 MB/frame heat-map stack is only written if requested
+    const float dec = net_decrease_factor(model_);
+    const float nf = upsampling_ > 0.f ? upsampling_ : dec;
+    const int H = (int)std::round(((float)outs[0].h * nf - 1.f) * 1.f) + 1;
+    const int W = (int)std::round(((float)outs[0].w * nf - 1.f) * 1.f) + 1;
+    OPK_CHECK_ARG(H >= 1 && W >= 1, "upsampling ratio gives an empty heat map");
     HeatMap heat{};
     if (maps_ == kMapsCuda) {   // resizeAndMergeGpu's arithmetic (maps.h)
         OPK_CHECK_ARG(nscales == 1 || have_ratios_,
@@ -359,8 +374,11 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
         }
     }
 
-    // 2. scale net -> output (poseExtractorCaffe.cpp:281-310), net output size == net input size
-    const double sp = resize_scale_factor(prod_w, prod_h, net_w, net_h);
+    // 2. scale net -> output (poseExtractorCaffe.cpp:281-310): mNetOutputSize = the net input
+    //    size x (ratio / decrease factor), ratio 1 without --upsampling_ratio
+    const float ratio = upsampling_ <= 0.f ? 1.f : upsampling_ / dec;
+    const int out_w = (int)(ratio * (float)net_w + 0.5f), out_h = (int)(ratio * (float)net_h + 0.5f);
+    const double sp = resize_scale_factor(prod_w, prod_h, out_w, out_h);
     const int nw = (int)(sp * prod_w + 0.5f), nh = (int)(sp * prod_h + 0.5f);
     const float scale = (float)resize_scale_factor(nw, nh, prod_w, prod_h);
 

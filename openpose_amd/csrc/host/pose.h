@@ -28,6 +28,10 @@ public:
     int map_semantics() const { return maps_; }
     double property(int prop) const { return props_[prop]; }
     void set_overlay(const float* overlay) { overlay_ = overlay; }
+    // --upsampling_ratio (flags.hpp:136): heat maps at round(ratio x net output) instead of the net
+    // input size; <= 0 is the default (the net's decrease factor, poseExtractorCaffe.cpp:47-54)
+    void set_upsampling_ratio(float ratio);
+    float upsampling_ratio() const { return upsampling_; }
 
     void forward(const float* frames, int n, int net_h, int net_w, int prod_w, int prod_h);
     void forward_net_output(const float* net_out, int n, int out_h, int out_w, int net_h,
@@ -111,6 +115,7 @@ private:
     bool have_ratios_ = false;
     double props_[5];
     const float* overlay_ = nullptr;
+    float upsampling_ = 0.f;
     hipStream_t copy_ = nullptr;         // D2H of collected batches (overlaps the next batch)
     // multi-scale: the nets of scales 1.. run on their own streams beside scale 0's
     hipStream_t scale_streams_[kMaxResizeSources - 1] = {};

@@ -286,28 +286,32 @@ def test_pose_injection_gpu_semantics(ctx, model, people):
         np.testing.assert_array_equal(ks, rs)
 
 
-def test_multiscale_config4_bitexact(ctx):
-    """SURVEY.md §8 config 4: four scales (nets 656x368, 480x272, 320x176, 160x80) through
-    opk_pose_forward_multi: the merged heat maps (resizeAndMergeCpu average of the x8 cubic
-    resizes), peaks and people are bit-identical to the oracle chain fed with the same per-scale
-    net outputs."""
-    sizes = [(368, 656), (272, 480), (176, 320), (80, 160)]
+def _multiscale_case(ctx, nscales, gap, seed, nms_stream=1):
+    """--scale_number nscales --scale_gap gap through opk_pose_forward_multi, sizes from
+    ScaleAndSizeExtractor (scaleAndSizeExtractor.cpp:74-88); merged heat maps (resizeAndMergeCpu
+    average, resizeAndMergeBase.cpp:55-106), peaks and people bit-identical to the oracle chain fed
+    with the same per-scale net outputs.  nms_stream=0: the windowed lazy NMS instead of the
+    streaming walk (dev switch; the same candidates)."""
+    from openpose_amd.api import dev_switches, scale_and_size
+    _, net_sizes = scale_and_size((1280, 720), (-1, 368), 1.0, nscales, gap)
+    sizes = [(h, w) for (w, h) in net_sizes]
     graph = body25.layers()
-    params = synth.he_weights(graph, seed=21, out_scale=0.02)
+    params = synth.he_weights(graph, seed=seed, out_scale=0.02)
     net = Net(ctx, "builtin:BODY_25")
     net.set_params(params)
-    rng = np.random.default_rng(22)
+    rng = np.random.default_rng(seed + 1)
     xs = [rng.uniform(-0.5, 0.5, (2, 3, h, w)).astype(np.float32) for h, w in sizes]
     outs = []
     for x in xs:
         net.forward(_dev(x))
         outs.append(net.output_numpy())
-    assert [o.shape[2:] for o in outs] == [(46, 82), (34, 60), (22, 40), (10, 20)]
+    assert [o.shape[2:] for o in outs] == [(h // 8, w // 8) for h, w in sizes]
     ov = np.stack([synth.overlay(4, 46, 82, seed=2300 + k) for k in range(2)]).astype(np.float32)
     pose = PoseExtractor(ctx, net)
     ovd = _dev(ov)
     pose.set_overlay(ovd)
-    pose.forward_multi([_dev(x) for x in xs], (1280, 720))
+    with dev_switches(NMS_STREAM=nms_stream):
+        pose.forward_multi([_dev(x) for x in xs], (1280, 720))
     s = pose.scale_net_to_output()
     assert abs(s - 1.959128) < 1e-5
     off = float(np.float32(0.5 / np.float64(s)))
@@ -323,3 +327,69 @@ def test_multiscale_config4_bitexact(ctx):
         assert len(kp) >= 1
         np.testing.assert_array_equal(kp, rk)
         np.testing.assert_array_equal(ks, rs)
+
+
+def test_multiscale_config4_bitexact(ctx):
+    """SURVEY.md §8 config 4: four scales (nets 656x368, 480x272, 320x176, 160x80) through
+    opk_pose_forward_multi, bit-identical to the oracle chain (the 4-source streaming NMS walk)."""
+    from openpose_amd.api import scale_and_size
+    assert scale_and_size((1280, 720), (-1, 368), 1.0, 4, 0.25)[1] == \
+        [(656, 368), (480, 272), (320, 176), (160, 80)]
+    _multiscale_case(ctx, 4, 0.25, 21)
+
+
+@pytest.mark.parametrize("nscales,gap,nms_stream", [(2, 0.25, 1), (3, 0.25, 1), (6, 0.15, 1),
+                                                    (2, 0.25, 0), (3, 0.3, 0), (4, 0.25, 0)])
+def test_multiscale_other_scale_numbers_bitexact(ctx, nscales, gap, nms_stream):
+    """--scale_number 2 / 3 (the 2- and 3-source streaming NMS walks) and 6 (more than 4 sources:
+    the windowed lazy NMS), and the windowed kernel for 2-4 sources (NMS_STREAM=0)."""
+    _multiscale_case(ctx, nscales, gap, 40 + nscales, nms_stream)
+
+
+def _resize_get_scale_factor(init, target):
+    """resizeGetScaleFactor (src/openpose/utilities/openCv.cpp:182-195)"""
+    return min((target[0] - 1) / float(init[0] - 1), (target[1] - 1) / float(init[1] - 1))
+
+
+@pytest.mark.parametrize("ratio", [4.0, 2.5, 16.0, 1.0])
+def test_upsampling_ratio_bitexact(ctx, ratio):
+    """--upsampling_ratio (flags.hpp:136): the heat maps are round(h * r - 1) + 1 rows of the
+    46 x 82 net output (ResizeAndMergeCaffe::Reshape, resizeAndMergeCaffe.cpp:77-81, with
+    reshapePoseExtractorCaffe's netFactor = r, poseExtractorCaffe.cpp:47-54), NMS and the connector
+    run at that size, and scaleNetToOutput comes from mNetOutputSize = round(r / 8 x net input)
+    (poseExtractorCaffe.cpp:281-310).  Bit-identical to the oracle chain at that size."""
+    rng = np.random.default_rng(77)
+    fields = np.stack([synth.overlay(5, 46, 82, seed=7700 + k) +
+                       rng.normal(0, 0.01, (78, 46, 82)) for k in range(2)]).astype(np.float32)
+    pose = PoseExtractor(ctx, None)
+    pose.set_upsampling_ratio(ratio)
+    pose.forward_net_output(_dev(fields), (656, 368), (1280, 720))
+    f32 = np.float32
+    H = int(np.round(f32(46) * f32(ratio) - f32(1))) + 1
+    W = int(np.round(f32(82) * f32(ratio) - f32(1))) + 1
+    r = f32(ratio) / f32(8)
+    out = (int(r * f32(656) + f32(0.5)), int(r * f32(368) + f32(0.5)))
+    sp = _resize_get_scale_factor((1280, 720), out)
+    net = (int(sp * 1280 + 0.5), int(sp * 720 + 0.5))
+    s = f32(_resize_get_scale_factor(net, (1280, 720)))
+    assert pose.scale_net_to_output() == s
+    off = float(np.float32(0.5 / np.float64(s)))
+    gpu_heat = pose.heatmaps_numpy()
+    assert gpu_heat.shape == (2, 78, H, W)
+    gpu_peaks = pose.peaks_numpy()
+    for k in range(2):
+        heat = oracle.resize_merge([fields[k]], H, W)
+        np.testing.assert_array_equal(gpu_heat[k], heat)
+        peaks = oracle.nms(heat, 0.05, 128, (off, off))
+        np.testing.assert_array_equal(gpu_peaks[k], peaks)
+        rk, rs = oracle.connect(heat, peaks, scale=float(s))
+        kp, ks = pose.keypoints(k)
+        assert len(kp) >= 1 or ratio < 2
+        np.testing.assert_array_equal(kp, rk)
+        np.testing.assert_array_equal(ks, rs)
+    # the CUDA build's resize accepts x8 only for one source (resizeAndMergeBase.cu:276-300)
+    if ratio not in (1.0, 8.0):
+        from openpose_amd._lib import OpkError
+        pose.set_map_semantics(1)
+        with pytest.raises(OpkError, match="8x resize"):
+            pose.forward_net_output(_dev(fields), (656, 368), (1280, 720))

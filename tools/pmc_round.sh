@@ -1,0 +1,16 @@
+#!/bin/bash
+# PMC passes over a short bench.py run (one rocprofv3 pass per counter set, each under its own
+# time limit), then tools/pmc_report.py turns them into per-kernel-group summaries:
+#   pmc_round.sh OUTDIR [bench args...]
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+out=gpurun_out/$1; shift
+mkdir -p $out
+B="python bench.py --steps 3 --warmup 1 --no-cpu-baseline $*"
+i=0
+for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_INSTS_VALU GRBM_GUI_ACTIVE GRBM_COUNT" \
+           "SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAVES" \
+           "FETCH_SIZE" "WRITE_SIZE"; do
+  i=$((i+1))
+  timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $out/p$i -o run -- $B > $out/p$i.log 2>&1 || exit 1
+done
+python tools/pmc_report.py $out/p1 $out/p2 $out/p3 $out/p4 --json $out/report.json > $out/report.txt 2>&1
