@@ -48,7 +48,7 @@ namespace op
             ~SyncedHip()
             {
                 if (mOwnGpu && mGpu)
-                    opk_free(mCtx, mGpu);
+                    opk_free(mCtx.get(), mGpu);
             }
             SyncedHip(const SyncedHip&) = delete;
             SyncedHip& operator=(const SyncedHip&) = delete;
@@ -70,7 +70,7 @@ namespace op
                 if (data == nullptr)
                     error("set_gpu_data: NULL pointer.", __LINE__, __FUNCTION__, __FILE__);
                 if (mOwnGpu && mGpu)
-                    opk_free(mCtx, mGpu);
+                    opk_free(mCtx.get(), mGpu);
                 mCtx = opkShimThreadContext();
                 mGpu = data;
                 mOwnGpu = false;
@@ -90,7 +90,7 @@ namespace op
                 if (mGpu)
                     return;
                 mCtx = opkShimThreadContext();
-                checkOpk(opk_malloc(mCtx, &mGpu, std::max<size_t>(mBytes, 1)), __LINE__, __FUNCTION__);
+                checkOpk(opk_malloc(mCtx.get(), &mGpu, std::max<size_t>(mBytes, 1)), __LINE__, __FUNCTION__);
                 mOwnGpu = true;
             }
             void toCpu()
@@ -105,7 +105,7 @@ namespace op
                     case HEAD_AT_GPU:
                         allocCpu();
                         if (mBytes)
-                            checkOpk(opk_memcpy_d2h(mCtx, cpuPtr(), mGpu, mBytes), __LINE__, __FUNCTION__);
+                            checkOpk(opk_memcpy_d2h(mCtx.get(), cpuPtr(), mGpu, mBytes), __LINE__, __FUNCTION__);
                         mHead = SYNCED;
                         break;
                     default:
@@ -118,13 +118,13 @@ namespace op
                 {
                     case UNINITIALIZED:
                         allocGpu();
-                        checkOpk(opk_memset(mCtx, mGpu, 0, mBytes), __LINE__, __FUNCTION__);
+                        checkOpk(opk_memset(mCtx.get(), mGpu, 0, mBytes), __LINE__, __FUNCTION__);
                         mHead = HEAD_AT_GPU;
                         break;
                     case HEAD_AT_CPU:
                         allocGpu();
                         if (mBytes)
-                            checkOpk(opk_memcpy_h2d(mCtx, mGpu, cpuPtr(), mBytes), __LINE__, __FUNCTION__);
+                            checkOpk(opk_memcpy_h2d(mCtx.get(), mGpu, cpuPtr(), mBytes), __LINE__, __FUNCTION__);
                         mHead = SYNCED;
                         break;
                     default:
@@ -136,7 +136,7 @@ namespace op
             Head mHead = UNINITIALIZED;
             std::vector<unsigned char> mOwnCpu;
             void* mCpu = nullptr;   // external host buffer (set_cpu_data), else mOwnCpu
-            opk_ctx* mCtx = nullptr;
+            OpkContext mCtx;   // the context of the device buffer (kept alive by this)
             void* mGpu = nullptr;
             bool mOwnGpu = false;
         };

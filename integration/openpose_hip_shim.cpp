@@ -24,6 +24,7 @@
 // -DOPK_SHIM_MAPS=OPK_MAPS_CPU, which gives the CPU path's numerics (resizeAndMergeCpu / nmsCpu);
 // everything else follows the CPU path.  Errors come back through op::error, the
 // reference's convention (errorAndLog.cpp:158-233).  See INTEGRATION.md for the build lines.
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -51,31 +52,42 @@
 
 namespace op
 {
-    namespace
+    // one context per calling thread = per GPU worker thread (wrapperAuxiliary.hpp:1050-1067);
+    // the reference runs everything on the legacy default stream, so does this context.  Shared
+    // ownership: see opk_shim.hpp.
+    OpkContext opkShimThreadContext(const int device)
     {
-        // one context per calling thread = per GPU worker thread (wrapperAuxiliary.hpp:1050-1067);
-        // the reference runs everything on the legacy default stream, so does this context.
-        opk_ctx* threadContext(const int device = -2)
+        thread_local OpkContext ctx;
+        thread_local int bound = -1;
+        const int want = device >= 0 ? device : (bound >= 0 ? bound : 0);
+        if (!ctx || want != bound)
         {
-            thread_local std::unique_ptr<opk_ctx, int (*)(opk_ctx*)> ctx{nullptr, opk_ctx_destroy};
-            thread_local int bound = -1;
-            const int want = device >= 0 ? device : (bound >= 0 ? bound : 0);
-            if (!ctx || want != bound)
-            {
-                opk_ctx* raw = nullptr;
-                if (opk_ctx_create(want, nullptr, &raw) != OPK_OK)
-                    error(opk_last_error(), __LINE__, __FUNCTION__, __FILE__);
-                ctx.reset(raw);
-                bound = want;
-            }
-            return ctx.get();
+            opk_ctx* raw = nullptr;
+            if (opk_ctx_create(want, nullptr, &raw) != OPK_OK)
+                error(opk_last_error(), __LINE__, __FUNCTION__, __FILE__);
+            ctx = OpkContext{raw, opk_ctx_destroy};
+            bound = want;
         }
-
+        return ctx;
     }
 
-    opk_ctx* opkShimThreadContext()
+    namespace
     {
-        return threadContext();
+        opk_ctx* threadContext() { return opkShimThreadContext().get(); }
+
+        // CvMatToOpInput's device buffers are members of the reference's own class
+        // (cvMatToOpInput.hpp), so the context they were allocated on is kept beside it
+        std::mutex gInputCtxMutex;
+        std::map<const void*, OpkContext> gInputCtx;
+
+        OpkContext inputContext(const void* owner)
+        {
+            std::lock_guard<std::mutex> lock{gInputCtxMutex};
+            auto& c = gInputCtx[owner];
+            if (!c)
+                c = opkShimThreadContext();
+            return c;
+        }
     }
 
     namespace
@@ -239,15 +251,15 @@ namespace op
         virtual ~NetHip()
         {
             if (mInput)
-                opk_free(mCtx, mInput);
+                opk_free(mCtx.get(), mInput);
             if (mNet)
                 opk_net_destroy(mNet);
-        }
+        }   // the context itself goes when its last holder does
 
         void initializationOnThread()
         {
-            mCtx = threadContext(mGpuId);   // binds this thread to the GPU (netCaffe.cpp:169-170)
-            check(opk_net_create(mCtx, mProto.c_str(), mModel.c_str(), &mNet), __LINE__, __FUNCTION__);
+            mCtx = opkShimThreadContext(mGpuId);   // binds this thread to the GPU (netCaffe.cpp:169-170)
+            check(opk_net_create(mCtx.get(), mProto.c_str(), mModel.c_str(), &mNet), __LINE__, __FUNCTION__);
         }
 
         void forwardPass(const Array<float>& inputNetData) const
@@ -259,11 +271,12 @@ namespace op
             if (bytes > mInputBytes)
             {
                 if (mInput)
-                    opk_free(mCtx, mInput);
-                check(opk_malloc(mCtx, &mInput, bytes), __LINE__, __FUNCTION__);
+                    opk_free(mCtx.get(), mInput);
+                mInput = nullptr;
+                check(opk_malloc(mCtx.get(), &mInput, bytes), __LINE__, __FUNCTION__);
                 mInputBytes = bytes;
             }
-            check(opk_memcpy_h2d(mCtx, mInput, inputNetData.getConstPtr(), bytes), __LINE__, __FUNCTION__);
+            check(opk_memcpy_h2d(mCtx.get(), mInput, inputNetData.getConstPtr(), bytes), __LINE__, __FUNCTION__);
             check(opk_net_forward(mNet, (const float*)mInput, size[0], size[2], size[3]), __LINE__,
                   __FUNCTION__);
             if (spOutput)
@@ -303,7 +316,7 @@ namespace op
 
         const std::string mProto, mModel;
         const int mGpuId;
-        opk_ctx* mCtx = nullptr;
+        OpkContext mCtx;
         opk_net* mNet = nullptr;
         mutable void* mInput = nullptr;
         mutable size_t mInputBytes = 0;
@@ -323,7 +336,9 @@ namespace op
         std::string proto, model;
         bool enableNet, maximizePositives;
         int parts = 0, heatChannels = 0;
-        opk_ctx* ctx = nullptr;
+        float upsamplingRatio = 0.f;
+        OpkContext ctxOwner;
+        opk_ctx* ctx = nullptr;             // ctxOwner.get()
         opk_net* net = nullptr;
         opk_pose* pose = nullptr;
         std::vector<void*> inputs;          // device net inputs, one per scale
@@ -404,7 +419,8 @@ namespace op
         try
         {
             auto& impl = *upImpl;
-            impl.ctx = threadContext(impl.gpuId);   // binds this thread to the GPU (netCaffe.cpp:169-170)
+            impl.ctxOwner = opkShimThreadContext(impl.gpuId);   // binds this thread to the GPU (netCaffe.cpp:169-170)
+            impl.ctx = impl.ctxOwner.get();
             if (impl.enableNet)
                 check(opk_net_create(impl.ctx, impl.proto.c_str(), impl.model.c_str(), &impl.net), __LINE__,
                       __FUNCTION__);
@@ -651,11 +667,23 @@ namespace op
 
     CvMatToOpInput::~CvMatToOpInput()
     {
-        opk_ctx* ctx = threadContext();
-        if (pInputImageCuda)
-            opk_free(ctx, pInputImageCuda);
-        if (pOutputImageCuda)
-            opk_free(ctx, pOutputImageCuda);
+        OpkContext owner;
+        {
+            std::lock_guard<std::mutex> lock{gInputCtxMutex};
+            auto it = gInputCtx.find(this);
+            if (it != gInputCtx.end())
+            {
+                owner = it->second;
+                gInputCtx.erase(it);
+            }
+        }
+        if (owner)   // the buffers belong to the context they were allocated on
+        {
+            if (pInputImageCuda)
+                opk_free(owner.get(), pInputImageCuda);
+            if (pOutputImageCuda)
+                opk_free(owner.get(), pOutputImageCuda);
+        }
     }
 
     std::vector<Array<float>> CvMatToOpInput::createArray(
@@ -669,7 +697,8 @@ namespace op
             error("Input images must be 3-channel BGR.", __LINE__, __FUNCTION__, __FILE__);
         if (scaleInputToNetInputs.size() != netInputSizes.size())
             error("scaleInputToNetInputs.size() != netInputSizes.size().", __LINE__, __FUNCTION__, __FILE__);
-        opk_ctx* ctx = threadContext();
+        const OpkContext owner = inputContext(this);   // the context of the first call, for good
+        opk_ctx* ctx = owner.get();
         const size_t step = inputData.step1(0);   // bytes per row (uchar)
         const unsigned long long frameBytes = (unsigned long long)step * inputData.rows();
         if (pInputMaxSize < frameBytes)
@@ -715,7 +744,8 @@ namespace op
         {
             std::string proto, model;
             int gpuId = 0;
-            opk_ctx* ctx = nullptr;
+            OpkContext ctxOwner;
+            opk_ctx* ctx = nullptr;   // ctxOwner.get()
             opk_net* net = nullptr;
             opk_extractor* ex = nullptr;
             void* frame = nullptr;
@@ -735,7 +765,8 @@ namespace op
 
             void initialize(const int kind, const Point<int>& netSize)
             {
-                ctx = threadContext(gpuId);
+                ctxOwner = opkShimThreadContext(gpuId);
+                ctx = ctxOwner.get();
                 check(opk_net_create(ctx, proto.c_str(), model.c_str(), &net), __LINE__, __FUNCTION__);
                 check(opk_extractor_create(ctx, net, kind, netSize.x, netSize.y, &ex), __LINE__,
                       __FUNCTION__);

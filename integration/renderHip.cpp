@@ -31,7 +31,7 @@ namespace op
         {
             if (rc != OPK_OK)
                 error(std::string{"libopk_hip: "} + opk_last_error(), line, function, __FILE__);
-            if (opk_sync(opkShimThreadContext()) != OPK_OK)
+            if (opk_sync(opkShimThreadContext().get()) != OPK_OK)
                 error(std::string{"libopk_hip: "} + opk_last_error(), line, function, __FILE__);
         }
     }
@@ -45,7 +45,7 @@ namespace op
         (void)maxPtr;
         (void)minPtr;
         (void)scalePtr;
-        run(opk_render_pose_keypoints(opkShimThreadContext(), framePtr, (int)poseModel, numberPeople,
+        run(opk_render_pose_keypoints(opkShimThreadContext().get(), framePtr, (int)poseModel, numberPeople,
                                       frameSize.x, frameSize.y, posePtr, renderThreshold,
                                       googlyEyes ? 1 : 0, blendOriginalFrame ? 1 : 0, alphaBlending),
             __LINE__, __FUNCTION__);
@@ -56,7 +56,7 @@ namespace op
         const Point<int>& heatMapSize, const float scaleToKeepRatio, const unsigned int part,
         const float alphaBlending)
     {
-        run(opk_render_pose_heat_map(opkShimThreadContext(), frame, frameSize.x, frameSize.y,
+        run(opk_render_pose_heat_map(opkShimThreadContext().get(), frame, frameSize.x, frameSize.y,
                                      heatMapPtr, heatMapSize.x, heatMapSize.y, scaleToKeepRatio,
                                      part, alphaBlending),
             __LINE__, __FUNCTION__);
@@ -67,7 +67,7 @@ namespace op
         const float* const heatMapPtr, const Point<int>& heatMapSize, const float scaleToKeepRatio,
         const float alphaBlending)
     {
-        run(opk_render_pose_heat_maps(opkShimThreadContext(), frame, (int)poseModel, frameSize.x,
+        run(opk_render_pose_heat_maps(opkShimThreadContext().get(), frame, (int)poseModel, frameSize.x,
                                       frameSize.y, heatMapPtr, heatMapSize.x, heatMapSize.y,
                                       scaleToKeepRatio, alphaBlending),
             __LINE__, __FUNCTION__);
@@ -78,7 +78,7 @@ namespace op
         const float* const heatMapPtr, const Point<int>& heatMapSize, const float scaleToKeepRatio,
         const int part, const float alphaBlending)
     {
-        run(opk_render_pose_paf(opkShimThreadContext(), framePtr, (int)poseModel, frameSize.x,
+        run(opk_render_pose_paf(opkShimThreadContext().get(), framePtr, (int)poseModel, frameSize.x,
                                 frameSize.y, heatMapPtr, heatMapSize.x, heatMapSize.y,
                                 scaleToKeepRatio, part, alphaBlending),
             __LINE__, __FUNCTION__);
@@ -89,7 +89,7 @@ namespace op
         const float* const heatMapPtr, const Point<int>& heatMapSize, const float scaleToKeepRatio,
         const float alphaBlending)
     {
-        run(opk_render_pose_pafs(opkShimThreadContext(), framePtr, (int)poseModel, frameSize.x,
+        run(opk_render_pose_pafs(opkShimThreadContext().get(), framePtr, (int)poseModel, frameSize.x,
                                  frameSize.y, heatMapPtr, heatMapSize.x, heatMapSize.y,
                                  scaleToKeepRatio, alphaBlending),
             __LINE__, __FUNCTION__);
@@ -100,7 +100,7 @@ namespace op
         const Point<int>& heatMapSize, const float scaleToKeepRatio, const unsigned int part,
         const float alphaBlending)
     {
-        run(opk_render_pose_distance(opkShimThreadContext(), framePtr, frameSize.x, frameSize.y,
+        run(opk_render_pose_distance(opkShimThreadContext().get(), framePtr, frameSize.x, frameSize.y,
                                      heatMapPtr, heatMapSize.x, heatMapSize.y, scaleToKeepRatio,
                                      part, alphaBlending),
             __LINE__, __FUNCTION__);
@@ -114,7 +114,7 @@ namespace op
         (void)maxPtr;
         (void)minPtr;
         (void)scalePtr;
-        run(opk_render_face_keypoints(opkShimThreadContext(), framePtr, frameSize.x, frameSize.y,
+        run(opk_render_face_keypoints(opkShimThreadContext().get(), framePtr, frameSize.x, frameSize.y,
                                       facePtr, numberPeople, renderThreshold, alphaColorToAdd),
             __LINE__, __FUNCTION__);
     }
@@ -127,7 +127,7 @@ namespace op
         (void)maxPtr;
         (void)minPtr;
         (void)scalePtr;
-        run(opk_render_hand_keypoints(opkShimThreadContext(), framePtr, frameSize.x, frameSize.y,
+        run(opk_render_hand_keypoints(opkShimThreadContext().get(), framePtr, frameSize.x, frameSize.y,
                                       handsPtr, numberHands, renderThreshold, alphaColorToAdd),
             __LINE__, __FUNCTION__);
     }

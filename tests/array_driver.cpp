@@ -26,11 +26,15 @@ namespace op
         throw std::runtime_error(message + " (" + file + ":" + std::to_string(line) + " " + function + ")");
     }
 
-    opk_ctx* opkShimThreadContext()
+    OpkContext opkShimThreadContext(const int)
     {
-        static opk_ctx* ctx = nullptr;
-        if (!ctx && opk_ctx_create(0, nullptr, &ctx) != OPK_OK)
-            throw std::runtime_error(opk_last_error());
+        static OpkContext ctx;
+        if (!ctx) {
+            opk_ctx* raw = nullptr;
+            if (opk_ctx_create(0, nullptr, &raw) != OPK_OK)
+                throw std::runtime_error(opk_last_error());
+            ctx = OpkContext{raw, opk_ctx_destroy};
+        }
         return ctx;
     }
 }
@@ -88,7 +92,7 @@ static int cpu_checks()
 
 static int gpu_checks()
 {
-    opk_ctx* ctx = op::opkShimThreadContext();
+    opk_ctx* ctx = op::opkShimThreadContext().get();
     op::ArrayCpuGpu<float> a(1, 2, 3, 4);
     float* h = a.mutable_cpu_data();
     for (int i = 0; i < 24; ++i) h[i] = (float)i;

@@ -26,11 +26,15 @@ namespace op
         throw std::runtime_error(message + " (" + file + ":" + std::to_string(line) + " " + function + ")");
     }
 
-    opk_ctx* opkShimThreadContext()
+    OpkContext opkShimThreadContext(const int)
     {
-        static opk_ctx* ctx = nullptr;
-        if (!ctx && opk_ctx_create(0, nullptr, &ctx) != OPK_OK)
-            throw std::runtime_error(opk_last_error());
+        static OpkContext ctx;
+        if (!ctx) {
+            opk_ctx* raw = nullptr;
+            if (opk_ctx_create(0, nullptr, &raw) != OPK_OK)
+                throw std::runtime_error(opk_last_error());
+            ctx = OpkContext{raw, opk_ctx_destroy};
+        }
         return ctx;
     }
 }
@@ -59,8 +63,8 @@ namespace
     void* upload(const void* host, size_t bytes)
     {
         void* dev = nullptr;
-        if (opk_malloc(op::opkShimThreadContext(), &dev, bytes ? bytes : 4) != OPK_OK ||
-            opk_memcpy_h2d(op::opkShimThreadContext(), dev, host, bytes) != OPK_OK)
+        if (opk_malloc(op::opkShimThreadContext().get(), &dev, bytes ? bytes : 4) != OPK_OK ||
+            opk_memcpy_h2d(op::opkShimThreadContext().get(), dev, host, bytes) != OPK_OK)
             throw std::runtime_error(opk_last_error());
         return dev;
     }
@@ -78,7 +82,7 @@ int main(int argc, char** argv)
         const auto pose = load<float>(dir + "/pose.f32", (size_t)people * 25 * 3);
         const auto heat = load<float>(dir + "/heat.f32", (size_t)78 * hw * hh);
         const auto face = load<float>(dir + "/face.f32", (size_t)faces * 70 * 3);
-        opk_ctx* ctx = op::opkShimThreadContext();
+        opk_ctx* ctx = op::opkShimThreadContext().get();
         float* dframe = static_cast<float*>(upload(frame.data(), fn * 4));
         const float* dpose = static_cast<const float*>(upload(pose.data(), pose.size() * 4));
         const float* dheat = static_cast<const float*>(upload(heat.data(), heat.size() * 4));

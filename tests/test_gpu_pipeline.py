@@ -306,7 +306,9 @@ def _multiscale_case(ctx, nscales, gap, seed, nms_stream=1):
         net.forward(_dev(x))
         outs.append(net.output_numpy())
     assert [o.shape[2:] for o in outs] == [(h // 8, w // 8) for h, w in sizes]
+    # the overlay rides on scale 0 only: scaled so that the average over the scales keeps people
     ov = np.stack([synth.overlay(4, 46, 82, seed=2300 + k) for k in range(2)]).astype(np.float32)
+    ov *= np.float32(max(1.0, nscales / 4.0))
     pose = PoseExtractor(ctx, net)
     ovd = _dev(ov)
     pose.set_overlay(ovd)
