@@ -377,6 +377,9 @@ int opk_pose_records(opk_pose* pose, float* records_host, size_t capacity, size_
  * full stack on first request after a collect, while no later batch is in flight.  With
  * opk_pose_forward_net_output the net output buffer must stay unchanged until then. */
 int opk_pose_heatmaps(opk_pose* pose, float** heat_dev, int shape[4]);
+/* shape of the last collected batch's heat maps (spHeatMapsBlob->shape(), poseExtractorCaffe.cpp:
+ * 651-663) without writing them */
+int opk_pose_heatmap_size(opk_pose* pose, int shape[4]);
 int opk_pose_peaks(opk_pose* pose, float** peaks_dev, int shape[4]);
 float opk_pose_scale_net_to_output(opk_pose* pose);
 /* PoseExtractorNet::getHeatMapsCopy (src/openpose/pose/poseExtractorNet.cpp:106-244) for every

@@ -57,15 +57,18 @@ namespace op
             const void* gpu() { toGpu(); return mGpu; }
             void* mutableCpu() { toCpu(); mHead = HEAD_AT_CPU; return cpuPtr(); }
             void* mutableGpu() { toGpu(); mHead = HEAD_AT_GPU; return mGpu; }
-            void setCpu(void* data)
+            // an adopted (external) buffer holds `bytes` = the blob's current count, which may be less
+            // than this memory's capacity after a shrinking Reshape: transfers are limited to it
+            void setCpu(void* data, const size_t bytes)
             {
                 if (data == nullptr)
                     error("set_cpu_data: NULL pointer.", __LINE__, __FUNCTION__, __FILE__);
                 mOwnCpu.clear();
                 mCpu = data;
+                mExtBytes = std::min(bytes, mBytes);
                 mHead = HEAD_AT_CPU;
             }
-            void setGpu(void* data)
+            void setGpu(void* data, const size_t bytes)
             {
                 if (data == nullptr)
                     error("set_gpu_data: NULL pointer.", __LINE__, __FUNCTION__, __FILE__);
@@ -74,12 +77,14 @@ namespace op
                 mCtx = opkShimThreadContext();
                 mGpu = data;
                 mOwnGpu = false;
+                mExtBytes = std::min(bytes, mBytes);
                 mHead = HEAD_AT_GPU;
             }
             size_t bytes() const { return mBytes; }
 
         private:
             void* cpuPtr() { return mCpu ? mCpu : (void*)mOwnCpu.data(); }
+            size_t xfer() const { return mCpu || (mGpu && !mOwnGpu) ? mExtBytes : mBytes; }
             void allocCpu()
             {
                 if (!mCpu && mOwnCpu.size() != mBytes)
@@ -104,8 +109,8 @@ namespace op
                         break;
                     case HEAD_AT_GPU:
                         allocCpu();
-                        if (mBytes)
-                            checkOpk(opk_memcpy_d2h(mCtx.get(), cpuPtr(), mGpu, mBytes), __LINE__, __FUNCTION__);
+                        if (xfer())
+                            checkOpk(opk_memcpy_d2h(mCtx.get(), cpuPtr(), mGpu, xfer()), __LINE__, __FUNCTION__);
                         mHead = SYNCED;
                         break;
                     default:
@@ -123,8 +128,8 @@ namespace op
                         break;
                     case HEAD_AT_CPU:
                         allocGpu();
-                        if (mBytes)
-                            checkOpk(opk_memcpy_h2d(mCtx.get(), mGpu, cpuPtr(), mBytes), __LINE__, __FUNCTION__);
+                        if (xfer())
+                            checkOpk(opk_memcpy_h2d(mCtx.get(), mGpu, cpuPtr(), xfer()), __LINE__, __FUNCTION__);
                         mHead = SYNCED;
                         break;
                     default:
@@ -136,6 +141,7 @@ namespace op
             Head mHead = UNINITIALIZED;
             std::vector<unsigned char> mOwnCpu;
             void* mCpu = nullptr;   // external host buffer (set_cpu_data), else mOwnCpu
+            size_t mExtBytes = 0;   // bytes of an adopted buffer
             OpkContext mCtx;   // the context of the device buffer (kept alive by this)
             void* mGpu = nullptr;
             bool mOwnGpu = false;
@@ -347,7 +353,7 @@ namespace op
     {
         if (!spImpl->data)
             error("set_cpu_data on an unshaped blob.", __LINE__, __FUNCTION__, __FILE__);
-        spImpl->data->setCpu(data);
+        spImpl->data->setCpu(data, (size_t)spImpl->count * sizeof(T));
     }
 
     template<typename T>
@@ -367,7 +373,7 @@ namespace op
     {
         if (!spImpl->data)
             error("set_gpu_data on an unshaped blob.", __LINE__, __FUNCTION__, __FILE__);
-        spImpl->data->setGpu(data);
+        spImpl->data->setGpu(data, (size_t)spImpl->count * sizeof(T));
     }
 
     template<typename T>

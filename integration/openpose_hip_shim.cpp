@@ -392,10 +392,7 @@ namespace op
         try
         {
             (void)enableGoogleLogging;
-            // heat maps at the net input resolution (mUpsamplingRatio <= 0, poseExtractorCaffe.cpp:274-276)
-            if (upsamplingRatio > 0.f && upsamplingRatio != getPoseNetDecreaseFactor(poseModel))
-                error("libopk_hip produces heat maps at the net input resolution only (--upsampling_ratio 0).",
-                      __LINE__, __FUNCTION__, __FILE__);
+            upImpl->upsamplingRatio = upsamplingRatio;   // --upsampling_ratio (poseExtractorCaffe.cpp:47-54,281-287)
             upImpl->poseModel = poseModel;
             upImpl->gpuId = gpuId;
             upImpl->enableNet = enableNet;
@@ -433,6 +430,7 @@ namespace op
                   __LINE__, __FUNCTION__);
             check(opk_pose_model_info((int)impl.poseModel, &impl.parts, nullptr, nullptr, &impl.heatChannels,
                                       nullptr, nullptr), __LINE__, __FUNCTION__);
+            check(opk_pose_set_upsampling_ratio(impl.pose, impl.upsamplingRatio), __LINE__, __FUNCTION__);
         }
         catch (const std::exception& e)
         {
@@ -531,9 +529,15 @@ namespace op
                 mPoseScores.reset();
             }
             mScaleNetToOutput = opk_pose_scale_net_to_output(impl.pose);
-            mNetOutputSize = Point<int>{netW, netH};   // ratio 1 (poseExtractorCaffe.cpp:271-279)
-            impl.heatH = netH;
-            impl.heatW = netW;
+            // mNetOutputSize = the net input size x (ratio / decrease factor), ratio 1 without
+            // --upsampling_ratio (poseExtractorCaffe.cpp:281-287)
+            const auto ratio = (impl.upsamplingRatio <= 0.f
+                                    ? 1.f : impl.upsamplingRatio / getPoseNetDecreaseFactor(impl.poseModel));
+            mNetOutputSize = Point<int>{int(ratio * netW + 0.5f), int(ratio * netH + 0.5f)};
+            int shape[4];
+            check(opk_pose_heatmap_size(impl.pose, shape), __LINE__, __FUNCTION__);
+            impl.heatH = shape[2];
+            impl.heatW = shape[3];
             impl.heatFresh = false;
             impl.peaksFresh = false;
         }

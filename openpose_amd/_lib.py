@@ -72,6 +72,7 @@ _SIGS = {
     "opk_pose_forward": (_i, [_p, _p, _i, _i, _i, _i, _i]),
     "opk_pose_forward_net_output": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i]),
     "opk_pose_set_upsampling_ratio": (_i, [_p, _f]),
+    "opk_pose_heatmap_size": (_i, [_p, _ip]),
     "opk_pose_set_overlay": (_i, [_p, _p]),
     "opk_pose_submit": (_i, [_p, _p, _i, _i, _i, _i, _i]),
     "opk_pose_submit_net_output": (_i, [_p, _p, _i, _i, _i, _i, _i, _i, _i]),

@@ -318,6 +318,14 @@ int opk_pose_heatmaps(opk_pose* p, float** heat, int shape[4])
     });
 }
 
+int opk_pose_heatmap_size(opk_pose* p, int shape[4])
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p && shape, "NULL argument");
+        p->pose->heatmap_size(shape);
+    });
+}
+
 int opk_pose_peaks(opk_pose* p, float** peaks, int shape[4])
 {
     return guarded_net([&] {

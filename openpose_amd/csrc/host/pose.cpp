@@ -95,6 +95,12 @@ size_t PoseHip::record_floats() const
     return 1 + (size_t)m.npairs() * kMaxPeaks * kMaxPeaks;
 }
 
+void PoseHip::heatmap_size(int shape[4]) const
+{
+    OPK_CHECK_ARG(last_ >= 0, "no collected batch");
+    shape[0] = n_; shape[1] = slots_[last_].heat.channels; shape[2] = hh_; shape[3] = hw_;
+}
+
 float* PoseHip::heatmaps(int shape[4])
 {
     OPK_CHECK_ARG(last_ >= 0, "no collected batch");

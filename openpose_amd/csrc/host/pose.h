@@ -63,6 +63,7 @@ public:
     // pipeline evaluates them lazily from the net output: HeatMap in kernels.h); only while no
     // later batch is in flight (its net forward overwrites the net output)
     float* heatmaps(int shape[4]);
+    void heatmap_size(int shape[4]) const;   // the last collected batch's, nothing materialised
     float* peaks(int shape[4]) const;
     // PoseExtractorNet::getHeatMapsCopy (poseExtractorNet.cpp:106-244) for every frame of the last
     // collected batch: types bit 0 parts, bit 1 background, bit 2 PAFs (in that order), scale_mode
