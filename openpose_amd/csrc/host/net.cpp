@@ -229,6 +229,22 @@ void NetHip::plan(const std::vector<LayerDesc>& layers)
             a.out32_coff < 0 && b.out32_coff < 0)
             fuse1_ = {steps_[0].idx, steps_[1].idx, steps_[2].idx, abuf, bbuf};
     }
+    // conv -> pool pairs whose conv output only the pool reads (pool2 after conv2_2, pool3 after
+    // conv3_4 in BODY_25): candidates for the pool-fused conv3w8 epilogue
+    pool_conv_.assign(pools_.size(), -1);
+    for (size_t si = 0; si + 1 < steps_.size(); ++si) {
+        if (!steps_[si].conv || steps_[si + 1].conv) continue;
+        const ConvPlan& c = convs_[steps_[si].idx];
+        const PoolPlan& p = pools_[steps_[si + 1].idx];
+        if (c.from_image || c.info.k != 3 || c.outs.size() != 1 || c.outs[0].coff != 0 ||
+            c.out32_coff >= 0 || c.info.cout % 128 != 0 || border_ != 1 || fuse1_.b == steps_[si].idx ||
+            p.in_buf != c.outs[0].buf)
+            continue;
+        int readers = 0;
+        for (const auto& q : convs_) readers += q.in.buf == p.in_buf;
+        for (const auto& q : pools_) readers += q.in_buf == p.in_buf;
+        if (readers == 1) pool_conv_[steps_[si + 1].idx] = steps_[si].idx;
+    }
     // Mconv6 -> Mconv7 head pairs (conv_head.hip)
     for (size_t si = 0; si + 1 < steps_.size(); ++si) {
         if (!steps_[si].conv || !steps_[si + 1].conv) continue;
@@ -410,6 +426,18 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
                conv1_fused_supported(h, w, 64, 64);
     // HEAD_FUSE=0 (opk_dev_set, A/B tests): Mconv6 and Mconv7 as two conv3 launches
     S.fusedh = !heads_.empty() && dev_switch("HEAD_FUSE", 1) != 0;
+    // POOL_FUSE=0 (opk_dev_set, A/B tests): the pools as their own kernels
+    S.poolfused.assign(pools_.size(), 0);
+    for (size_t q = 0; q < pools_.size(); ++q) {
+        const int ci = pool_conv_[q];
+        if (ci < 0 || dev_switch("POOL_FUSE", 1) == 0) continue;
+        const ConvPlan& c = convs_[ci];
+        const int H = lh_[c.level], W = lw_[c.level];
+        const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, 3, border_);
+        S.poolfused[q] = s3.persist && s3.nw == 16 && H % 2 == 0 && W % 2 == 0 && s3.sw % 2 == 0 &&
+                         6 * (s3.sw + 2) <= 512 && s3.sw + 2 > 16 &&
+                         lh_[c.level + 1] == H / 2 && lw_[c.level + 1] == W / 2;
+    }
     for (size_t i = 0; i < bufs_.size(); ++i) {
         S.mem.push_back(std::make_unique<DevBuf>());
         if ((int)i == image_buf_) continue;   // conv_image reads the NCHW input itself
@@ -418,6 +446,10 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
         if (S.fusedh && head_buf) continue;   // Mconv6 outputs live only inside conv_head_kernel
         if (S.fused1 && ((int)i == fuse1_.abuf || (int)i == fuse1_.bbuf))
             continue;   // conv1_1 / conv1_2 outputs live only inside conv1_fused_kernel
+        bool pooled_away = false;
+        for (size_t q = 0; q < pools_.size(); ++q)
+            pooled_away = pooled_away || (S.poolfused[q] && pools_[q].in_buf == (int)i);
+        if (pooled_away) continue;   // written pooled by its conv's epilogue
         // zeroed guards: the kernels read up to W+3 positions before the first frame and up to
         // kConvGuardTail positions after the last one (conv.h)
         const int L = bufs_[i].level, B = border_;
@@ -458,7 +490,9 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
             a.sw = s3.sw;
             a.nstrips = s3.nstrips;
             a.sink = sink;
-            a.cus = cus_;
+            // GRID_CUS (opk_dev_set, dev): persistent grids of fewer CUs, e.g. two pipelines on
+            // concurrent streams sharing the chip
+            a.cus = std::min(cus_, std::max(1, dev_switch("GRID_CUS", cus_)));
         }
         a.w = static_cast<const uint16_t*>(use3 ? c.w3.ptr : c.w.ptr);
         a.wg = use3 ? static_cast<const uint16_t*>(c.wg.ptr) : nullptr;
@@ -476,6 +510,14 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
             a.dst_cs[d] = bufs_[c.outs[d].buf].cs;
             a.dst_coff[d] = c.outs[d].coff;
         }
+        for (size_t q = 0; q < pools_.size(); ++q)
+            if (S.poolfused[q] && pool_conv_[q] == (int)ci) {   // the pooled image instead
+                a.pool = 1;
+                a.ndst = 1;
+                a.dst[0] = ptr[pools_[q].out_buf];
+                a.dst_cs[0] = bufs_[pools_[q].out_buf].cs;
+                a.dst_coff[0] = 0;
+            }
         if (c.out32_coff >= 0) {
             OPK_CHECK_ARG(c.level == out_level_, c.info.name + ": output at another resolution");
             a.out32 = S.out32;
@@ -538,7 +580,7 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
         fa.out_coff = 0;
         fa.OH = lh_[1];
         fa.OW = lw_[1];
-        launch_conv1_fused(fa, cus_, st);
+        launch_conv1_fused(fa, std::min(cus_, std::max(1, dev_switch("GRID_CUS", cus_))), st);
         first = 3;
     }
     for (size_t si = first; si < steps_.size(); ++si) {
@@ -582,6 +624,7 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
             if (c.from_image) launch_conv_image(a, input, st);
             else launch_conv3(a, st);
         } else {
+            if (S.poolfused[s.idx]) continue;   // ran in its conv's epilogue
             const PoolPlan& p = pools_[s.idx];
             const int L = p.level_in;
             launch_maxpool2(ptr[p.out_buf], ptr[p.in_buf], n, lh_[L], lw_[L],

@@ -87,6 +87,7 @@ private:
         float* out32 = nullptr;
         bool fused1 = false;           // conv1_fused_kernel runs for this shape
         bool fusedh = false;           // conv_head_kernel runs the fused head pairs
+        std::vector<char> poolfused;   // per pool: run inside its conv's epilogue (conv3w8 POOL)
         std::vector<ConvArgs> args;    // per conv
         std::vector<char> use3;        // per conv: launch conv3
     };
@@ -111,6 +112,9 @@ private:
     // a 1x1 conv with <= 64 outputs, consecutive steps; buf = a's output buffer
     struct FuseHead { int a = -1, b = -1, step = -1, buf = -1; };
     std::vector<FuseHead> heads_;
+    // conv -> 2x2 max pool pairs (conv3w8.hip POOL epilogue), per pool: the conv that alone feeds it
+    // (and nothing else reads), -1 none; per input shape it runs fused where conv3w8 supports it
+    std::vector<int> pool_conv_;
     int cus_ = 256;               // compute units (persistent-kernel grid)
     int border_ = 1;              // zero border of every padded image (widest conv pad, >= 1)
 

@@ -42,6 +42,8 @@ struct ConvArgs {
     void* sink;           // conv3 persistent variant: >= kConv3SinkBytes of scratch (masked stores)
     int cus;              // conv3 persistent variant: compute units (grid size); 0 disables it
     int border;           // zero border of the padded images (conv3 / conv_image; 0 means 1)
+    int pool;             // conv3w8: 2x2/2 max pool fused into the epilogue; dst[0] is the pooled
+                          // padded image [frames][H/2+2][W/2+2][cs] (conv3w8_pool_supported)
 };
 
 // conv3.hip: 7x7, 3x3 and 1x1, input halo staged once per 32-channel chunk over a "virtual image" of
@@ -67,6 +69,7 @@ bool conv3w_supported(const ConvArgs& a);
 void launch_conv3w(const ConvArgs& a, hipStream_t stream);
 // conv3w8.hip: the same tile with 8 waves of 64 x BN (fewer LDS fragment reads per MFMA)
 bool conv3w8_supported(const ConvArgs& a);
+bool conv3w8_pool_supported(const ConvArgs& a);
 void launch_conv3w8(const ConvArgs& a, hipStream_t stream);
 // conv3wg.hip: the persistent 3x3 kernel as Winograd F(2,3) along x (2/3 of the MFMAs), 256 x
 // {128, 96} tiles; weights a.wg packed by conv3wg_pack: [cout/BN][cin_pad/32][ky][term 4][BN][32]

@@ -764,6 +764,14 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     const int nn = (a.cout + s.bn - 1) / s.bn;
     const long ntiles = ((total + s.bm - 1) / s.bm) * nn;
     dim3 grid((unsigned)ntiles);
+    // conv + 2x2 max pool in one persistent kernel (conv3w8.hip POOL epilogue); the planner only
+    // asks for it where conv3w8_pool_supported holds
+    if (a.pool) {
+        OPK_CHECK_ARG(s.nw == 16 && s.persist && VW > 16 && conv3w8_pool_supported(a),
+                      "pool fusion requested for an unsupported conv");
+        launch_conv3w8(a, stream);
+        return;
+    }
     // Winograd F(2,3) along x for the persistent 3x3 layers (conv3wg.hip), opt-in (CONV3WG=1):
     // measured 15-20 % SLOWER than the direct kernels on every BODY_25 layer (CNN 17.28 -> 19.72
     // ms per 64 frames, profiles/round3/wino/): its 4 accumulators per output pair halve the wave

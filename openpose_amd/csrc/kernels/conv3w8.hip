@@ -45,7 +45,14 @@ constexpr int k8_BM = 512, k8_HR = 688, k8_NW = 8;
     asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst_) : "v"(addr_), "i"(off_))
 #endif
 
-template <int BN, int NB>
+// POOL: the 2x2 / stride-2 max pool that follows the conv (pool2 / pool3 of BODY_25,
+// pose_deploy.prototxt:70-87,149-166) fused into the epilogue: a tile is 6 virtual rows starting
+// at an odd row, one position in (p0 = (6m + 1) VW + 1), so every pooling window lies inside one
+// tile with its column pair in lanes (2k, 2k+1) of a fragment; the lanes take the horizontal max
+// through a DPP swap, the first row of each window stores it into the pooled image, and after a
+// workgroup barrier the second row's lanes read it back, take the max and store.  The full-size
+// conv output is never written.
+template <int BN, int NB, bool POOL>
 __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a)
 {
     constexpr int NW = k8_NW, BM = k8_BM, HR = k8_HR;
@@ -70,7 +77,11 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int r16 = lane & 15, q = lane >> 4;
     const Strips g(a);
-    const int ntm = (g.total + BM - 1) / BM;
+    // POOL tiles: 6 rows of VW positions from row 6m + 1, position 1 (the 512 computed positions
+    // overlap the next tile's first 512 - 6 VW, which are not stored)
+    const int BMP = POOL ? 6 * g.VW : BM;
+    const int ntm = POOL ? (g.total / g.VW - 1 + 5) / 6 : (g.total + BM - 1) / BM;
+#define OPK8_P0(mt_) (POOL ? (6 * (mt_) + 1) * g.VW + 1 : (mt_) * BM)
     // output-channel blocks of BN: tile t = (m-tile t / NB, n-block t % NB);
     // the grid is a multiple
     // of NB (host), so a block keeps one n-block -- its weights and bias -- for the whole launch
@@ -110,7 +121,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         const int hr_ = ((i_) * NW + wave) * 16 + lrow;                                       \
         const int lp_ = phys ^ (((hr_ >> 2) & 1) << 1);                                       \
         int f_, yy_, xx_, s_;                                                                 \
-        const long pos_ = g.map((mt_) * BM - g.VW - 1 + hr_, f_, yy_, xx_, s_);               \
+        const long pos_ = g.map(OPK8_P0(mt_) - g.VW - 1 + hr_, f_, yy_, xx_, s_);             \
         (uint32_t)(((pos_ + 1) * a.in_cs + lp_ * 8) * 2);                                     \
     })
 #define OPK8_AROW(dst_, mt_)                                                                  \
@@ -294,7 +305,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         int prow[MF];
         bool pok[MF];
         {
-            const int pbase = m * BM + wave * WROWS + er16;
+            const int pbase = OPK8_P0(m) + wave * WROWS + er16;
             int f, yy, xx, s;
             prow[0] = (int)g.map(pbase, f, yy, xx, s);
             pok[0] = g.interior(yy, xx, s, a.W);
@@ -320,6 +331,83 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         const int nd = a.ndst;
         uint16_t* const d0 = a.dst[0] + a.dst_coff[0] + nblk * BN;
         const int cs0 = a.dst_cs[0];
+        if constexpr (POOL) {
+            // pooled position of each fragment's lane pair; phase 1 = the window's first row
+            int qrow[MF];
+            bool qok[MF], first[MF];
+            {
+                const int OWp = (a.W >> 1) + 2, OHp = (a.H >> 1) + 2;
+                const int pb = OPK8_P0(m) + wave * WROWS + er16;
+#pragma unroll
+                for (int i = 0; i < MF; ++i) {
+                    int f, yy, xx, s;
+                    (void)g.map(pb + i * 16, f, yy, xx, s);
+                    const int k = wave * WROWS + i * 16 + er16;   // tile-local position
+                    qok[i] = pok[i] && (er16 & 1) == 0 && k < BMP;
+                    first[i] = (yy & 1) != 0;
+                    qrow[i] = qok[i] ? (f * OHp + ((yy - 1) >> 1) + 1) * OWp + ((s * g.sw + xx - 1) >> 1) + 1 : 0;
+                }
+            }
+            uint4 keep[MF][NF / 2];
+#pragma unroll
+            for (int j = 0; j < NF; j += 2) {
+                float4_t bq[2], mq[2];
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    bq[k] = *reinterpret_cast<const float4_t*>(lb + (j + k) * 64);
+                    mq[k] = *reinterpret_cast<const float4_t*>(lb + BN * 4 + (j + k) * 64);
+                }
+#pragma unroll
+                for (int i = 0; i < MF; ++i) {
+                    uint32_t pk[2][2];
+#pragma unroll
+                    for (int h = 0; h < 2; ++h) {
+                        const float4_t t = acc[i][j + h] + bq[h];
+                        const float4_t tm = t * mq[h];
+                        float v[4];
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) {
+                            v[r] = t[r] > 0.f ? t[r] : tm[r];
+                            // the column pair's max: lane ^ 1 holds the next position
+                            const float o = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                __builtin_bit_cast(int, v[r]), 0xB1, 0xF, 0xF, false));
+                            v[r] = fmaxf(v[r], o);
+                        }
+                        pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
+                        pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                    }
+                    const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+                    const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+                    keep[i][j / 2] = make_uint4(sl[0], sh[0], sl[1], sh[1]);
+                    uint4* p = reinterpret_cast<uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
+                    *(qok[i] && first[i] ? p : sink4) = keep[i][j / 2];
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            uint4 got[MF][NF / 2];
+#pragma unroll
+            for (int j = 0; j < NF; j += 2)
+#pragma unroll
+                for (int i = 0; i < MF; ++i) {
+                    const uint4* p = reinterpret_cast<const uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
+                    got[i][j / 2] = *(qok[i] && !first[i] ? p : sink4);
+                }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+            for (int j = 0; j < NF; j += 2)
+#pragma unroll
+                for (int i = 0; i < MF; ++i) {
+                    const uint4 x = keep[i][j / 2], y = got[i][j / 2];
+                    uint4 r;
+                    r.x = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(half2_t, x.x), __builtin_bit_cast(half2_t, y.x)));
+                    r.y = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(half2_t, x.y), __builtin_bit_cast(half2_t, y.y)));
+                    r.z = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(half2_t, x.z), __builtin_bit_cast(half2_t, y.z)));
+                    r.w = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(half2_t, x.w), __builtin_bit_cast(half2_t, y.w)));
+                    uint4* p = reinterpret_cast<uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
+                    *(qok[i] && !first[i] ? p : sink4) = r;
+                }
+        } else {
 #pragma unroll
         for (int j = 0; j < NF; j += 2) {
             float4_t bq[2], mq[2];
@@ -357,6 +445,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                 }
             }
         }
+        }
 #pragma unroll
         for (int i = 0; i < MF; ++i)
 #pragma unroll
@@ -376,6 +465,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
 #undef OPK8_ISSUE
 #undef OPK8_AROW
 #undef OPK8_AROW1
+#undef OPK8_P0
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
 }
 
@@ -395,19 +485,38 @@ bool conv3w8_supported(const ConvArgs& a)
            a.sw + 2 * a.border > 16;
 }
 
+bool conv3w8_pool_supported(const ConvArgs& a)
+{
+    // windows never straddle a strip or a 6-row tile: even sizes, even strips, 1-pixel border;
+    // the pooled image is dst[0] (one destination)
+    return conv3w8_supported(a) && a.cout % 128 == 0 && a.ndst == 1 && a.border == 1 &&
+           a.H % 2 == 0 && a.W % 2 == 0 && a.sw % 2 == 0 && 6 * (a.sw + 2) <= k8_BM;
+}
+
 void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
 {
     OPK_CHECK_ARG(conv3w8_supported(a), "conv3w8: 96 or k x 128 output channels, 3x3, one aligned slice");
     const long total = (long)a.frames * a.nstrips * (a.H + 2 * a.border) * (a.sw + 2 * a.border);
-    const long ntm = (total + k8_BM - 1) / k8_BM;
+    const int VW = a.sw + 2 * a.border;
+    const bool pool = a.pool != 0;
+    if (pool)
+        OPK_CHECK_ARG(conv3w8_pool_supported(a), "conv3w8 + pool: even H, W and strips, 128k outputs, border 1");
+    const long ntm = pool ? (total / VW - 1 + 5) / 6 : (total + k8_BM - 1) / k8_BM;
     const int nb = a.cout == 96 ? 1 : a.cout / 128;
     // a multiple of the n-block count (each block keeps one n-block)
     const unsigned G = (unsigned)(std::min<long>(a.cus / nb, ntm) * nb);
     OPK_CHECK_ARG(G >= 1 && G <= 1024, "persistent grid exceeds the sink");
-    if (nb == 4) hipLaunchKernelGGL((conv3w8_kernel<128, 4>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
-    else if (nb == 2) hipLaunchKernelGGL((conv3w8_kernel<128, 2>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
-    else if (a.cout == 128) hipLaunchKernelGGL((conv3w8_kernel<128, 1>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
-    else hipLaunchKernelGGL((conv3w8_kernel<96, 1>), dim3(G), dim3(64 * k8_NW), 0, stream, a);
+#define OPK8_LAUNCH(BN_, NB_, P_) \
+    hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_>), dim3(G), dim3(64 * k8_NW), 0, stream, a)
+    if (pool) {
+        if (nb == 4) OPK8_LAUNCH(128, 4, true);
+        else if (nb == 2) OPK8_LAUNCH(128, 2, true);
+        else OPK8_LAUNCH(128, 1, true);
+    } else if (nb == 4) OPK8_LAUNCH(128, 4, false);
+    else if (nb == 2) OPK8_LAUNCH(128, 2, false);
+    else if (a.cout == 128) OPK8_LAUNCH(128, 1, false);
+    else OPK8_LAUNCH(96, 1, false);
+#undef OPK8_LAUNCH
     OPK_LAUNCH_CHECK();
 }
 

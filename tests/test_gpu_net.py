@@ -304,6 +304,8 @@ def torch_forward(graph, params, x):
             blobs[l["top"][0]] = F.prelu(blobs[l["bottom"][0]], s)
         elif t == "Concat":
             blobs[l["top"][0]] = torch.cat([blobs[b] for b in l["bottom"]], 1)
+        elif t == "Pooling":   # Caffe MAX 2x2 / 2, ceil sizing
+            blobs[l["top"][0]] = F.max_pool2d(blobs[l["bottom"][0]], 2, 2, ceil_mode=True)
     return blobs["net_output"].numpy()
 
 
@@ -386,3 +388,38 @@ def test_head_fusion_matches_unfused_and_oracle(ctx):
     assert rel_l2(outs["fused"], ref) < SMALL_TOL
     for c in range(ref.shape[1]):
         assert rel_l2(outs["fused"][:, c], ref[:, c]) < CHANNEL_TOL, c
+
+
+def test_pool_fused_epilogue_bit_identical(ctx):
+    """2x2 max pools fused into the epilogue of the conv that alone feeds them (conv3w8 POOL:
+    pool2 / pool3 of BODY_25, pose_deploy.prototxt:70-87,149-166) are bit-identical to the separate
+    pool kernel: one 128-channel and one 256-channel (2 n-block) conv, 8 x 368 x 328 (persistent
+    tiles, even 82-column strips at both levels)."""
+    L = conv("c1", "image", 64, 3, "relu") + conv("c2", "c1", 128, 3, "relu")
+    L.append(dict(name="p1", type="Pooling", bottom=["c2"], top=["p1"], kernel_size=2, stride=2))
+    L += conv("c3", "p1", 256, 3, "relu")
+    L.append(dict(name="p2", type="Pooling", bottom=["c3"], top=["p2"], kernel_size=2, stride=2))
+    L += conv("c4", "p2", 52, 1)
+    L.append(dict(name="net_output", type="Concat", bottom=["c4"], top=["net_output"]))
+    text = prototxt.emit(L)
+    graph = prototxt.parse(text)
+    params = synth.he_weights(graph, seed=17)
+    x = np.random.default_rng(18).uniform(-0.5, 0.5, (8, 3, 368, 328)).astype(np.float32)
+    with tempfile.NamedTemporaryFile("w", suffix=".prototxt", delete=False) as f:
+        f.write(text)
+        path = f.name
+    outs = {}
+    try:
+        for name, fuse in (("fused", 1), ("separate", 0)):
+            with dev_switches(POOL_FUSE=fuse):
+                net = Net(ctx, path)
+                net.set_params(params)
+                net.forward(torch.from_numpy(x).cuda())
+                outs[name] = net.output_numpy()
+                net.close()
+    finally:
+        os.unlink(path)
+    assert np.abs(outs["fused"]).max() > 0
+    np.testing.assert_array_equal(outs["fused"], outs["separate"])
+    ref = torch_forward(graph, params, x[:2])
+    assert rel_l2(outs["fused"][:2], ref) < SMALL_TOL

@@ -62,9 +62,16 @@ for r in fw:
             continue
         fl = flops(l, lvl)
         key = (l['num_output'], l['kernel_size'], lvl)
+        pooled = 'true>' in name and 'conv3w8' in name   # conv3w8 POOL: the next pool ran inside
+        if pooled:
+            key = ('N=%4d k=%d lvl=%d +pool' % key, 3, lvl)
         if per_layer:
-            print('%-28s cin=%4d cout=%4d k=%d lvl=%d %8.1f us %7.1f TF/s' %
-                  (l['name'], l['cin'], l['num_output'], l['kernel_size'], lvl, d, fl / d / 1e6))
+            print('%-28s cin=%4d cout=%4d k=%d lvl=%d %8.1f us %7.1f TF/s%s' %
+                  (l['name'], l['cin'], l['num_output'], l['kernel_size'], lvl, d, fl / d / 1e6,
+                   ' (+ %s)' % L[li]['name'] if pooled else ''))
+        if pooled:
+            li += 1
+            lvl += 1
     tot += d
     a = byn.setdefault(key, [0, 0, 0])
     a[0] += d

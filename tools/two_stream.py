@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 from openpose_amd import synth  # noqa: E402
-from openpose_amd.api import Context, Net, PoseExtractor  # noqa: E402
+from openpose_amd.api import Context, Net, PoseExtractor, dev_switches  # noqa: E402
 
 
 def run(streams, batch, steps, warmup=3):
@@ -65,9 +65,16 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--streams", type=int, nargs="+", default=[1, 2, 1, 2])
+    ap.add_argument("--grid-cus", type=int, default=0, help="GRID_CUS for runs with > 1 stream")
     args = ap.parse_args()
     for s in args.streams:
-        print(json.dumps(run(s, args.batch, args.steps)), flush=True)
+        if s > 1 and args.grid_cus:
+            with dev_switches(GRID_CUS=args.grid_cus):
+                r = run(s, args.batch, args.steps)
+            r["grid_cus"] = args.grid_cus
+        else:
+            r = run(s, args.batch, args.steps)
+        print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
