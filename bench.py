@@ -129,7 +129,7 @@ def pmc_traffic(batch):
     """HBM bytes of one CNN forward from the committed rocprofv3 PMC summary (FETCH_SIZE x2 on
     gfx950 + WRITE_SIZE over every kernel of one forward; tools/pmc_summary.py), or None when the
     summary was taken at another batch size."""
-    for rnd in ("round2", "round1"):
+    for rnd in ("round3", "round2", "round1"):
         path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
         try:
             with open(path) as f:
@@ -142,7 +142,7 @@ def pmc_traffic(batch):
 
 # per-step PMC counts of the post-processing kernels (overlay add, NMS detect + finalize, PAF
 # integrals) at 64 frames, from the committed rocprofv3 summary (tools/pmc_round.sh + pmc_report.py)
-POST_PMC = os.path.join(ROOT, "profiles", "round3", "pmc_head_r3a", "report.json")
+POST_PMC = os.path.join(ROOT, "profiles", "round3", "pmc_head_r3e", "report.json")
 POST_PMC_B135 = os.path.join(ROOT, "profiles", "round3", "pmc_body135", "report.json")
 VALU_PEAK_GINSTS = 1024 * 0.5 * 2.4   # wave64 VALU instructions: 1 per 2 cycles per SIMD-32, 2.4 GHz
 

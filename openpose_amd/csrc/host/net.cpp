@@ -307,13 +307,6 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
                     packed3[idx] = f2h(w[(((size_t)co * cin + ci) * k + t / k) * k + t % k]);
                 }
     }
-    // conv3wg.hip layout (Winograd-transformed weights) for the 3x3 layers it can run, only while
-    // the opt-in kernel is enabled (CONV3WG=1 when the weights are set)
-    std::vector<uint16_t> packedg;
-    if (!c.from_image && k == 3 && dev_switch("CONV3WG", 0) != 0 && (c.info.cout == 96 || c.info.cout % 128 == 0) && c.info.cout <= 512) {
-        packedg.resize(conv3wg_packed_elems(c.info.cout, c.cin_pad));
-        conv3wg_pack(packedg.data(), w, c.info.cout, cin, c.cin_pad);
-    }
     // conv_head.hip layouts: Mconv6 [cin_pad/32][n1][32]; Mconv7 K-permuted [n2 <= 32 ? 32 : 64][n1]
     std::vector<uint16_t> packedh;
     if (c.head >= 0) {
@@ -341,11 +334,6 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
     if (!packed3.empty()) {
         void* dw3 = c.w3.get(packed3.size() * 2);
         OPK_HIP(hipMemcpyAsync(dw3, packed3.data(), packed3.size() * 2, hipMemcpyHostToDevice,
-                               ctx_->stream));
-    }
-    if (!packedg.empty()) {
-        void* dwg = c.wg.get(packedg.size() * 2);
-        OPK_HIP(hipMemcpyAsync(dwg, packedg.data(), packedg.size() * 2, hipMemcpyHostToDevice,
                                ctx_->stream));
     }
     if (!packedh.empty()) {
@@ -495,7 +483,6 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
             a.cus = std::min(cus_, std::max(1, dev_switch("GRID_CUS", cus_)));
         }
         a.w = static_cast<const uint16_t*>(use3 ? c.w3.ptr : c.w.ptr);
-        a.wg = use3 ? static_cast<const uint16_t*>(c.wg.ptr) : nullptr;
         a.bias = static_cast<const float*>(c.bias.ptr);
         a.slope = static_cast<const float*>(c.slope.ptr);
         a.act = c.info.act;

@@ -69,7 +69,6 @@ private:
         int out32_coff = -1;
         DevBuf w, bias, slope;
         DevBuf w3;            // halo-kernel weight layout (3x3 convs)
-        DevBuf wg;            // Winograd F(2,3) layout (conv3wg.hip; 3x3 convs of 96 / 128k outputs)
         DevBuf wh;            // conv_head.hip layout when this conv is half of a fused head pair
         int head = -1;        // index into heads_ (as either half), -1 none
         bool loaded = false;

@@ -23,7 +23,6 @@ struct ConvArgs {
     int tapoff[9];        // position offset of each tap from the window's top-left position
     int ksteps;           // ceil(ntaps * cin_pad / 64)
     const uint16_t* w;    // [cout_pad][ksteps*64] fp16 bits
-    const uint16_t* wg;   // 3x3 only, optional: Winograd F(2,3)-along-x weights (conv3wg.hip)
     const float* bias;    // [cout]
     const float* slope;   // [cout] PReLU slopes (act == 2)
     int act;              // 0 none, 1 ReLU, 2 PReLU
@@ -71,14 +70,6 @@ void launch_conv3w(const ConvArgs& a, hipStream_t stream);
 bool conv3w8_supported(const ConvArgs& a);
 bool conv3w8_pool_supported(const ConvArgs& a);
 void launch_conv3w8(const ConvArgs& a, hipStream_t stream);
-// conv3wg.hip: the persistent 3x3 kernel as Winograd F(2,3) along x (2/3 of the MFMAs), 256 x
-// {128, 96} tiles; weights a.wg packed by conv3wg_pack: [cout/BN][cin_pad/32][ky][term 4][BN][32]
-// with U0 = g0, U1 = (g0+g1+g2)/2, U2 = (g0-g1+g2)/2, U3 = g2 (fp32 sums rounded to fp16)
-bool conv3wg_supported(const ConvArgs& a);
-void launch_conv3wg(const ConvArgs& a, hipStream_t stream);
-// host: w [cout][cin][3][3] fp32 -> the conv3wg layout (BN = 96 for cout 96, else 128)
-void conv3wg_pack(uint16_t* dst, const float* w, int cout, int cin, int cin_pad);
-size_t conv3wg_packed_elems(int cout, int cin_pad);
 
 // conv_head.hip: Mconv6 (1x1, n1 = 256 / 512 outputs, act6) -> Mconv7 (1x1, n2 <= 64 outputs) in
 // one kernel; the Mconv6 activations never leave the chip.  Input / outputs as ConvArgs (padded

@@ -772,26 +772,9 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
         launch_conv3w8(a, stream);
         return;
     }
-    // Winograd F(2,3) along x for the persistent 3x3 layers (conv3wg.hip), opt-in (CONV3WG=1):
-    // measured 15-20 % SLOWER than the direct kernels on every BODY_25 layer (CNN 17.28 -> 19.72
-    // ms per 64 frames, profiles/round3/wino/): its 4 accumulators per output pair halve the wave
-    // tile, doubling the LDS fragment reads per MFMA, with 8 MFMAs per term to hide them
-    if (s.nw == 16 && s.persist && a.wg && B == 1 && dev_switch("CONV3WG", 0) != 0) {
-        // its own strips: an even width (output pairs stay inside a virtual row), at most 92
-        // columns (the halo plane holds 128 + VW + 1 rows)
-        ConvArgs g = a;
-        g.nstrips = (a.W + 91) / 92;
-        g.sw = (a.W + g.nstrips - 1) / g.nstrips;
-        g.sw += g.sw & 1;
-        g.rcp[0] = (float)(1.0 / ((double)(a.H + 2 * B) * (g.sw + 2 * B)));
-        g.rcp[1] = (float)(1.0 / (double)(g.sw + 2 * B));
-        g.rcp[2] = (float)(1.0 / (double)g.nstrips);
-        const long gtotal = (long)a.frames * g.nstrips * (a.H + 2 * B) * (g.sw + 2 * B);
-        if (gtotal + 512 < (1L << 24) && conv3wg_supported(g)) {
-            launch_conv3wg(g, stream);
-            return;
-        }
-    }
+    // (a Winograd F(2,3)-along-x variant of the persistent kernel measured 15-50 % slower on every
+    // BODY_25 layer -- LDS-read bound: 4 accumulators per output pair halve the wave tile, doubling
+    // the fragment reads per MFMA; removed, source and numbers in profiles/round3/wino/)
     // several 128-channel n-blocks (the VGG 256 / 512-channel layers): conv3w8 with one n-block
     // per persistent block (bit-identical; CONV3W8N=0: the 16-wave conv3_kernel)
     if (s.nw == 16 && s.persist && nn > 1 && s.bn == 128 && a.sink && !a.out32 && VW > 16 &&

@@ -395,3 +395,62 @@ def test_upsampling_ratio_bitexact(ctx, ratio):
         pose.set_map_semantics(1)
         with pytest.raises(OpkError, match="8x resize"):
             pose.forward_net_output(_dev(fields), (656, 368), (1280, 720))
+
+
+def test_two_threads_own_contexts_concurrent(ctx):
+    """The drop-in's threading model in-process (wrapperAuxiliary.hpp:328-337: one worker thread per
+    --num_gpu, each with its own PoseExtractor): two host threads, each with its own opk context on
+    its own stream, net and PoseExtractor, forward concurrently (ctypes drops the GIL in every
+    library call) and every repetition gives the single-thread keypoints, peaks and heat maps."""
+    import threading
+    from openpose_amd.api import Context
+    graph = body25.layers()
+    params = synth.he_weights(graph, seed=61, out_scale=0.02)
+    rng = np.random.default_rng(62)
+    x = rng.uniform(-0.5, 0.5, (2, 3, 368, 656)).astype(np.float32)
+    ov = np.stack([synth.overlay(4, 46, 82, seed=6300 + k) for k in range(2)]).astype(np.float32)
+
+    def run(c, reps):
+        net = Net(c, "builtin:BODY_25")
+        net.set_params(params)
+        pose = PoseExtractor(c, net)
+        pose.set_overlay(_dev(ov))
+        res = []
+        for _ in range(reps):
+            pose.forward(_dev(x), (1280, 720))
+            res.append(([pose.keypoints(k) for k in range(2)], pose.peaks_numpy().copy(),
+                        pose.heatmaps_numpy().copy()))
+        pose.close()
+        net.close()
+        return res
+
+    ref = run(ctx, 1)[0]
+    assert sum(len(kp) for kp, _ in ref[0]) >= 2
+    results, errors = {}, []
+    start = threading.Barrier(2)
+
+    def worker(t):
+        try:
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                c = Context(0, s)
+                start.wait()
+                results[t] = run(c, 3)
+                c.close()
+        except Exception as e:   # re-raised on the main thread below
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for th in threads:
+        th.start()
+    for th in threads:
+        th.join()
+    assert not errors, errors
+    for t in range(2):
+        assert len(results[t]) == 3
+        for kps, peaks, heat in results[t]:
+            for (kp, ks), (rk, rs) in zip(kps, ref[0]):
+                np.testing.assert_array_equal(kp, rk)
+                np.testing.assert_array_equal(ks, rs)
+            np.testing.assert_array_equal(peaks, ref[1])
+            np.testing.assert_array_equal(heat, ref[2])
