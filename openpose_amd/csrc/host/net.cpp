@@ -330,6 +330,9 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
     std::vector<float> bias(cpad, 0.f), sl(cpad, 0.f);
     std::copy(b, b + c.info.cout, bias.begin());
     if (slope) std::copy(slope, slope + c.info.cout, sl.begin());
+    c.slope01 = true;
+    if (slope)
+        for (int i = 0; i < c.info.cout; ++i) c.slope01 = c.slope01 && slope[i] >= 0.f && slope[i] <= 1.f;
     ctx_->bind();
     if (!packed3.empty()) {
         void* dw3 = c.w3.get(packed3.size() * 2);
@@ -486,6 +489,7 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
         a.bias = static_cast<const float*>(c.bias.ptr);
         a.slope = static_cast<const float*>(c.slope.ptr);
         a.act = c.info.act;
+        a.actmax = dev_switch("EPI_MAX", 1) != 0;   // and the conv's slopes (at launch: set_conv may follow)
         a.frames = n;
         a.H = H;
         a.W = W;
@@ -608,8 +612,13 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
                 ++si;   // Mconv7 ran inside
                 continue;
             }
-            if (c.from_image) launch_conv_image(a, input, st);
-            else launch_conv3(a, st);
+            if (c.from_image) {
+                launch_conv_image(a, input, st);
+            } else {
+                ConvArgs a3 = a;
+                a3.actmax = a.actmax && c.slope01;
+                launch_conv3(a3, st);
+            }
         } else {
             if (S.poolfused[s.idx]) continue;   // ran in its conv's epilogue
             const PoolPlan& p = pools_[s.idx];

@@ -72,6 +72,7 @@ private:
         DevBuf wh;            // conv_head.hip layout when this conv is half of a fused head pair
         int head = -1;        // index into heads_ (as either half), -1 none
         bool loaded = false;
+        bool slope01 = true;  // PReLU slopes all in [0, 1] (ConvArgs::actmax)
     };
     struct PoolPlan { int in_buf, out_buf, level_in, channels; };
     struct Step { bool conv; int idx; };

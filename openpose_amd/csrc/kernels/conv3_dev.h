@@ -98,7 +98,23 @@ struct Strips {
         s = vf - f * nstrips;
         return (long)(f * Hp + yy) * Wp + s * sw + xx;
     }
+    // padded-image position of virtual position v only (halo rows): with one strip the virtual
+    // image IS the padded image (sw = W, VW = Wp), so no division is needed
+    __device__ long pos(int v) const
+    {
+        if (nstrips == 1) return v >= 0 && v < total ? v : -1;
+        int f, yy, xx, s;
+        return map(v, f, yy, xx, s);
+    }
 };
+
+// epilogue activation of t = acc + bias with tm = t * m (m = 1 none, 0 ReLU, slope PReLU):
+// MX (ConvArgs::actmax, every m in [0, 1]) -> max(t, tm), which equals the select for every finite t
+template <bool MX>
+__device__ __forceinline__ float act_pick(float t, float tm)
+{
+    return MX ? __builtin_fmaxf(t, tm) : (t > 0.f ? t : tm);
+}
 
 #define OPK3_VM_CASE(n_) case n_: vm_wait<n_>(); break;
 __device__ __forceinline__ void vm_wait_rt64(int n)

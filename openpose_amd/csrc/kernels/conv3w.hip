@@ -91,7 +91,8 @@ __device__ __forceinline__ void opkw_st(uint2* p, const uint2& v)
 // DMA_END (the default): issue unit u+2's DMA after tap 2 instead of right after the mid-unit
 // barrier -- fewer registers live at the issue point (no spills), two thirds of a unit less lead
 // time; measured 2-3 % faster on the stage layers.  CONV3W=2 selects the other placement (A/B).
-template <int BN, bool DMA_END>
+// MX: the activation as max(t, t*m) (ConvArgs::actmax; conv3_dev.h act_pick)
+template <int BN, bool DMA_END, bool MX>
 __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
 {
     constexpr int NW = kW_NW, BM = kW_BM, HR = kW_HR;
@@ -150,8 +151,7 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
         _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_) {                                  \
             const int hr_ = (i_ * NW + wave) * 16 + lrow;                                     \
             const int lp_ = phys ^ (((hr_ >> 2) & 1) << 1);                                   \
-            int f_, yy_, xx_, s_;                                                             \
-            const long pos_ = g.map((mt_) * BM - g.VW - 1 + hr_, f_, yy_, xx_, s_);           \
+            const long pos_ = g.pos((mt_) * BM - g.VW - 1 + hr_);                              \
             dst_[i_] = (uint32_t)(((pos_ + 1) * a.in_cs + lp_ * 8) * 2);                      \
         }                                                                                     \
     } while (0)
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
         const float4_t t_ = acc[i_][j_] + bq[(j_) & 1];                                       \
         const float4_t tm_ = t_ * mq[(j_) & 1];                                               \
         float v_[4];                                                                          \
-        _Pragma("unroll") for (int r_ = 0; r_ < 4; ++r_) v_[r_] = t_[r_] > 0.f ? t_[r_] : tm_[r_]; \
+        _Pragma("unroll") for (int r_ = 0; r_ < 4; ++r_) v_[r_] = act_pick<MX>(t_[r_], tm_[r_]); \
         lo_ = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v_[0], v_[1]}, half2_t)); \
         hi_ = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v_[2], v_[3]}, half2_t)); \
     } while (0)
@@ -464,13 +464,19 @@ void launch_conv3w(const ConvArgs& a, hipStream_t stream)
     const unsigned G = (unsigned)std::min<long>(a.cus, ntm);
     OPK_CHECK_ARG(G <= 1024, "persistent grid exceeds the sink");
     const bool dma_end = dev_switch("CONV3W", 1) != 2;   // 2: DMA right after the barrier (A/B)
+    // (the DMA-after-barrier A/B variant only with the select activation)
+#define OPKW_LAUNCH(BN_, DE_, MX_) \
+    hipLaunchKernelGGL((conv3w_kernel<BN_, DE_, MX_>), dim3(G), dim3(64 * kW_NW), 0, stream, a)
     if (a.cout == 128) {
-        if (dma_end) hipLaunchKernelGGL((conv3w_kernel<128, true>), dim3(G), dim3(64 * kW_NW), 0, stream, a);
-        else hipLaunchKernelGGL((conv3w_kernel<128, false>), dim3(G), dim3(64 * kW_NW), 0, stream, a);
+        if (!dma_end) OPKW_LAUNCH(128, false, false);
+        else if (a.actmax) OPKW_LAUNCH(128, true, true);
+        else OPKW_LAUNCH(128, true, false);
     } else {
-        if (dma_end) hipLaunchKernelGGL((conv3w_kernel<96, true>), dim3(G), dim3(64 * kW_NW), 0, stream, a);
-        else hipLaunchKernelGGL((conv3w_kernel<96, false>), dim3(G), dim3(64 * kW_NW), 0, stream, a);
+        if (!dma_end) OPKW_LAUNCH(96, false, false);
+        else if (a.actmax) OPKW_LAUNCH(96, true, true);
+        else OPKW_LAUNCH(96, true, false);
     }
+#undef OPKW_LAUNCH
     OPK_LAUNCH_CHECK();
 }
 

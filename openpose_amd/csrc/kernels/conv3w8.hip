@@ -52,7 +52,8 @@ constexpr int k8_BM = 512, k8_HR = 688, k8_NW = 8;
 // through a DPP swap, the first row of each window stores it into the pooled image, and after a
 // workgroup barrier the second row's lanes read it back, take the max and store.  The full-size
 // conv output is never written.
-template <int BN, int NB, bool POOL>
+// MX: the activation as max(t, t*m) (ConvArgs::actmax; conv3_dev.h act_pick)
+template <int BN, int NB, bool POOL, bool MX>
 __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a)
 {
     constexpr int NW = k8_NW, BM = k8_BM, HR = k8_HR;
@@ -367,7 +368,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                         float v[4];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
-                            v[r] = t[r] > 0.f ? t[r] : tm[r];
+                            v[r] = act_pick<MX>(t[r], tm[r]);
                             // the column pair's max: lane ^ 1 holds the next position
                             const float o = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
                                 __builtin_bit_cast(int, v[r]), 0xB1, 0xF, 0xF, false));
@@ -425,7 +426,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                     const float4_t tm = t * mq[h];
                     float v[4];
 #pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
+                    for (int r = 0; r < 4; ++r) v[r] = act_pick<MX>(t[r], tm[r]);
                     pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
                     pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
                 }
@@ -506,8 +507,13 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
     // a multiple of the n-block count (each block keeps one n-block)
     const unsigned G = (unsigned)(std::min<long>(a.cus / nb, ntm) * nb);
     OPK_CHECK_ARG(G >= 1 && G <= 1024, "persistent grid exceeds the sink");
-#define OPK8_LAUNCH(BN_, NB_, P_) \
-    hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_>), dim3(G), dim3(64 * k8_NW), 0, stream, a)
+#define OPK8_LAUNCH(BN_, NB_, P_)                                                                \
+    do {                                                                                        \
+        if (a.actmax)                                                                           \
+            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, true>), dim3(G), dim3(64 * k8_NW), 0, stream, a); \
+        else                                                                                    \
+            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, false>), dim3(G), dim3(64 * k8_NW), 0, stream, a); \
+    } while (0)
     if (pool) {
         if (nb == 4) OPK8_LAUNCH(128, 4, true);
         else if (nb == 2) OPK8_LAUNCH(128, 2, true);

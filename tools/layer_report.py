@@ -7,6 +7,7 @@ conv1_fused_kernel launch stands for conv1_1 + conv1_2 + pool1_stage1, a conv_he
 stage's Mconv6 + Mconv7.
 """
 import csv
+import re
 import sys
 
 sys.path.insert(0, '.')
@@ -62,7 +63,8 @@ for r in fw:
             continue
         fl = flops(l, lvl)
         key = (l['num_output'], l['kernel_size'], lvl)
-        pooled = 'true>' in name and 'conv3w8' in name   # conv3w8 POOL: the next pool ran inside
+        m8 = re.search(r'conv3w8_kernel<\d+, \d+, (true|false)', name)
+        pooled = bool(m8) and m8.group(1) == 'true'   # conv3w8 POOL: the next pool ran inside
         if pooled:
             key = ('N=%4d k=%d lvl=%d +pool' % key, 3, lvl)
         if per_layer:
