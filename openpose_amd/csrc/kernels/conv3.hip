@@ -792,9 +792,10 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
         if (aligned && nn == 1 && dev_switch("CONV3W", 1) != 0 && conv3w_supported(a)) {
             // 8 waves of 64 x 128 (conv3w8.hip, bit-identical): 25 % fewer LDS fragment reads,
             // measured 2-4 % faster from cin 384 up and 4 % slower at cin 128 (tile transitions
-            // weigh more there); CONV3W8=0 disables, 2 forces it
+            // weigh more there); CONV3W8=0 disables, 2 forces it for 128 outputs, 3 also for 96
             const int w8 = dev_switch("CONV3W8", 1);
-            if (w8 != 0 && conv3w8_supported(a) && a.cout == 128 && (a.cin_pad >= 384 || w8 == 2)) {
+            if (w8 != 0 && conv3w8_supported(a) &&
+                ((a.cout == 128 && (a.cin_pad >= 384 || w8 >= 2)) || (a.cout == 96 && w8 == 3))) {
                 launch_conv3w8(a, stream);
                 return;
             }

@@ -36,7 +36,8 @@ constexpr int k8_BM = 512, k8_HR = 688, k8_NW = 8;
 #ifndef OPK8_ABLATE   // dev probe only (tools/conv3w_probe.hip): 1 no mid-unit barrier, 2 no MFMAs,
 #define OPK8_ABLATE 0  // 3 no fragment reads, 4 no DMA after the prologue, 5 no MFMAs in tap 1 of
                        // each unit (a third fewer, replaced by VALU adds), 6 the same with nothing
-                       // issued in their place (timing only, wrong results)
+                       // issued in their place, 7 no halo DMA / 8 no weight DMA after the
+                       // prologue (timing only, wrong results)
 #endif
 #if OPK8_ABLATE == 3
 #define OPK8_DSR(dst_, addr_, off_) asm volatile("; no read %1" : "=v"(dst_) : "v"(addr_))
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     } while (0)
 #define OPK8_ISSUE(c_, ky_, aslot_, bslot_, nt_)                                              \
     do {                                                                                      \
-        if ((ky_) == 0) {                                                                     \
+        if ((ky_) == 0 && (OPK8_ABLATE != 7 || !dma_ab)) {                                    \
             const int as_ = (aslot_) * ASLOT;                                                 \
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
                 if (API % NW == 0 || i_ * NW + wave < API)                                    \
@@ -144,7 +145,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         const int bs_ = 2 * ASLOT + (bslot_) * BSLOT;                                         \
         const uint16_t* ub_ = a.w + (size_t)(ublk + (c_) * 3 + (ky_)) * BROWS * 32;                  \
         _Pragma("unroll") for (int j_ = 0; j_ < BIW; ++j_)                                    \
-            if (BPI % NW == 0 || j_ * NW + wave < BPI) {                                      \
+            if ((BPI % NW == 0 || j_ * NW + wave < BPI) && (OPK8_ABLATE != 8 || !dma_ab)) {   \
                 const int bo_ = OPK8_BOFF(j_);                                                \
                 __builtin_amdgcn_global_load_lds(                                             \
                     (const void*)(ub_ + bo_),                                                 \
@@ -247,8 +248,11 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
 
     // ---- prologue: units 0 and 1 of the first tile in flight, unit 0 visible, tap 0 read ------
     OPK8_AROW(aoff, m);
+    bool dma_ab = false;   // (dev ablations 7 / 8: set after the prologue)
     OPK8_ISSUE(0, 0, 0, 0, false);
     OPK8_ISSUE(0, 1, 0, 1, false);
+    dma_ab = true;
+    (void)dma_ab;
     vm_wait_rt(bi);
     __builtin_amdgcn_s_barrier();
     {
