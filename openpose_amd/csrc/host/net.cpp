@@ -608,6 +608,8 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
                 h.out32 = b.out32;
                 h.out32_c = b.out32_c;
                 h.out32_coff = b.out32_coff;
+                // persistent grid (HEAD_PERSIST=0: one workgroup per tile, dev A/B)
+                h.cus = dev_switch("HEAD_PERSIST", 1) != 0 ? a.cus : 0;
                 launch_conv_head(h, st);
                 ++si;   // Mconv7 ran inside
                 continue;

@@ -17,6 +17,9 @@
 //   phase 3  the N1/128 partial products of a position block (one per wave column) are summed
 //            through LDS in a fixed order (deterministic), + bias, fp16 into every concat slice and
 //            the fp32 NCHW net output when requested.
+// PERSIST: one workgroup per CU walks tiles (XCD-aware order): no workgroup turnover, the bias
+// read once; the next tile's first two K steps are issued into the ring (which the partials
+// alias) as soon as every wave has read its partial sums and issued its stores.
 // MFMA f32_16x16x32_f16, C^T arrangement (weights as the A operand) as in conv3.hip.
 #include "conv.h"
 
@@ -33,7 +36,7 @@ using namespace conv3dev;
 
 constexpr int kH_BM = 128, kH_NW = 8;
 
-template <int N1, int NF2>
+template <int N1, int NF2, bool PERSIST>
 __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs a)
 {
     constexpr int NW = kH_NW, BM = kH_BM;
@@ -59,7 +62,15 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     const int r16 = lane & 15, q = lane >> 4;
     const int Hp = a.H + 2, Wp = a.W + 2;
     const int total = a.frames * Hp * Wp;
-    const int p0 = blockIdx.x * BM;
+    const int ntiles = (total + BM - 1) / BM;
+    // tile order: blockIdx.x, or (PERSIST) the XCD-aware bijection of conv3w.hip, G apart
+    const int G = gridDim.x;
+    int tile = blockIdx.x;
+    if constexpr (PERSIST) {
+        const int xcd = blockIdx.x & 7, qq = G >> 3, rr = G & 7;
+        tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (blockIdx.x >> 3);
+        if (tile >= ntiles) return;
+    }
 
     for (int i = tid; i < N1; i += 64 * NW) {
         const float neg = a.act6 == 1 ? 0.f : 1.f;
@@ -74,8 +85,8 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     // A DMA: instruction `wave` covers tile rows wave*16 .. +15 (positions past the end read the
     // zeroed guard after the last frame, conv.h kConvGuardTail)
     const int arow = wave * 16 + lrow;
-    const uint16_t* asrc = a.in + a.in_coff + (size_t)(p0 + arow) * a.in_cs +
-                           (phys ^ (((arow >> 2) & 1) << 1)) * 8;
+#define OPKH_ASRC(p0_) (a.in + a.in_coff + (size_t)((p0_) + arow) * a.in_cs + (phys ^ (((arow >> 2) & 1) << 1)) * 8)
+    const uint16_t* asrc = OPKH_ASRC(tile * BM);
 #define OPKH_ISSUE(s_)                                                                        \
     do {                                                                                      \
         const int sl_ = (s_) % 3;                                                             \
@@ -92,16 +103,26 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         }                                                                                     \
     } while (0)
 
+    OPKH_ISSUE(0);
+    if (KS > 1) OPKH_ISSUE(1);
+    for (;;) {
+    const int p0 = tile * BM;
+    // lane terms re-derived per tile (opaque): nothing lane-dependent is hoisted out of the tile
+    // loop and kept live through phase 2's registers
+    int lane_t = lane;
+    asm volatile("" : "+v"(lane_t));
+    const int r16 = lane_t & 15, q = lane_t >> 4, lrow = lane_t >> 2, phys = lane_t & 3;
+    const int arow = wave * 16 + lrow;
+    (void)arow;
     float4_t acc[MF][NF];
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
         for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
-    OPKH_ISSUE(0);
-    if (KS > 1) OPKH_ISSUE(1);
     for (int s = 0; s < KS; ++s) {
         // own DMA of step s landed once only step s+1's (1 + BIW instructions) may be in flight
+        // (a previous tile's output stores are older)
         if (s + 1 < KS) vm_wait<1 + BIW>();
         else vm_wait<0>();
         __builtin_amdgcn_s_barrier();
@@ -121,7 +142,6 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
             for (int j = 0; j < NF; ++j)
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
-#undef OPKH_ISSUE
 
     // ---- phase 2: activated Mconv6 block -> Mconv7 partial over this wave's 128 channels -------
     // lane (r16, q) of acc[i][j] holds channels wn*128 + 16j + 4q .. +3 of tile row
@@ -134,12 +154,15 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         for (int f = 0; f < NF2; ++f) acc2[i][f] = float4_t{0.f, 0.f, 0.f, 0.f};
     const float* lb = lbias + wn * 128 + 4 * q;
     const float* lm = lmul + wn * 128 + 4 * q;
+    // (read per tile, not hoisted out of the persistent loop into registers it has not got)
+    const uint16_t* w7 = a.w7;
+    asm volatile("" : "+s"(w7));
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         half8_t a7[NF2];
 #pragma unroll
         for (int f = 0; f < NF2; ++f)
-            a7[f] = *reinterpret_cast<const half8_t*>(a.w7 + (size_t)(f * 16 + r16) * N1 + wn * 128 +
+            a7[f] = *reinterpret_cast<const half8_t*>(w7 + (size_t)(f * 16 + r16) * N1 + wn * 128 +
                                                       kb * 32 + q * 8);
         float4_t bq[2], mq[2];
 #pragma unroll
@@ -179,17 +202,32 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         for (int f = 0; f < NF2; ++f)
             part[(wave * WROWS + i * 16 + r16) * PSTRIDE + f * 4 + q] = acc2[i][f];
     __syncthreads();
-    for (int f = wn; f < NF2; f += WN1) {
-        const int ch = f * 16 + 4 * q;   // this lane's 4 output channels
-        if (ch >= a.n2) continue;
-        const float4_t b7 = *reinterpret_cast<const float4_t*>(a.b7 + ch);   // zero-padded to N2P
+    // this lane's sums: output fragments f = wn, wn + WN1, ... of its wave row
+    constexpr int NFO = (NF2 + WN1 - 1) / WN1;
+    float4_t outv[NFO][MF];
+#pragma unroll
+    for (int k = 0; k < NFO; ++k) {
+        const int f = wn + k * WN1;
+        if (f >= NF2) continue;
+        const float4_t b7 = *reinterpret_cast<const float4_t*>(a.b7 + f * 16 + 4 * q);   // zero-padded to N2P
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
             const int row = wm * WROWS + i * 16 + r16;
             float4_t v = part[((wm * WN1) * WROWS + row - wm * WROWS) * PSTRIDE + f * 4 + q];
             for (int w = 1; w < WN1; ++w)
                 v = v + part[((wm * WN1 + w) * WROWS + row - wm * WROWS) * PSTRIDE + f * 4 + q];
-            v = v + b7;
+            outv[k][i] = v + b7;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < NFO; ++k) {
+        const int f = wn + k * WN1;
+        const int ch = f * 16 + 4 * q;   // this lane's 4 output channels
+        if (f >= NF2 || ch >= a.n2) continue;
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+            const int row = wm * WROWS + i * 16 + r16;
+            const float4_t v = outv[k][i];
             const int p = p0 + row;
             if (p >= total) continue;
             const int fr = p / (Hp * Wp), rem = p - fr * Hp * Wp;
@@ -212,6 +250,23 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
             }
         }
     }
+    int next = -1;
+    if constexpr (PERSIST) {
+        // the ring (aliased by the partials) is free once every wave has read its sums: the
+        // next tile's first two K steps (older than nothing but these stores)
+        __syncthreads();
+        next = tile + G;
+        if (next < ntiles) {
+            asrc = OPKH_ASRC(next * BM);
+            OPKH_ISSUE(0);
+            if (KS > 1) OPKH_ISSUE(1);
+        }
+    }
+    if (!PERSIST || next >= ntiles) break;
+    tile = next;
+    }   // tiles
+#undef OPKH_ISSUE
+#undef OPKH_ASRC
 }
 
 }  // namespace
@@ -239,15 +294,26 @@ void launch_conv_head(const HeadArgs& a, hipStream_t stream)
     OPK_CHECK_ARG(a.ndst <= kConvMaxDst, "conv_head: too many destinations");
     const long total = (long)a.frames * (a.H + 2) * (a.W + 2);
     OPK_CHECK_ARG(total < (1L << 30), "conv_head: too many positions");
-    const unsigned G = (unsigned)((total + kH_BM - 1) / kH_BM);
+    const long ntiles = (total + kH_BM - 1) / kH_BM;
+    // persistent at N1 = 512 (one 143 KB workgroup per CU: 4-5 % faster than one workgroup per
+    // tile); at N1 = 256 two per-tile workgroups share a CU and the persistent grid measured
+    // 23 % slower (one per CU) or unchanged-slow (two per CU) -- profiles/round3/head/
+    const bool persist = a.cus > 0 && a.n1 == 512;
+    const unsigned G = (unsigned)(persist ? std::min<long>(a.cus, ntiles) : ntiles);
     const dim3 blk(64 * kH_NW);
+#define OPKH_LAUNCH(N1_, NF2_)                                                                 \
+    do {                                                                                       \
+        if (persist) hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, true>), dim3(G), blk, 0, stream, a); \
+        else hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, false>), dim3(G), blk, 0, stream, a); \
+    } while (0)
     if (a.n1 == 512) {
-        if (a.n2 <= 32) hipLaunchKernelGGL((conv_head_kernel<512, 2>), dim3(G), blk, 0, stream, a);
-        else hipLaunchKernelGGL((conv_head_kernel<512, 4>), dim3(G), blk, 0, stream, a);
+        if (a.n2 <= 32) OPKH_LAUNCH(512, 2);
+        else OPKH_LAUNCH(512, 4);
     } else {
-        if (a.n2 <= 32) hipLaunchKernelGGL((conv_head_kernel<256, 2>), dim3(G), blk, 0, stream, a);
-        else hipLaunchKernelGGL((conv_head_kernel<256, 4>), dim3(G), blk, 0, stream, a);
+        if (a.n2 <= 32) OPKH_LAUNCH(256, 2);
+        else OPKH_LAUNCH(256, 4);
     }
+#undef OPKH_LAUNCH
     OPK_LAUNCH_CHECK();
 }
 
