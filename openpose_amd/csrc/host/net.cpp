@@ -571,6 +571,7 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
         fa.out_coff = 0;
         fa.OH = lh_[1];
         fa.OW = lw_[1];
+        fa.actmax = a.slope01 && b.slope01 && dev_switch("EPI_MAX", 1) != 0;
         launch_conv1_fused(fa, std::min(cus_, std::max(1, dev_switch("GRID_CUS", cus_))), st);
         first = 3;
     }

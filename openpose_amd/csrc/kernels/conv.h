@@ -119,6 +119,7 @@ struct Conv1FusedArgs {
     int act2;
     uint16_t* out;
     int out_cs, out_coff, OH, OW;
+    int actmax;           // both convs' negative-side multipliers in [0, 1] (ConvArgs::actmax)
 };
 bool conv1_fused_supported(int H, int W, int cout1, int cout2);
 void launch_conv1_fused(const Conv1FusedArgs& a, int workgroups, hipStream_t stream);

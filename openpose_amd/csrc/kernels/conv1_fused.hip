@@ -24,6 +24,7 @@
 #include <algorithm>
 
 #include "../common.h"
+#include "conv3_dev.h"
 
 namespace opk {
 
@@ -54,15 +55,16 @@ static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 
 __device__ __forceinline__ int swz64(int row, int piece) { return row * 4 + (piece ^ (((row >> 2) & 1) << 1)); }
 
-__device__ __forceinline__ uint32_t hmax2(uint32_t a, uint32_t b)
+__device__ __forceinline__ uint32_t hmax4(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
 {
-    const half2_t x = __builtin_bit_cast(half2_t, a), y = __builtin_bit_cast(half2_t, b);
-    half2_t r;
-    r[0] = (float)y[0] > (float)x[0] ? y[0] : x[0];   // maxpool2_kernel's comparison
-    r[1] = (float)y[1] > (float)x[1] ? y[1] : x[1];
-    return __builtin_bit_cast(uint32_t, r);
+    const half2_t m = __builtin_elementwise_max(
+        __builtin_elementwise_max(__builtin_bit_cast(half2_t, a), __builtin_bit_cast(half2_t, b)),
+        __builtin_elementwise_max(__builtin_bit_cast(half2_t, c), __builtin_bit_cast(half2_t, d)));
+    return __builtin_bit_cast(uint32_t, m);
 }
 
+// MX: activations as max(t, t*m) (Conv1FusedArgs::actmax, conv3_dev.h act_pick)
+template <bool MX>
 __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs a)
 {
     __shared__ uint4 lds[LDS_BYTES / 16];
@@ -200,7 +202,7 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
                 float v[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const float a_ = t[r] > 0.f ? t[r] : tm[r];
+                    const float a_ = conv3dev::act_pick<MX>(t[r], tm[r]);
                     v[r] = in ? a_ : 0.f;
                 }
                 pk[g][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
@@ -279,7 +281,7 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
                 const float4_t tm = t * m2[j];
                 float v[4];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
+                for (int r = 0; r < 4; ++r) v[r] = conv3dev::act_pick<MX>(t[r], tm[r]);
                 pk[j][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
                 pk[j][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
             }
@@ -307,11 +309,13 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
             const uint4 v1 = *reinterpret_cast<const uint4*>(s0 + TSTRIDE);
             const uint4 v2 = *reinterpret_cast<const uint4*>(s0 + VW * TSTRIDE);
             const uint4 v3 = *reinterpret_cast<const uint4*>(s0 + (VW + 1) * TSTRIDE);
-            // Caffe window order (y, x), (y, x+1), (y+1, x), (y+1, x+1)
-            v0.x = hmax2(hmax2(hmax2(v0.x, v1.x), v2.x), v3.x);
-            v0.y = hmax2(hmax2(hmax2(v0.y, v1.y), v2.y), v3.y);
-            v0.z = hmax2(hmax2(hmax2(v0.z, v1.z), v2.z), v3.z);
-            v0.w = hmax2(hmax2(hmax2(v0.w, v1.w), v2.w), v3.w);
+            // packed fp16 max (v_pk_max_f16): the window's maximum; it may differ from Caffe's
+            // ordered comparison only in the sign of a zero, which no later conv or pool
+            // distinguishes (products of +-0 are zeros, and sums start at +0)
+            v0.x = hmax4(v0.x, v1.x, v2.x, v3.x);
+            v0.y = hmax4(v0.y, v1.y, v2.y, v3.y);
+            v0.z = hmax4(v0.z, v1.z, v2.z, v3.z);
+            v0.w = hmax4(v0.w, v1.w, v2.w, v3.w);
             uint16_t* dst = a.out + (((size_t)f * (a.OH + 2) + oy + 1) * (a.OW + 2) + ox + 1) * a.out_cs +
                             a.out_coff + cg * 8;
             *reinterpret_cast<uint4*>(dst) = v0;
@@ -338,7 +342,8 @@ void launch_conv1_fused(const Conv1FusedArgs& a, int workgroups, hipStream_t str
     const long tiles = (long)a.frames * ((a.W + TC - 1) / TC) * ((a.H + TR - 1) / TR);
     OPK_CHECK_ARG(tiles < (1L << 31), "conv1 fusion: too many tiles");
     const int grid = (int)std::min<long>(tiles, workgroups > 0 ? workgroups : 256);
-    hipLaunchKernelGGL(conv1_fused_kernel, dim3(grid), dim3(NT), 0, stream, a);
+    if (a.actmax) hipLaunchKernelGGL(conv1_fused_kernel<true>, dim3(grid), dim3(NT), 0, stream, a);
+    else hipLaunchKernelGGL(conv1_fused_kernel<false>, dim3(grid), dim3(NT), 0, stream, a);
     OPK_LAUNCH_CHECK();
 }
 
