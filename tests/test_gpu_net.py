@@ -406,3 +406,48 @@ def test_pool_fused_epilogue_bit_identical(ctx):
     np.testing.assert_array_equal(outs["fused"], outs["separate"])
     ref = torch_forward(graph, params, x[:2])
     assert rel_l2(outs["fused"][:2], ref) < SMALL_TOL
+
+
+def test_prelu_slopes_outside_unit_interval(ctx):
+    """The epilogues use max(t, t*m) only when every negative-side multiplier of a conv lies in
+    [0, 1] (ConvArgs::actmax, set per conv from its slopes); trained PReLU slopes may not.  With
+    slopes drawn from [-0.5, 1.5] every conv falls back to the select, through conv1_fused, the
+    persistent stage kernels and the pool-fused conv3w8: the fp32 reference is met and the result
+    equals the EPI_MAX=0 build bit for bit."""
+    L = conv("c1", "image", 64, 3, "prelu") + conv("c2", "c1", 64, 3, "prelu")
+    L.append(dict(name="p1", type="Pooling", bottom=["c2"], top=["p1"], pool="MAX", kernel_size=2, stride=2))
+    L += conv("c3", "p1", 128, 3, "prelu") + conv("c4", "c3", 128, 3, "prelu")
+    L.append(dict(name="p2", type="Pooling", bottom=["c4"], top=["p2"], pool="MAX", kernel_size=2, stride=2))
+    L += conv("c5", "p2", 128, 3, "prelu") + conv("c6", "c5", 96, 3, "prelu") + conv("c7", "c6", 52, 1)
+    L.append(dict(name="net_output", type="Concat", bottom=["c7"], top=["net_output"]))
+    text = prototxt.emit(L)
+    graph = prototxt.parse(text)
+    params = synth.he_weights(graph, seed=41)
+    rng = np.random.default_rng(42)
+    wild = 0
+    for name, (w, b, s) in list(params.items()):
+        if s is not None:
+            s = rng.uniform(-0.5, 1.5, s.shape).astype(np.float32)
+            wild += int(((s < 0) | (s > 1)).any())
+            params[name] = (w, b, s)
+    assert wild >= 5
+    x = rng.uniform(-0.5, 0.5, (2, 3, 368, 656)).astype(np.float32)
+    with tempfile.NamedTemporaryFile("w", suffix=".prototxt", delete=False) as f:
+        f.write(text)
+        path = f.name
+    outs = []
+    try:
+        for sw in ({}, {"EPI_MAX": 0}):
+            with dev_switches(**sw):
+                net = Net(ctx, path)
+                net.set_params(params)
+                net.forward(torch.from_numpy(x).cuda())
+                outs.append(net.output_numpy())
+                net.close()
+    finally:
+        os.unlink(path)
+    ref = torch_forward(graph, params, x)
+    err = rel_l2(outs[0], ref)
+    print("PReLU slopes in [-0.5, 1.5]: rel-L2 %.3e" % err)
+    assert err < SMALL_TOL and ch_ok(outs[0], ref)
+    np.testing.assert_array_equal(outs[0], outs[1])
