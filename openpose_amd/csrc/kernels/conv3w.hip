@@ -124,13 +124,15 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
     int m = tix;
     if (m >= ntm) return;
 
-    // bias and negative-side multiplier (1 none, 0 ReLU, slope PReLU) for the whole launch
+    // bias and negative-side multiplier (1 none, 0 ReLU, slope PReLU) for the whole launch:
+    // loaded into registers here, stored to LDS once the prologue's DMA wait has covered them
+    // (a cold global load no longer delays the first DMA issue)
+    float bias_v = 0.f, mul_v = 0.f;
     if (tid < BN) {
         const float neg = a.act == 1 ? 0.f : 1.f;
-        lbias[tid] = a.bias[tid];
-        lmul[tid] = a.act == 2 ? a.slope[tid] : neg;
+        bias_v = a.bias[tid];
+        mul_v = a.act == 2 ? a.slope[tid] : neg;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     const int lrow = lane >> 2, phys = lane & 3;
     const int cpt = a.cin_pad >> 5;
@@ -253,7 +255,11 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
     OPKW_AROW(aoffn, m + G);
     OPKW_ISSUE(0, 0, 0, 0, false);
     OPKW_ISSUE(0, 1, 0, 1, false);
-    vm_wait_rt(bi);
+    vm_wait_rt(bi);   // (the bias loads are older than unit 0's DMA)
+    if (tid < BN) {
+        lbias[tid] = bias_v;
+        lmul[tid] = mul_v;
+    }
     __builtin_amdgcn_s_barrier();
     OPKW_STAMP(1);
     int tcount = 0;   // (dev probe) tiles done

@@ -97,12 +97,14 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     int m = tix >> LGNB;
     if (m >= ntm) return;
 
+    // bias / negative-side multiplier of the n-block: registers now, LDS after the prologue's
+    // DMA wait (which covers these older loads), so they do not delay the first DMA issue
+    float bias_v = 0.f, mul_v = 0.f;
     if (tid < BN) {
         const float neg = a.act == 1 ? 0.f : 1.f;
-        lbias[tid] = a.bias[nblk * BN + tid];
-        lmul[tid] = a.act == 2 ? a.slope[nblk * BN + tid] : neg;
+        bias_v = a.bias[nblk * BN + tid];
+        mul_v = a.act == 2 ? a.slope[nblk * BN + tid] : neg;
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
     const int lrow = lane >> 2, phys = lane & 3;
     const int cpt = a.cin_pad >> 5;
@@ -254,6 +256,10 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     dma_ab = true;
     (void)dma_ab;
     vm_wait_rt(bi);
+    if (tid < BN) {
+        lbias[tid] = bias_v;
+        lmul[tid] = mul_v;
+    }
     __builtin_amdgcn_s_barrier();
     {
         const uint32_t bb0 = OPK8_BBASE(0);
