@@ -175,7 +175,7 @@ const Context::WarpAxes& Context::warp_axis_tables(double scale, int dw, int dh)
 }
 
 void cvmat_to_input(Context* ctx, float* dst, const uint8_t* src, int n, int sw, int sh,
-                    size_t step, double scale, int dw, int dh, int normalize)
+                    size_t step, double scale, int dw, int dh, int normalize, hipStream_t stream)
 {
     OPK_CHECK_ARG(dst && src, "NULL buffer");
     OPK_CHECK_ARG(n > 0 && sw > 0 && sh > 0 && dw > 0 && dh > 0, "empty frame or net input");
@@ -188,7 +188,7 @@ void cvmat_to_input(Context* ctx, float* dst, const uint8_t* src, int n, int sw,
     const short* w = ctx->warp_weight_table(cubic);
     const auto& ax = ctx->warp_axis_tables(scale, dw, dh);
     launch_cvmat_to_input(dst, src, n, sh, sw, step ? step : (size_t)sw * 3, dh, dw, ax.x, ax.y, w,
-                          cubic ? 4 : 2, normalize, ctx->stream);
+                          cubic ? 4 : 2, normalize, stream ? stream : ctx->stream);
 }
 
 }  // namespace opk

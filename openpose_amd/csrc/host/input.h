@@ -1,5 +1,6 @@
 // input.h -- frame -> net input: ScaleAndSizeExtractor + CvMatToOpInput (internal).
 #pragma once
+#include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
 
@@ -24,7 +25,8 @@ void warp_axis_table(double scale, int d, bool cubic, int* tab /* 2*d */);
 // op::CvMatToOpInput::createArray for one scale (cvMatToOpInput.cpp:63-98), a batch of n frames:
 // src BGR uint8 [n][sh][step bytes] on device -> dst [n][3][dh][dw] fp32 on device
 // (resizeFixedAspectRatio + uCharCvMatToFloatPtr with the VGG normalisation when normalize != 0).
+// (stream: where the warp runs; nullptr = the context's stream)
 void cvmat_to_input(Context* ctx, float* dst, const uint8_t* src, int n, int sw, int sh,
-                    size_t step, double scale, int dw, int dh, int normalize);
+                    size_t step, double scale, int dw, int dh, int normalize, hipStream_t stream = nullptr);
 
 }  // namespace opk

@@ -59,6 +59,12 @@ PoseHip::~PoseHip()
         (void)hipStreamSynchronize(ctx_->stream);
         (void)hipStreamDestroy(copy_);
     }
+    if (warp_) {
+        (void)hipStreamSynchronize(warp_);
+        (void)hipStreamDestroy(warp_);
+        (void)hipEventDestroy(warp_done_);
+        (void)hipEventDestroy(nets_done_);
+    }
     for (auto& s : slots_)
         if (s.done) (void)hipEventDestroy(s.done);
     for (auto& st : scale_streams_)
@@ -201,6 +207,7 @@ void PoseHip::submit(const float* frames, int n, int net_h, int net_w, int prod_
     OPK_CHECK_ARG(net_ != nullptr, "no network: use forward_net_output (poseNetOutput path)");
     OPK_CHECK_ARG(count_ < 2, "two batches already in flight: collect first");
     net_->forward(frames, n, net_h, net_w);
+    mark_nets_done();
     submit_net_output(net_->output(), n, net_->out_h(), net_->out_w(), net_h, net_w, prod_w,
                       prod_h);
 }
@@ -229,14 +236,32 @@ void PoseHip::submit_frames(const uint8_t* frames, int n, int w, int h, size_t s
     scale_and_size(w, h, in_net_w_, in_net_h_, dyn_, scale_number_, scale_gap_, scales, input_hw_);
     const float* ptrs[kMaxResizeSources];
     int hw[2 * kMaxResizeSources];
+    // the warps run on their own stream after the previous batch's nets (the readers of these
+    // input buffers), i.e. beside that batch's post-processing; the nets wait for them
+    const bool side = dev_switch("WARP_STREAM", 1) != 0;
+    if (side && !warp_) {
+        ctx_->bind();
+        OPK_HIP(hipStreamCreateWithFlags(&warp_, hipStreamNonBlocking));
+        OPK_HIP(hipEventCreateWithFlags(&warp_done_, hipEventDisableTiming));
+        OPK_HIP(hipEventCreateWithFlags(&nets_done_, hipEventDisableTiming));
+    }
+    hipStream_t ws = side ? warp_ : ctx_->stream;
+    if (side) {
+        // (no batch recorded yet: everything queued on the context stream so far)
+        if (!nets_recorded_) OPK_HIP(hipEventRecord(nets_done_, ctx_->stream));
+        OPK_HIP(hipStreamWaitEvent(warp_, nets_done_, 0));
+    }
     for (int i = 0; i < scale_number_; ++i) {
         const int nw = input_hw_[2 * i], nh = input_hw_[2 * i + 1];
         float* x = static_cast<float*>(inputs_[i].get((size_t)n * 3 * nh * nw * sizeof(float)));
-        // the net of the previous batch read this buffer earlier on the same stream
-        cvmat_to_input(ctx_, x, frames, n, w, h, step, scales[i], nw, nh, 1);
+        cvmat_to_input(ctx_, x, frames, n, w, h, step, scales[i], nw, nh, 1, ws);
         ptrs[i] = x;
         hw[2 * i] = nh;
         hw[2 * i + 1] = nw;
+    }
+    if (side) {
+        OPK_HIP(hipEventRecord(warp_done_, warp_));
+        OPK_HIP(hipStreamWaitEvent(ctx_->stream, warp_done_, 0));
     }
     inputs_n_ = n;
     for (int i = 0; i < scale_number_; ++i) map_ratios_[i] = (float)scales[i];
@@ -316,7 +341,16 @@ void PoseHip::submit_multi(const float* const* frames, const int* net_hw, int ns
         for (int i = 1; i < nscales; ++i) OPK_HIP(hipStreamWaitEvent(s, join_[i - 1], 0));
         net_->time_end(s);
     }
+    mark_nets_done();
     submit_outputs(outs.data(), nscales, n, net_hw[0], net_hw[1], prod_w, prod_h);
+}
+
+void PoseHip::mark_nets_done()
+{
+    // the nets of this batch have read their inputs: the next batch's warps may overwrite them
+    if (!warp_) return;
+    OPK_HIP(hipEventRecord(nets_done_, ctx_->stream));
+    nets_recorded_ = true;
 }
 
 void PoseHip::submit_net_output(const float* net_out, int n, int oh, int ow, int net_h,

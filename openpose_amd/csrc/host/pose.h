@@ -118,6 +118,12 @@ private:
     const float* overlay_ = nullptr;
     float upsampling_ = 0.f;
     hipStream_t copy_ = nullptr;         // D2H of collected batches (overlaps the next batch)
+    // raw-frame path: the warp of batch i+1 runs on its own stream once the nets of batch i are
+    // done with the net inputs, beside batch i's post-processing (WARP_STREAM=0: in order)
+    hipStream_t warp_ = nullptr;
+    hipEvent_t warp_done_ = nullptr, nets_done_ = nullptr;
+    bool nets_recorded_ = false;
+    void mark_nets_done();
     // multi-scale: the nets of scales 1.. run on their own streams beside scale 0's
     hipStream_t scale_streams_[kMaxResizeSources - 1] = {};
     hipEvent_t fork_ = nullptr, join_[kMaxResizeSources - 1] = {};
