@@ -125,6 +125,15 @@ def cpu_baseline(args, params, frames_np, overlays_np):
                                        "speed.md:21), other hardware"}
 
 
+def host_breakdown(host, steps):
+    """Rank 0's host time in the timed region: per step, the submit call (enqueue), collect (wait
+    for the batch + people assembly) and records (pack + gather push); finish (the ordered gather's
+    unpack on rank 0) once for the whole run."""
+    out = {k: round(v / steps * 1e3, 3) for k, v in host.items() if k != "finish"}
+    out["finish_total"] = round(host.get("finish", 0.0) * 1e3, 3)
+    return out
+
+
 def pmc_traffic(batch):
     """HBM bytes of one CNN forward from the committed rocprofv3 PMC summary (FETCH_SIZE x2 on
     gfx950 + WRITE_SIZE over every kernel of one forward; tools/pmc_summary.py), or None when the
@@ -250,15 +259,24 @@ def rank_main(args, rank, world, local):
     rec_buf = np.empty(cap, np.float32)
     collected = [0]
 
+    host = {"submit": 0.0, "collect": 0.0, "records": 0.0}   # host seconds in the timed steps
+
     def collect(timed):
+        c0 = time.perf_counter()
         pose.collect()
         if timed:
+            c1 = time.perf_counter()
             i = collected[0]
             gather.push(i, (i * world + rank) * B, B, pose.records(rec_buf))
             collected[0] += 1
+            host["collect"] += c1 - c0
+            host["records"] += time.perf_counter() - c1
 
     def step(i, timed):
+        s0 = time.perf_counter()
         pose.submit_frames(frames[i % 2])
+        if timed:
+            host["submit"] += time.perf_counter() - s0
         if pose.pending() > 1:
             collect(timed)
 
@@ -283,7 +301,9 @@ def rank_main(args, rank, world, local):
     for i in range(args.steps):
         step(i, True)
     drain(True)
+    f0 = time.perf_counter()
     ordered = gather.finish(PARTS)        # rank 0: every frame's record, in frame order
+    host["finish"] = time.perf_counter() - f0
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -371,6 +391,7 @@ def rank_main(args, rank, world, local):
             "frac_of_measured_random_operand_mfma": round(achieved / peaks["mfma_fp16_random_tflops"], 4),
         },
         "post_roofline": post_roofline(B, post_ms) if nscales == 1 else None,
+        "host_ms": host_breakdown(host, args.steps),
     }
     if rank == 0 and world == 1 and nscales == 1 and not args.no_cpu_baseline:
         frames_np = frames[0][:2].cpu().numpy()   # uint8 [2][720][1280][3]
@@ -408,15 +429,24 @@ def rank_main_body135(args, rank, world, local):
     rec_buf = np.empty(cap, np.float32)
     collected = [0]
 
+    host = {"submit": 0.0, "collect": 0.0, "records": 0.0}   # host seconds in the timed steps
+
     def collect(timed):
+        c0 = time.perf_counter()
         pose.collect()
         if timed:
+            c1 = time.perf_counter()
             i = collected[0]
             gather.push(i, (i * world + rank) * B, B, pose.records(rec_buf))
             collected[0] += 1
+            host["collect"] += c1 - c0
+            host["records"] += time.perf_counter() - c1
 
     def step(i, timed):
+        s0 = time.perf_counter()
         pose.submit_net_output(net_out[i % 2], (NET_W, NET_H), PRODUCER)
+        if timed:
+            host["submit"] += time.perf_counter() - s0
         if pose.pending() > 1:
             collect(timed)
 
@@ -437,7 +467,9 @@ def rank_main_body135(args, rank, world, local):
     for i in range(args.steps):
         step(i, True)
     drain(True)
+    f0 = time.perf_counter()
     ordered = gather.finish(parts)
+    host["finish"] = time.perf_counter() - f0
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -481,6 +513,7 @@ def rank_main_body135(args, rank, world, local):
             "frames_gathered_in_order": total_frames,
         },
         "roofline": dict(post_roofline(B, post_ms, POST_PMC_B135, post_bytes), traffic=None),
+        "host_ms": host_breakdown(host, args.steps),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle   # the CPU baseline leg only

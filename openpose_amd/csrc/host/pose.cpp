@@ -479,59 +479,52 @@ int PoseHip::collect()
     kp_.assign(n, {});
     ks_.assign(n, {});
     // per-frame compact-record offsets; records longer than the eagerly copied head are fetched
-    // whole, all of them in one round of copies (many-people / BODY_135 frames)
+    // whole below
     std::vector<std::vector<int>> offsets(n);
     std::vector<size_t> over_at(n, (size_t)-1);
-    size_t over_total = 0;
+    int over_first = -1, over_last = -1;
+    size_t over_w = 0;
     for (int f = 0; f < n; ++f) {
         const int total = compact_offsets(m, hp + (size_t)f * peak_floats, kMaxPeaks, offsets[f]);
         OPK_CHECK_ARG((int)hr[(size_t)f * K] == total, "PAF record count differs from the peak counts");
         if ((size_t)total + 1 > K) {
-            over_at[f] = over_total;
-            over_total += (size_t)total + 1;
+            if (over_first < 0) over_first = f;
+            over_last = f;
+            over_w = std::max(over_w, (size_t)total + 1);
         }
     }
-    if (over_total > 0) {
-        float* ho = static_cast<float*>(overflow_.get(over_total * 4));
-        for (int f = 0; f < n; ++f)
-            if (over_at[f] != (size_t)-1)
-                OPK_HIP(hipMemcpyAsync(ho + over_at[f],
-                                       static_cast<const float*>(sl.records.ptr) + (size_t)f * rf,
-                                       ((size_t)hr[(size_t)f * K] + 1) * 4, hipMemcpyDeviceToHost,
-                                       copy_));
+    if (over_first >= 0) {
+        // records longer than the eagerly copied head (many-people / BODY_135 frames): one 2-D
+        // copy of the longest such record's length for the frame range that holds them
+        const size_t rows = (size_t)(over_last - over_first + 1);
+        float* ho = static_cast<float*>(overflow_.get(rows * over_w * 4));
+        OPK_HIP(hipMemcpy2DAsync(ho, over_w * 4,
+                                 static_cast<const float*>(sl.records.ptr) + (size_t)over_first * rf,
+                                 rf * 4, over_w * 4, rows, hipMemcpyDeviceToHost, copy_));
+        for (int f = over_first; f <= over_last; ++f)
+            if ((int)hr[(size_t)f * K] + 1 > (int)K) over_at[f] = (size_t)(f - over_first) * over_w;
         OPK_HIP(hipStreamSynchronize(copy_));
     }
-    // people assembly: frames are independent (connectBodyParts* per frame), so they run on up
-    // to kAssemblyThreads host threads; every frame's result is the single-threaded one
+    // people assembly: frames are independent (connectBodyParts* per frame), so they run on the
+    // pool's kAssemblyThreads host threads; every frame's result is the single-threaded one
+    if (!pool_ && n > 1) {
+        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+        pool_ = std::make_unique<WorkerPool>((int)std::min<unsigned>(kAssemblyThreads, hw));
+    }
+    const int workers = pool_ ? pool_->workers() : 1;
+    if ((int)scratch_.size() < workers) scratch_.resize(workers);
     const float* ho = static_cast<const float*>(overflow_.ptr);
-    auto frame = [&](int f) {
+    auto frame = [&](int f, int worker) {
         PairScores ps;
         ps.data = (over_at[f] != (size_t)-1 ? ho + over_at[f] : hr + (size_t)f * K) + 1;
         ps.compact = true;
         ps.offsets = offsets[f].data();
         people_[f] = assemble_people(m, hp + (size_t)f * peak_floats, kMaxPeaks, ps, cp, kp_[f],
-                                     ks_[f]);
+                                     ks_[f], &scratch_[worker]);
     };
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    const int T = (int)std::min<unsigned>({(unsigned)n, (unsigned)kAssemblyThreads, hw});
-    if (T <= 1) {
-        for (int f = 0; f < n; ++f) frame(f);
-    } else {
-        std::vector<std::exception_ptr> err(T);
-        std::vector<std::thread> pool;
-        pool.reserve(T);
-        for (int t = 0; t < T; ++t)
-            pool.emplace_back([&, t] {
-                try {
-                    for (int f = t; f < n; f += T) frame(f);
-                } catch (...) {
-                    err[t] = std::current_exception();
-                }
-            });
-        for (auto& th : pool) th.join();
-        for (auto& e : err)
-            if (e) std::rethrow_exception(e);
-    }
+    if (pool_) pool_->run(n, frame);
+    else
+        for (int f = 0; f < n; ++f) frame(f, 0);
     head_ = (head_ + 1) & 1;
     --count_;
     last_ = si;

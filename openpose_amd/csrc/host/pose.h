@@ -1,10 +1,12 @@
 // pose.h -- PoseHip: the op::PoseExtractorCaffe::forwardPass replacement for a batch of frames.
 #pragma once
+#include <memory>
 #include <vector>
 
 #include "connector.h"
 #include "context.h"
 #include "net.h"
+#include "pool.h"
 
 namespace opk {
 
@@ -132,6 +134,10 @@ private:
     Slot slots_[2];
     int head_ = 0, count_ = 0, last_ = -1;
     HostBuf overflow_;                   // records longer than kRecordHead (pinned)
+    // people assembly: worker threads (started by the first multi-frame collect) and one
+    // scratch per worker
+    std::unique_ptr<WorkerPool> pool_;
+    std::vector<AssemblyScratch> scratch_;
 
     float scale_net_to_output_ = 1.f;
     int n_ = 0, hh_ = 0, hw_ = 0;

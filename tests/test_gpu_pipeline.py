@@ -286,6 +286,39 @@ def test_pose_injection_gpu_semantics(ctx, model, people):
         np.testing.assert_array_equal(ks, rs)
 
 
+def test_pose_injection_mixed_record_lengths(ctx):
+    """One BODY_135 batch whose frames' PAF records are longer than the eagerly copied head
+    (kRecordHead floats: 20+ people) and shorter (0-3 people) in alternation: the long records come
+    over in one 2-D copy spanning short frames too, the frames are assembled by the worker pool in
+    any order; every frame bit-exact against the oracle chain, over two batches in flight."""
+    t = oracle.pose_tables()[BODY_135]
+    C = t["parts"] + int(t["bkg"]) + len(t["map_idx"])
+    people = [1, 20, 0, 25, 3, 20]
+    fields = np.stack([synth.overlay(p, 46, 82, seed=4100 + k, table=t) +
+                       np.random.default_rng(k).normal(0, 0.01, (C, 46, 82)).astype(np.float32)
+                       for k, p in enumerate(people)]).astype(np.float32)
+    pose = PoseExtractor(ctx, None, pose_model=BODY_135, semantics=CONNECT_GPU)
+    order = [np.arange(len(people)), np.arange(len(people))[::-1]]
+    devs = [_dev(np.ascontiguousarray(fields[o])) for o in order]
+    for d in devs:
+        pose.submit_net_output(d, (656, 368), (1280, 720))
+    ref = {}
+    for o in order:
+        pose.collect()
+        s = pose.scale_net_to_output()
+        off = float(np.float32(0.5 / np.float64(s)))
+        for k, src in enumerate(o):
+            if src not in ref:
+                heat = oracle.resize_merge([fields[src]], 368, 656)
+                peaks = oracle.nms(heat, 0.05, 128, (off, off), channels=t["parts"])
+                ps = oracle.pair_scores_table(heat, peaks, t)
+                ref[src] = oracle.connect_gpu_semantics(ps, peaks, t, scale=s)
+            kp, ks = pose.keypoints(k)
+            np.testing.assert_array_equal(kp, ref[src][0])
+            np.testing.assert_array_equal(ks, ref[src][1])
+            assert (len(kp) > 0) == (people[src] > 0)
+
+
 def _multiscale_case(ctx, nscales, gap, seed, nms_stream=1):
     """--scale_number nscales --scale_gap gap through opk_pose_forward_multi, sizes from
     ScaleAndSizeExtractor (scaleAndSizeExtractor.cpp:74-88); merged heat maps (resizeAndMergeCpu
