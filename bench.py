@@ -53,10 +53,11 @@ POST_BYTES_FRAME = 100_675_360
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--batch", type=int, default=64,
-                    help="frames per step per GPU (throughput mode; DESIGN.md §5 lists 16 too)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="frames per step per GPU (throughput mode); 0: tile-aligned (body25 / "
+                         "multiscale: tile_aligned_batch, 130 on a 256-CU MI355X), 64 for body135")
     ap.add_argument("--config", choices=["body25", "multiscale", "body135"], default="body25",
                     help="body25: BASELINE configs[1]/[2]; multiscale: configs[3] (4 scales); "
                          "body135: configs[4] (BODY_135 net-output injection, 20 people)")
@@ -67,6 +68,17 @@ def parse():
     ap.add_argument("--dev", action="append", default=[], metavar="KEY=VAL",
                     help="kernel-variant switch for A/B runs (opk_dev_set; include/opk.h)")
     return ap.parse_args()
+
+
+def tile_aligned_batch(cus, rounds=4):
+    """Frames per step that fill whole rounds of 512-position conv tiles at the 1/8-resolution
+    level, where 91 of the 3x3 layers run one persistent workgroup per CU: the padded 48 x 84
+    image of 46 x 82 is 4,032 positions per frame, so 4 x 256 x 512 // 4032 = 130 frames make
+    1,024 tiles = 4 per CU (64 frames make 504: 8 CUs idle in the second round; 66 make 520:
+    a third round for 8 CUs, -12 %).  Measured in one call (profiles/round3/batch/): 3,551 /
+    3,591 / 3,139 / 3,612 / 3,625 frames/s at 64 / 65 / 66 / 128 / 130 frames."""
+    ppf = (NET_H // 8 + 2) * (NET_W // 8 + 2)
+    return max(1, rounds * cus * 512 // ppf)
 
 
 def cpu_model():
@@ -150,8 +162,9 @@ def pmc_traffic(batch):
 
 
 # per-step PMC counts of the post-processing kernels (overlay add, NMS detect + finalize, PAF
-# integrals) at 64 frames, from the committed rocprofv3 summary (tools/pmc_round.sh + pmc_report.py)
-POST_PMC = os.path.join(ROOT, "profiles", "round3", "pmc_head_r3f", "report.json")
+# integrals) from the committed rocprofv3 summary (tools/pmc_round.sh + pmc_report.py; its "batch"
+# must equal the bench's frames per step)
+POST_PMC = os.path.join(ROOT, "profiles", "round3", "pmc_r3g", "report.json")
 POST_PMC_B135 = os.path.join(ROOT, "profiles", "round3", "pmc_body135", "report.json")
 VALU_PEAK_GINSTS = 1024 * 0.5 * 2.4   # wave64 VALU instructions: 1 per 2 cycles per SIMD-32, 2.4 GHz
 
@@ -176,7 +189,12 @@ def post_roofline(batch, post_ms, pmc_path=POST_PMC, ref_bytes_frame=POST_BYTES_
             pmc = json.load(f)["post_step"]
     except (OSError, ValueError, KeyError):
         pmc = None
-    if pmc is None or batch != 64:
+    try:
+        with open(pmc_path) as f:
+            pmc_batch = json.load(f).get("batch", 64)
+    except (OSError, ValueError):
+        pmc_batch = None
+    if pmc is None or batch != pmc_batch:
         out.update({"bound": None, "achieved": None, "peak": None, "unit": None, "frac": None,
                     "note": "no PMC summary for this batch size"})
         return out
@@ -231,7 +249,7 @@ def rank_main(args, rank, world, local):
     net.set_params(params)
     pose = PoseExtractor(ctx, net)
 
-    B = args.batch
+    B = args.batch or tile_aligned_batch(torch.cuda.get_device_properties(local).multi_processor_count)
     nscales = 4 if args.config == "multiscale" else 1
     gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     W_IN, H_IN = PRODUCER
@@ -414,7 +432,7 @@ def rank_main_body135(args, rank, world, local):
     t = pose_model_info(BODY_135)   # the library's tables (generated from poseParameters.cpp)
     C = t["parts"] + int(t["bkg"]) + len(t["map_idx"])   # 439
     H8, W8 = NET_H // 8, NET_W // 8
-    B = args.batch
+    B = args.batch or 64   # no CNN in this config: no tile alignment
     distinct = 8
     fields = np.stack([synth.overlay(people, H8, W8, seed=7000 * rank + k, table=t) +
                        np.random.default_rng(k).normal(0, 0.01, (C, H8, W8)).astype(np.float32)

@@ -1,6 +1,6 @@
 """Per-kernel PMC summary of tools/pmc_round.sh passes (rocprofv3 --pmc, one pass per counter set).
 
-    python tools/pmc_report.py <pass dir>... [--json out.json]
+    python tools/pmc_report.py <pass dir>... [--json out.json] [--batch FRAMES]
 
 Per kernel (mean per launch): duration, effective clock (GRBM_GUI_ACTIVE / 8 XCDs / duration),
 MFMA busy (SQ_VALU_MFMA_BUSY_CYCLES over 1024 SIMDs x the cycles the launch ran), wave time parked
@@ -81,8 +81,10 @@ def summarise(vals, durs):
 def main():
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
     js = sys.argv[sys.argv.index("--json") + 1] if "--json" in sys.argv else None
-    if js in args:
-        args.remove(js)
+    batch = int(sys.argv[sys.argv.index("--batch") + 1]) if "--batch" in sys.argv else 64
+    for x in (js, str(batch)):
+        if x in args:
+            args.remove(x)
     vals, durs = load(args)
     ks = summarise(vals, durs)
     conv = {k: e for k, e in ks.items() if ("conv" in k and "kernel" in k) or "maxpool" in k}
@@ -96,7 +98,7 @@ def main():
     step = {"valu_insts": sum(e.get("valu_insts", 0.0) for e in post.values()),
             "hbm_bytes": sum(e.get("hbm_bytes", 0.0) for e in post.values()),
             "kernel_us": sum(e["mean_us"] for e in post.values())}
-    res = {"valu_peak_insts_per_s": VALU_PEAK,
+    res = {"batch": batch, "valu_peak_insts_per_s": VALU_PEAK,
            "cnn": {"conv_kernel_us_profiled": tot,
                    "time_weighted_mfma_busy": busy / tot if tot else None},
            "post_step": step, "post_kernels": post, "kernels": ks}

@@ -13,4 +13,8 @@ for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE
   i=$((i+1))
   timeout -s KILL 120 rocprofv3 --pmc $set --output-format csv -d $out/p$i -o run -- $B > $out/p$i.log 2>&1 || exit 1
 done
-python tools/pmc_report.py $out/p1 $out/p2 $out/p3 $out/p4 --json $out/report.json > $out/report.txt 2>&1
+# frames per step of the profiled run (bench.py's default unless --batch is passed)
+batch=$(python -c "import sys; a=sys.argv[1:]; print(a[a.index('--batch')+1] if '--batch' in a else '')" "$@")
+[ -z "$batch" ] && batch=$(python -c "import torch, bench; print(bench.tile_aligned_batch(torch.cuda.get_device_properties(0).multi_processor_count))")
+python tools/pmc_report.py $out/p1 $out/p2 $out/p3 $out/p4 --json $out/report.json --batch $batch > $out/report.txt 2>&1 &&
+python tools/pmc_summary.py $out/p3/run_counter_collection.csv $out/p4/run_counter_collection.csv $batch $out/pmc_traffic.json > $out/pmc_traffic.log 2>&1
