@@ -526,7 +526,9 @@ def rank_main_body135(args, rank, world, local):
                         "+ PAF integrals + connectBodyPartsGpu assembly + ordered gather" % people,
             "frames_per_step_per_gpu": B,
             "heatmaps": [C, NET_H, NET_W],
-            "parallelism": "frame-parallel replicas x%d (one process per GPU)" % world,
+            "parallelism": ("frame-parallel replicas x%d (one process per GPU, RCCL ordered "
+                            "gather of per-frame records to rank 0)" % world) if comm_dev == "cuda"
+                           else "REHEARSAL x%d: every rank on GPU 0, gloo gather" % world,
             "people_per_frame_found": found,
             "frames_gathered_in_order": total_frames,
         },
