@@ -44,6 +44,8 @@ struct ConvArgs {
     int actmax;           // conv3w / conv3w8: every negative-side multiplier (1 none, 0 ReLU, the
                           // PReLU slopes) lies in [0, 1], so t > 0 ? t : t*m == max(t, t*m) for
                           // every finite t (the epilogue's 2 VALU per value become 1); set by the host
+    int bufst;            // conv3w: one destination whose extent is < 2^31 bytes -- epilogue stores
+                          // through a buffer resource (set by launch_conv3w)
     int pool;             // conv3w8: 2x2/2 max pool fused into the epilogue; dst[0] is the pooled
                           // padded image [frames][H/2+2][W/2+2][cs] (conv3w8_pool_supported)
 };

@@ -116,6 +116,27 @@ __device__ __forceinline__ float act_pick(float t, float tm)
     return MX ? __builtin_fmaxf(t, tm) : (t > 0.f ? t : tm);
 }
 
+// the same on a fragment's four values, kept as vector operations so that the bias add and the
+// multiply before it stay packed (v_pk_add_f32 / v_pk_mul_f32) instead of being scalarised
+template <bool MX>
+__device__ __forceinline__ float4_t act_pick4(float4_t t, float4_t tm)
+{
+    if constexpr (MX) return __builtin_elementwise_max(t, tm);
+    float4_t r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) r[k] = t[k] > 0.f ? t[k] : tm[k];
+    return r;
+}
+
+// 16-byte / 8-byte buffer stores through a raw buffer resource over a destination slice: lanes
+// whose byte offset is kOOB (>= num_records) are dropped by the range check, so a masked-off lane
+// needs neither a branch nor a sink address, and the address is one 32-bit VGPR per position
+constexpr uint32_t kBufOOB = 0x80000000u;
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t buf_rsrc(const void* base)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, 0x7fffffff, 0x00020000);
+}
+
 #define OPK3_VM_CASE(n_) case n_: vm_wait<n_>(); break;
 __device__ __forceinline__ void vm_wait_rt64(int n)
 {

@@ -77,6 +77,16 @@ __device__ __forceinline__ void opkw_st(uint2* p, const uint2& v)
     else *p = v;
 }
 
+// epilogue buffer stores (conv3_dev.h buf_rsrc: lanes at kBufOOB are dropped)
+__device__ __forceinline__ void opkw_bst(const uint4& v, __amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    __builtin_amdgcn_raw_buffer_store_b128((opkw_u4){v.x, v.y, v.z, v.w}, r, (int)off, 0, 0);
+}
+__device__ __forceinline__ void opkw_bst(const uint2& v, __amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    __builtin_amdgcn_raw_buffer_store_b64((opkw_u2){v.x, v.y}, r, (int)off, 0, 0);
+}
+
 #ifndef OPKW_ABLATE   // dev probe only (tools/conv3w_probe.hip): 1 no mid-unit barrier, 2 no MFMAs,
 #define OPKW_ABLATE 0  // 3 no fragment reads, 4 no DMA after the prologue (timing only, wrong results)
 #endif
@@ -92,7 +102,8 @@ __device__ __forceinline__ void opkw_st(uint2* p, const uint2& v)
 // barrier -- fewer registers live at the issue point (no spills), two thirds of a unit less lead
 // time; measured 2-3 % faster on the stage layers.  CONV3W=2 selects the other placement (A/B).
 // MX: the activation as max(t, t*m) (ConvArgs::actmax; conv3_dev.h act_pick)
-template <int BN, bool DMA_END, bool MX>
+// BST: one destination, epilogue stores through a buffer resource (ConvArgs::bufst)
+template <int BN, bool DMA_END, bool MX, bool BST>
 __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
 {
     constexpr int NW = kW_NW, BM = kW_BM, HR = kW_HR;
@@ -370,11 +381,9 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
 #define OPKW_ACT(i_, j_, lo_, hi_)                                                            \
     do {                                                                                      \
         const float4_t t_ = acc[i_][j_] + bq[(j_) & 1];                                       \
-        const float4_t tm_ = t_ * mq[(j_) & 1];                                               \
-        float v_[4];                                                                          \
-        _Pragma("unroll") for (int r_ = 0; r_ < 4; ++r_) v_[r_] = act_pick<MX>(t_[r_], tm_[r_]); \
-        lo_ = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v_[0], v_[1]}, half2_t)); \
-        hi_ = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v_[2], v_[3]}, half2_t)); \
+        const float4_t v_ = act_pick4<MX>(t_, t_ * mq[(j_) & 1]);                             \
+        lo_ = __builtin_bit_cast(uint32_t, __builtin_convertvector(v_.xy, half2_t));          \
+        hi_ = __builtin_bit_cast(uint32_t, __builtin_convertvector(v_.zw, half2_t));          \
     } while (0)
         // destinations: one concat slice (every stage layer but conv4_4_CPM) with its pointer and
         // stride in SGPRs; a loop over the slices otherwise
@@ -384,9 +393,17 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
 #ifndef OPKW_SINK_ONLY   // dev probe: every store to the sink (tile-transition store-burst test)
 #define OPKW_SINK_ONLY 0
 #endif
+        // one destination under 2 GiB (host): buffer stores, masked lanes out of range
+        const __amdgpu_buffer_rsrc_t rs0 = buf_rsrc(d0);
+        uint32_t vrow[MF];
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+            vrow[i] = BST && pok[i] ? (uint32_t)prow[i] * (uint32_t)(cs0 * 2) : kBufOOB;
 #define OPKW_STORE(T_, sink_, ch_, i_, val_)                                                  \
     do {                                                                                      \
-        if (nd == 1) {                                                                        \
+        if constexpr (BST) {                                                                  \
+            opkw_bst(val_, rs0, vrow[i_] + (ch_) * 2);                                        \
+        } else if (nd == 1) {                                                                 \
             T_* p_ = reinterpret_cast<T_*>(d0 + (ch_) + (size_t)prow[i_] * cs0);              \
             opkw_st(pok[i_] && !OPKW_SINK_ONLY ? p_ : sink_, val_);                           \
         } else {                                                                              \
@@ -470,9 +487,20 @@ void launch_conv3w(const ConvArgs& a, hipStream_t stream)
     const unsigned G = (unsigned)std::min<long>(a.cus, ntm);
     OPK_CHECK_ARG(G <= 1024, "persistent grid exceeds the sink");
     const bool dma_end = dev_switch("CONV3W", 1) != 2;   // 2: DMA right after the barrier (A/B)
+    // buffer-resource epilogue stores (BUFST=0: pointer stores, A/B): one destination whose
+    // positions x channel stride fit the 31-bit offsets of the raw buffer range check
+    ConvArgs b = a;
+    const long extent = ((long)a.frames * (a.H + 2 * a.border) * (a.W + 2 * a.border) + kConvGuardTail) *
+                        a.dst_cs[0] * 2;
+    b.bufst = a.ndst == 1 && extent < (1L << 31) - 4096 && dev_switch("BUFST", 1) != 0;
     // (the DMA-after-barrier A/B variant only with the select activation)
-#define OPKW_LAUNCH(BN_, DE_, MX_) \
-    hipLaunchKernelGGL((conv3w_kernel<BN_, DE_, MX_>), dim3(G), dim3(64 * kW_NW), 0, stream, a)
+#define OPKW_LAUNCH(BN_, DE_, MX_)                                                                 \
+    do {                                                                                          \
+        if (b.bufst)                                                                              \
+            hipLaunchKernelGGL((conv3w_kernel<BN_, DE_, MX_, true>), dim3(G), dim3(64 * kW_NW), 0, stream, b); \
+        else                                                                                      \
+            hipLaunchKernelGGL((conv3w_kernel<BN_, DE_, MX_, false>), dim3(G), dim3(64 * kW_NW), 0, stream, b); \
+    } while (0)
     if (a.cout == 128) {
         if (!dma_end) OPKW_LAUNCH(128, false, false);
         else if (a.actmax) OPKW_LAUNCH(128, true, true);

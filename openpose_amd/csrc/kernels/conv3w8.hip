@@ -54,7 +54,9 @@ constexpr int k8_BM = 512, k8_HR = 688, k8_NW = 8;
 // workgroup barrier the second row's lanes read it back, take the max and store.  The full-size
 // conv output is never written.
 // MX: the activation as max(t, t*m) (ConvArgs::actmax; conv3_dev.h act_pick)
-template <int BN, int NB, bool POOL, bool MX>
+// BST: one destination, epilogue stores through a buffer resource (ConvArgs::bufst)
+typedef unsigned int opk8_u4 __attribute__((ext_vector_type(4)));
+template <int BN, int NB, bool POOL, bool MX, bool BST>
 __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a)
 {
     constexpr int NW = k8_NW, BM = k8_BM, HR = k8_HR;
@@ -419,6 +421,8 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                     *(qok[i] && !first[i] ? p : sink4) = r;
                 }
         } else {
+        // one destination under 2 GiB (BST, host): buffer stores, masked lanes out of range
+        const __amdgpu_buffer_rsrc_t rs0 = buf_rsrc(d0);
 #pragma unroll
         for (int j = 0; j < NF; j += 2) {
             float4_t bq[2], mq[2];
@@ -433,18 +437,19 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const float4_t t = acc[i][j + h] + bq[h];
-                    const float4_t tm = t * mq[h];
-                    float v[4];
-#pragma unroll
-                    for (int r = 0; r < 4; ++r) v[r] = act_pick<MX>(t[r], tm[r]);
-                    pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
-                    pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                    const float4_t v = act_pick4<MX>(t, t * mq[h]);
+                    pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.xy, half2_t));
+                    pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.zw, half2_t));
                 }
                 const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
                 const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
                 const uint4 val = make_uint4(sl[0], sh[0], sl[1], sh[1]);
                 const int ch = cw + j * 16;
-                if (nd == 1) {
+                if constexpr (BST) {
+                    const uint32_t off = pok[i] ? ((uint32_t)prow[i] * (uint32_t)cs0 + ch) * 2 : kBufOOB;
+                    __builtin_amdgcn_raw_buffer_store_b128((opk8_u4){val.x, val.y, val.z, val.w}, rs0,
+                                                           (int)off, 0, 0);
+                } else if (nd == 1) {
                     uint4* p = reinterpret_cast<uint4*>(d0 + ch + (size_t)prow[i] * cs0);
                     *(pok[i] ? p : sink4) = val;
                 } else {
@@ -517,12 +522,23 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
     // a multiple of the n-block count (each block keeps one n-block)
     const unsigned G = (unsigned)(std::min<long>(a.cus / nb, ntm) * nb);
     OPK_CHECK_ARG(G >= 1 && G <= 1024, "persistent grid exceeds the sink");
+    // buffer-resource epilogue stores (BUFST=0: pointer stores, A/B): one destination whose
+    // positions x channel stride fit the 31-bit offsets of the raw buffer range check
+    ConvArgs b = a;
+    const long extent = ((long)a.frames * (a.H + 2 * a.border) * (a.W + 2 * a.border) + kConvGuardTail) *
+                        a.dst_cs[0] * 2;
+    b.bufst = !pool && a.ndst == 1 && extent < (1L << 31) - 4096 && dev_switch("BUFST", 1) != 0;
+#define OPK8_LAUNCH2(BN_, NB_, P_, MX_)                                                          \
+    do {                                                                                        \
+        if (b.bufst)                                                                            \
+            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, MX_, true>), dim3(G), dim3(64 * k8_NW), 0, stream, b); \
+        else                                                                                    \
+            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, MX_, false>), dim3(G), dim3(64 * k8_NW), 0, stream, b); \
+    } while (0)
 #define OPK8_LAUNCH(BN_, NB_, P_)                                                                \
     do {                                                                                        \
-        if (a.actmax)                                                                           \
-            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, true>), dim3(G), dim3(64 * k8_NW), 0, stream, a); \
-        else                                                                                    \
-            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, false>), dim3(G), dim3(64 * k8_NW), 0, stream, a); \
+        if (a.actmax) OPK8_LAUNCH2(BN_, NB_, P_, true);                                         \
+        else OPK8_LAUNCH2(BN_, NB_, P_, false);                                                 \
     } while (0)
     if (pool) {
         if (nb == 4) OPK8_LAUNCH(128, 4, true);
@@ -533,6 +549,7 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
     else if (a.cout == 128) OPK8_LAUNCH(128, 1, false);
     else OPK8_LAUNCH(96, 1, false);
 #undef OPK8_LAUNCH
+#undef OPK8_LAUNCH2
     OPK_LAUNCH_CHECK();
 }
 

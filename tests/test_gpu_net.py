@@ -222,7 +222,8 @@ VARIANTS = {k: dict(v) for k, v in {
     "conv1_512x64": {"CONV1_N64W16": 1},
     "nblocks_16wave": {"CONV3W8N": 0},
     "epilogue_select": {"EPI_MAX": 0}, "w8_epilogue_select": {"CONV3W8": 2, "EPI_MAX": 0},
-    "w8_all": {"CONV3W8": 3}, "head_per_tile": {"HEAD_PERSIST": 0}}.items()}
+    "w8_all": {"CONV3W8": 3}, "head_per_tile": {"HEAD_PERSIST": 0},
+    "pointer_stores": {"BUFST": 0}, "w8_pointer_stores": {"CONV3W8": 2, "BUFST": 0}}.items()}
 ROUNDING_VARIANTS = set()   # variants with another MFMA shape (another fp32 summation order)
 
 
