@@ -593,6 +593,7 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
                 h.b6 = a.bias;
                 h.s6 = a.slope;
                 h.act6 = a.act;
+                h.actmax = a.actmax && c.slope01;
                 h.w7 = static_cast<const uint16_t*>(cb.wh.ptr);
                 h.b7 = b.bias;
                 h.n1 = c.info.cout;

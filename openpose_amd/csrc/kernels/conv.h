@@ -97,6 +97,7 @@ struct HeadArgs {
     float* out32;
     int out32_c, out32_coff;
     int cus;              // > 0: persistent grid of this many workgroups (conv_head.hip)
+    int actmax;           // Mconv6's negative-side multipliers all in [0, 1] (ConvArgs::actmax)
 };
 bool conv_head_supported(int n1, int n2, int cin_pad);
 void conv_head_pack_w7(uint16_t* dst, const uint16_t* w7 /* [n2][n1] */, int n1, int n2);

@@ -36,7 +36,8 @@ using namespace conv3dev;
 
 constexpr int kH_BM = 128, kH_NW = 8;
 
-template <int N1, int NF2, bool PERSIST>
+// MX: Mconv6's activation as max(t, t*m) (HeadArgs::actmax; conv3_dev.h act_pick4)
+template <int N1, int NF2, bool PERSIST, bool MX>
 __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs a)
 {
     constexpr int NW = kH_NW, BM = kH_BM;
@@ -176,12 +177,9 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const float4_t t = acc[i][2 * kb + h] + bq[h];
-                const float4_t tm = t * mq[h];
-                float v[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
-                pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
-                pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                const float4_t v = act_pick4<MX>(t, t * mq[h]);
+                pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.xy, half2_t));
+                pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.zw, half2_t));
             }
             const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
             const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
@@ -219,33 +217,57 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
             outv[k][i] = v + b7;
         }
     }
+    // positions of this lane's MF rows: padded-image coordinates by float-reciprocal division
+    // (exact below 2^24, conv3_dev.h fdiv) instead of the integer division sequences
+    const int HW = Hp * Wp;
+    const float rHW = 1.f / (float)HW, rW = 1.f / (float)Wp;
+    int pos[MF], fri[MF], yyi[MF], xxi[MF];
+    bool ok[MF];
+#pragma unroll
+    for (int i = 0; i < MF; ++i) {
+        const int p = p0 + wm * WROWS + i * 16 + r16;
+        const int fr = fdiv(p, HW, rHW), rem = p - fr * HW;
+        const int yy = fdiv(rem, Wp, rW), xx = rem - yy * Wp;
+        pos[i] = p;
+        fri[i] = fr;
+        yyi[i] = yy;
+        xxi[i] = xx;
+        ok[i] = p < total && yy >= 1 && yy <= a.H && xx >= 1 && xx <= a.W;   // not a border position
+    }
 #pragma unroll
     for (int k = 0; k < NFO; ++k) {
         const int f = wn + k * WN1;
         const int ch = f * 16 + 4 * q;   // this lane's 4 output channels
         if (f >= NF2 || ch >= a.n2) continue;
+        const int nv = min(4, a.n2 - ch);
+        uint32_t lo[MF], hi[MF];
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
-            const int row = wm * WROWS + i * 16 + r16;
             const float4_t v = outv[k][i];
-            const int p = p0 + row;
-            if (p >= total) continue;
-            const int fr = p / (Hp * Wp), rem = p - fr * Hp * Wp;
-            const int yy = rem / Wp, xx = rem - yy * Wp;
-            if (yy < 1 || yy > a.H || xx < 1 || xx > a.W) continue;   // border position
-            const int nv = min(4, a.n2 - ch);
-            const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
-            const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
-            for (int d = 0; d < a.ndst; ++d) {
-                uint16_t* o = a.dst[d] + a.dst_coff[d] + ch + (size_t)p * a.dst_cs[d];
-                if (nv == 4 && ((a.dst_coff[d] | a.dst_cs[d]) & 3) == 0) {
-                    *reinterpret_cast<uint2*>(o) = make_uint2(lo, hi);
-                } else {
-                    for (int e = 0; e < nv; ++e) o[e] = (uint16_t)((e < 2 ? lo : hi) >> (16 * (e & 1)));
-                }
+            lo[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.xy, half2_t));
+            hi[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.zw, half2_t));
+        }
+        for (int d = 0; d < a.ndst; ++d) {
+            uint16_t* const od = a.dst[d] + a.dst_coff[d] + ch;
+            const int cs = a.dst_cs[d];
+            if (nv == 4 && ((a.dst_coff[d] | cs) & 3) == 0) {
+#pragma unroll
+                for (int i = 0; i < MF; ++i)
+                    if (ok[i]) *reinterpret_cast<uint2*>(od + (size_t)pos[i] * cs) = make_uint2(lo[i], hi[i]);
+            } else {
+#pragma unroll
+                for (int i = 0; i < MF; ++i)
+                    if (ok[i])
+                        for (int e = 0; e < nv; ++e)
+                            od[(size_t)pos[i] * cs + e] = (uint16_t)((e < 2 ? lo[i] : hi[i]) >> (16 * (e & 1)));
             }
-            if (a.out32) {
-                float* o = a.out32 + (((size_t)fr * a.out32_c + a.out32_coff + ch) * a.H + yy - 1) * a.W + xx - 1;
+        }
+        if (a.out32) {
+#pragma unroll
+            for (int i = 0; i < MF; ++i) {
+                if (!ok[i]) continue;
+                const float4_t v = outv[k][i];
+                float* o = a.out32 + (((size_t)fri[i] * a.out32_c + a.out32_coff + ch) * a.H + yyi[i] - 1) * a.W + xxi[i] - 1;
                 for (int e = 0; e < nv; ++e) o[(size_t)e * a.H * a.W] = v[e];
             }
         }
@@ -301,10 +323,15 @@ void launch_conv_head(const HeadArgs& a, hipStream_t stream)
     const bool persist = a.cus > 0 && a.n1 == 512;
     const unsigned G = (unsigned)(persist ? std::min<long>(a.cus, ntiles) : ntiles);
     const dim3 blk(64 * kH_NW);
+#define OPKH_LAUNCH2(N1_, NF2_, MX_)                                                            \
+    do {                                                                                       \
+        if (persist) hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, true, MX_>), dim3(G), blk, 0, stream, a); \
+        else hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, false, MX_>), dim3(G), blk, 0, stream, a); \
+    } while (0)
 #define OPKH_LAUNCH(N1_, NF2_)                                                                 \
     do {                                                                                       \
-        if (persist) hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, true>), dim3(G), blk, 0, stream, a); \
-        else hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, false>), dim3(G), blk, 0, stream, a); \
+        if (a.actmax) OPKH_LAUNCH2(N1_, NF2_, true);                                           \
+        else OPKH_LAUNCH2(N1_, NF2_, false);                                                   \
     } while (0)
     if (a.n1 == 512) {
         if (a.n2 <= 32) OPKH_LAUNCH(512, 2);
@@ -314,6 +341,7 @@ void launch_conv_head(const HeadArgs& a, hipStream_t stream)
         else OPKH_LAUNCH(256, 4);
     }
 #undef OPKH_LAUNCH
+#undef OPKH_LAUNCH2
     OPK_LAUNCH_CHECK();
 }
 
