@@ -344,6 +344,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         const int nd = a.ndst;
         uint16_t* const d0 = a.dst[0] + a.dst_coff[0] + nblk * BN;
         const int cs0 = a.dst_cs[0];
+        const __amdgpu_buffer_rsrc_t rs0 = buf_rsrc(d0);
         if constexpr (POOL) {
             // pooled position of each fragment's lane pair; phase 1 = the window's first row
             int qrow[MF];
@@ -360,6 +361,14 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                     first[i] = (yy & 1) != 0;
                     qrow[i] = qok[i] ? (f * OHp + ((yy - 1) >> 1) + 1) * OWp + ((s * g.sw + xx - 1) >> 1) + 1 : 0;
                 }
+            }
+            // (BST) byte offsets of the window's first / second-row lanes, the other lanes out of range
+            uint32_t qo1[MF], qo2[MF];
+#pragma unroll
+            for (int i = 0; i < MF; ++i) {
+                const uint32_t o = ((uint32_t)qrow[i] * (uint32_t)cs0 + cw) * 2;
+                qo1[i] = qok[i] && first[i] ? o : kBufOOB;
+                qo2[i] = qok[i] && !first[i] ? o : kBufOOB;
             }
             uint4 keep[MF][NF / 2];
 #pragma unroll
@@ -392,8 +401,14 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                     const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
                     const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
                     keep[i][j / 2] = make_uint4(sl[0], sh[0], sl[1], sh[1]);
-                    uint4* p = reinterpret_cast<uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
-                    *(qok[i] && first[i] ? p : sink4) = keep[i][j / 2];
+                    if constexpr (BST) {
+                        const uint4 k4 = keep[i][j / 2];
+                        __builtin_amdgcn_raw_buffer_store_b128((opk8_u4){k4.x, k4.y, k4.z, k4.w}, rs0,
+                                                               (int)(qo1[i] + j * 32), 0, 0);
+                    } else {
+                        uint4* p = reinterpret_cast<uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
+                        *(qok[i] && first[i] ? p : sink4) = keep[i][j / 2];
+                    }
                 }
             }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -403,8 +418,13 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
             for (int j = 0; j < NF; j += 2)
 #pragma unroll
                 for (int i = 0; i < MF; ++i) {
-                    const uint4* p = reinterpret_cast<const uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
-                    got[i][j / 2] = *(qok[i] && !first[i] ? p : sink4);
+                    if constexpr (BST) {
+                        const opk8_u4 g4 = __builtin_amdgcn_raw_buffer_load_b128(rs0, (int)(qo2[i] + j * 32), 0, 0);
+                        got[i][j / 2] = make_uint4(g4.x, g4.y, g4.z, g4.w);
+                    } else {
+                        const uint4* p = reinterpret_cast<const uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
+                        got[i][j / 2] = *(qok[i] && !first[i] ? p : sink4);
+                    }
                 }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
@@ -417,12 +437,16 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                     r.y = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(half2_t, x.y), __builtin_bit_cast(half2_t, y.y)));
                     r.z = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(half2_t, x.z), __builtin_bit_cast(half2_t, y.z)));
                     r.w = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(half2_t, x.w), __builtin_bit_cast(half2_t, y.w)));
-                    uint4* p = reinterpret_cast<uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
-                    *(qok[i] && !first[i] ? p : sink4) = r;
+                    if constexpr (BST) {
+                        __builtin_amdgcn_raw_buffer_store_b128((opk8_u4){r.x, r.y, r.z, r.w}, rs0,
+                                                               (int)(qo2[i] + j * 32), 0, 0);
+                    } else {
+                        uint4* p = reinterpret_cast<uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
+                        *(qok[i] && !first[i] ? p : sink4) = r;
+                    }
                 }
         } else {
         // one destination under 2 GiB (BST, host): buffer stores, masked lanes out of range
-        const __amdgpu_buffer_rsrc_t rs0 = buf_rsrc(d0);
 #pragma unroll
         for (int j = 0; j < NF; j += 2) {
             float4_t bq[2], mq[2];
@@ -527,7 +551,8 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
     ConvArgs b = a;
     const long extent = ((long)a.frames * (a.H + 2 * a.border) * (a.W + 2 * a.border) + kConvGuardTail) *
                         a.dst_cs[0] * 2;
-    b.bufst = !pool && a.ndst == 1 && extent < (1L << 31) - 4096 && dev_switch("BUFST", 1) != 0;
+    const long pextent = ((long)a.frames * (a.H / 2 + 2) * (a.W / 2 + 2) + kConvGuardTail) * a.dst_cs[0] * 2;
+    b.bufst = a.ndst == 1 && (pool ? pextent : extent) < (1L << 31) - 4096 && dev_switch("BUFST", 1) != 0;
 #define OPK8_LAUNCH2(BN_, NB_, P_, MX_)                                                          \
     do {                                                                                        \
         if (b.bufst)                                                                            \
