@@ -198,15 +198,10 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 const float4_t t = c1[gi][g] + b1[g];
-                const float4_t tm = t * m1[g];
-                float v[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const float a_ = conv3dev::act_pick<MX>(t[r], tm[r]);
-                    v[r] = in ? a_ : 0.f;
-                }
-                pk[g][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
-                pk[g][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                const float4_t a_ = conv3dev::act_pick4<MX>(t, t * m1[g]);   // packed add / mul
+                const float4_t v = in ? a_ : float4_t{0.f, 0.f, 0.f, 0.f};
+                pk[g][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.xy, half2_t));
+                pk[g][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.zw, half2_t));
             }
             // chunk c = channels 32c .. 32c+31 (groups 2c, 2c+1): v_permlane16_swap between lane
             // rows q and q^1 leaves lane row q channels 16 (q & 1) + 8 (q >> 1) .. +7 of the chunk,
@@ -278,12 +273,9 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
                 const float4_t t = acc[i][j] + b2[j];
-                const float4_t tm = t * m2[j];
-                float v[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) v[r] = conv3dev::act_pick<MX>(t[r], tm[r]);
-                pk[j][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
-                pk[j][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                const float4_t v = conv3dev::act_pick4<MX>(t, t * m2[j]);   // packed add / mul
+                pk[j][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.xy, half2_t));
+                pk[j][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.zw, half2_t));
             }
             // fragment pairs as in the halo write: 8 consecutive channels per lane, ds_write_b128
 #pragma unroll
