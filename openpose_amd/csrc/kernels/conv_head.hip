@@ -37,6 +37,9 @@ using namespace conv3dev;
 constexpr int kH_BM = 128, kH_NW = 8;
 
 // MX: Mconv6's activation as max(t, t*m) (HeadArgs::actmax; conv3_dev.h act_pick4)
+#ifndef OPKH_ABLATE   // dev probe only: 1 no Mconv6 weight DMA after a tile's first two K steps,
+#define OPKH_ABLATE 0  // 2 no phase 2/3 work beyond the partial-sum barrier, 3 no phase 3 (timing
+#endif                 // only, wrong results; profiles/round3/head_ablations/)
 template <int N1, int NF2, bool PERSIST, bool MX>
 __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs a)
 {
@@ -95,7 +98,7 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
                                          (__attribute__((address_space(3))) void*)(&lds[sl_ * ASLOT + wave * 64]), \
                                          16, 0, 0);                                           \
         const uint16_t* wb_ = a.w6 + (size_t)(s_) * N1 * 32;                                  \
-        _Pragma("unroll") for (int j_ = 0; j_ < BIW; ++j_) {                                  \
+        _Pragma("unroll") for (int j_ = 0; j_ < (OPKH_ABLATE == 1 && (s_) > 1 ? 0 : BIW); ++j_) { \
             const int rb_ = (j_ * NW + wave) * 16 + lrow;                                     \
             __builtin_amdgcn_global_load_lds(                                                 \
                 (const void*)(wb_ + rb_ * 32 + (phys ^ (((rb_ >> 2) & 1) << 1)) * 8),         \
@@ -144,6 +147,13 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
                 acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
 
+    if constexpr (OPKH_ABLATE == 2) {   // dev probe: keep the accumulators, skip phases 2 and 3
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+            for (int j = 0; j < NF; ++j) asm volatile("" :: "v"(acc[i][j]));
+        __syncthreads();
+    } else {
     // ---- phase 2: activated Mconv6 block -> Mconv7 partial over this wave's 128 channels -------
     // lane (r16, q) of acc[i][j] holds channels wn*128 + 16j + 4q .. +3 of tile row
     // wm*WROWS + 16i + r16; after the swap of pair (2kb, 2kb+1) it holds channels
@@ -190,6 +200,13 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         }
     }
 
+    if constexpr (OPKH_ABLATE == 3) {   // dev probe: phase 2 kept, phase 3 skipped
+#pragma unroll
+        for (int i = 0; i < MF; ++i)
+#pragma unroll
+            for (int f = 0; f < NF2; ++f) asm volatile("" :: "v"(acc2[i][f]));
+        __syncthreads();
+    } else {
     // ---- phase 3: sum the wave columns' partials in order, + bias, outputs ---------------------
     __syncthreads();   // every wave is past its last ring read
     float4_t* part = reinterpret_cast<float4_t*>(lds);
@@ -272,6 +289,8 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
             }
         }
     }
+    }   // OPKH_ABLATE != 3
+    }   // OPKH_ABLATE != 2
     int next = -1;
     if constexpr (PERSIST) {
         // the ring (aliased by the partials) is free once every wave has read its sums: the
