@@ -425,8 +425,10 @@ def rank_main_body135(args, rank, world, local):
     reference has no BODY_135 network); frames/s and the post-processing HBM roofline."""
     local, dist, comm_dev = dist_setup(world, local)
     from openpose_amd import synth
-    from openpose_amd.api import Context, PoseExtractor, pose_model_info
+    from openpose_amd.api import Context, PoseExtractor, dev_switches, pose_model_info
     from openpose_amd.pose_tables import BODY_135, CONNECT_GPU
+    if args.dev:   # A/B runs only; the product configuration has none
+        dev_switches(**{k: int(v) for k, v in (d.split("=", 1) for d in args.dev)}).__enter__()
 
     people = 20 if args.people == 5 else args.people
     t = pose_model_info(BODY_135)   # the library's tables (generated from poseParameters.cpp)

@@ -13,7 +13,8 @@
 //            B operands: v_permlane16_swap of fragment pairs (j, j+1) gives a lane the 8 channels
 //            16(q&1) + 8(q>>1) .. +7 of a 32-channel block -- a fixed permutation of the K order,
 //            which the host applies to Mconv7's weights instead (conv_head_pack_w7) -- and
-//            Mconv7's weights for the wave's 128 channels come from L2 into registers;
+//            Mconv7's weights for the wave's 128 channels come from L2 into registers (per-tile
+//            grid: from LDS, staged by one DMA at the last K step -- W7LDS below);
 //   phase 3  the N1/128 partial products of a position block (one per wave column) are summed
 //            through LDS in a fixed order (deterministic), + bias, fp16 into every concat slice and
 //            the fp32 NCHW net output when requested.
@@ -40,6 +41,21 @@ constexpr int kH_BM = 128, kH_NW = 8;
 #ifndef OPKH_ABLATE   // dev probe only: 1 no Mconv6 weight DMA after a tile's first two K steps,
 #define OPKH_ABLATE 0  // 2 no phase 2/3 work beyond the partial-sum barrier, 3 no phase 3 (timing
 #endif                 // only, wrong results; profiles/round3/head_ablations/)
+// W7LDS (per-tile grid, N1 = 256): Mconv7's weights reach phase 2 through LDS -- one DMA per tile
+// into the two ring B slots that are free during the last K step, then one barrier -- instead of
+// per-wave flat loads from L2 whose latency every 32-channel block of phase 2 waited for (4 exposed
+// L2 round trips per tile; each fragment fetched by both waves of a wave column).  Measured
+// (profiles/round3/head_w7/): N1 = 256 heads -12 % / -6 % (the CU's second workgroup covers the
+// barrier); the persistent N1 = 512 heads +3.5 % / +6.6 % (one workgroup per CU: the DMA wait and
+// barrier are exposed), so those keep the flat loads.  KSCHED (dev, off): a K step's fragment
+// reads in consumption order with counted lgkmcnt waits -- measured neutral to +1 %.  Both only
+// reorder data movement (bit-identical: tools/ab_outputs.py).
+#ifndef OPKH_W7LDS
+#define OPKH_W7LDS 1
+#endif
+#ifndef OPKH_KSCHED
+#define OPKH_KSCHED 0
+#endif
 template <int N1, int NF2, bool PERSIST, bool MX>
 __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs a)
 {
@@ -107,6 +123,29 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         }                                                                                     \
     } while (0)
 
+    // Mconv7's packed weights [N2P][N1] as ring rows: row r = K block (r / N2P) x output channel
+    // (r % N2P), 64 bytes, swizzled like a B slot; rows [h*N1, (h+1)*N1) fill B slot (KS + h) % 3
+    // (NF2 / 2 slots: the ones of K steps KS-2 and KS-3, free once every wave passed step KS-1's
+    // barrier; the next tile's DMA goes into the ring only after phase 3's barrier)
+    constexpr bool W7LDS = OPKH_W7LDS && !PERSIST;
+    constexpr int W7ROWS = (N1 / 32) * N2P, W7IW = W7ROWS / 16 / NW;
+    static_assert(W7ROWS <= 2 * N1 && W7ROWS % (16 * NW) == 0, "Mconv7 weights fit two B slots");
+#define OPKH_ISSUE_W7()                                                                       \
+    do {                                                                                      \
+        _Pragma("unroll") for (int k_ = 0; k_ < W7IW; ++k_) {                                 \
+            const int inst_ = k_ * NW + wave;                                                 \
+            const int r_ = inst_ * 16 + lrow;                                                 \
+            const int kb_ = r_ / N2P, o_ = r_ - (r_ / N2P) * N2P;                             \
+            const int sl_ = (KS + (inst_ * 16) / N1) % 3;                                     \
+            __builtin_amdgcn_global_load_lds(                                                 \
+                (const void*)(a.w7 + (size_t)o_ * N1 + kb_ * 32 + (phys ^ (((r_ >> 2) & 1) << 1)) * 8), \
+                (__attribute__((address_space(3))) void*)(&lds[3 * ASLOT + sl_ * BSLOT + ((inst_ * 16) % N1) * 4]), \
+                16, 0, 0);                                                                    \
+        }                                                                                     \
+    } while (0)
+    const uint32_t lds0 = (uint32_t)(uintptr_t)lds;
+    (void)lds0;
+
     OPKH_ISSUE(0);
     if (KS > 1) OPKH_ISSUE(1);
     for (;;) {
@@ -131,20 +170,77 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         else vm_wait<0>();
         __builtin_amdgcn_s_barrier();
         if (s + 2 < KS) OPKH_ISSUE(s + 2);
-        const uint4* As = lds + (s % 3) * ASLOT;
-        const uint4* Bs = lds + 3 * ASLOT + (s % 3) * BSLOT;
+        if (W7LDS && s == KS - 1) OPKH_ISSUE_W7();
         half8_t fa[MF], fb[NF];
+        if constexpr (OPKH_KSCHED) {
+            // rows i*16 / j*16 keep the swizzle bit: fragment i (j) is base + 1 KiB * i (j)
+            int ar = wm * WROWS + r16, br = wn * 128 + r16;
+            asm volatile("" : "+v"(ar), "+v"(br));
+            const uint32_t ab = lds0 + (uint32_t)(((s % 3) * ASLOT + swz64(ar, q)) * 16);
+            const uint32_t bb = lds0 + (uint32_t)(((3 * ASLOT + (s % 3) * BSLOT) + swz64(br, q)) * 16);
+            // reads in consumption order: fa[0], fb[0..NF-1], fa[1..MF-1] (R = MF + NF <= 15)
+            constexpr int R = MF + NF;
+            static_assert(R <= 15, "lgkmcnt range");
+#define OPKH_DSR(dst_, addr_, off_) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(dst_) : "v"(addr_), "i"(off_))
+            OPKH_DSR(fa[0], ab, 0);
+            OPKH_DSR(fb[0], bb, 0);
+            OPKH_DSR(fb[1], bb, 1024);
+            OPKH_DSR(fb[2], bb, 2048);
+            OPKH_DSR(fb[3], bb, 3072);
+            OPKH_DSR(fb[4], bb, 4096);
+            OPKH_DSR(fb[5], bb, 5120);
+            OPKH_DSR(fb[6], bb, 6144);
+            OPKH_DSR(fb[7], bb, 7168);
+            if (MF > 1) OPKH_DSR(fa[MF > 1 ? 1 : 0], ab, 1024);
+            if (MF > 2) OPKH_DSR(fa[MF > 2 ? 2 : 0], ab, 2048);
+            if (MF > 3) OPKH_DSR(fa[MF > 3 ? 3 : 0], ab, 3072);
+#undef OPKH_DSR
+            static_assert(NF == 8 && MF <= 4, "read list above");
+            // row 0 of the tile: MFMA j waits for read 1 + j (fa[0] is read 0)
+#define OPKH_WAIT(n_, r_) asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(r_) : "n"(n_))
+#define OPKH_ROW0(j_)                                                                         \
+    do {                                                                                      \
+        if ((j_) == 0) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(fa[0]), "+v"(fb[0]) : "n"(R - 2)); \
+        else OPKH_WAIT(R - 2 - (j_), fb[j_]);                                                 \
+        acc[0][j_] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j_], fa[0], acc[0][j_], 0, 0, 0); \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+    } while (0)
+            OPKH_ROW0(0); OPKH_ROW0(1); OPKH_ROW0(2); OPKH_ROW0(3);
+            OPKH_ROW0(4); OPKH_ROW0(5); OPKH_ROW0(6); OPKH_ROW0(7);
+#undef OPKH_ROW0
 #pragma unroll
-        for (int i = 0; i < MF; ++i)
-            fa[i] = __builtin_bit_cast(half8_t, As[swz64(wm * WROWS + i * 16 + r16, q)]);
+            for (int i = 1; i < MF; ++i) {
+                // fa[i] is read NF + i
+                switch (i) {
+                case 1: OPKH_WAIT(R - NF - 2 < 0 ? 0 : R - NF - 2, fa[i]); break;
+                case 2: OPKH_WAIT(R - NF - 3 < 0 ? 0 : R - NF - 3, fa[i]); break;
+                default: OPKH_WAIT(0, fa[i]); break;
+                }
 #pragma unroll
-        for (int j = 0; j < NF; ++j)
-            fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(wn * 128 + j * 16 + r16, q)]);
+                for (int j = 0; j < NF; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#undef OPKH_WAIT
+        } else {
+            const uint4* As = lds + (s % 3) * ASLOT;
+            const uint4* Bs = lds + 3 * ASLOT + (s % 3) * BSLOT;
 #pragma unroll
-        for (int i = 0; i < MF; ++i)
+            for (int i = 0; i < MF; ++i)
+                fa[i] = __builtin_bit_cast(half8_t, As[swz64(wm * WROWS + i * 16 + r16, q)]);
 #pragma unroll
             for (int j = 0; j < NF; ++j)
-                acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+                fb[j] = __builtin_bit_cast(half8_t, Bs[swz64(wn * 128 + j * 16 + r16, q)]);
+#pragma unroll
+            for (int i = 0; i < MF; ++i)
+#pragma unroll
+                for (int j = 0; j < NF; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (W7LDS) {   // Mconv7's weights landed (own DMA) and visible to every wave
+        vm_wait<0>();
+        __builtin_amdgcn_s_barrier();
     }
 
     if constexpr (OPKH_ABLATE == 2) {   // dev probe: keep the accumulators, skip phases 2 and 3
@@ -172,9 +268,16 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     for (int kb = 0; kb < 4; ++kb) {
         half8_t a7[NF2];
 #pragma unroll
-        for (int f = 0; f < NF2; ++f)
-            a7[f] = *reinterpret_cast<const half8_t*>(w7 + (size_t)(f * 16 + r16) * N1 + wn * 128 +
-                                                      kb * 32 + q * 8);
+        for (int f = 0; f < NF2; ++f) {
+            if constexpr (W7LDS) {   // ring row (K block wn*4 + kb) x N2P + f*16 + r16
+                const int r = (wn * 4 + kb) * N2P + f * 16 + r16;
+                const int sl = (KS + r / N1) % 3;
+                a7[f] = __builtin_bit_cast(half8_t, lds[3 * ASLOT + sl * BSLOT + swz64(r % N1, q)]);
+            } else {
+                a7[f] = *reinterpret_cast<const half8_t*>(w7 + (size_t)(f * 16 + r16) * N1 + wn * 128 +
+                                                          kb * 32 + q * 8);
+            }
+        }
         float4_t bq[2], mq[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {

@@ -263,6 +263,62 @@ __device__ __forceinline__ void refine_write(float* __restrict__ out, const Heat
     o[2] = heat_at(M, plane, px, py);
 }
 
+// refine_write for the peaks key[0 .. found) with the 7x7 windows' heat values evaluated by the whole
+// workgroup first (one lazy evaluation per lane instead of 49 in a row per peak-owning lane), then
+// summed by the peak's lane in refine_write's order with its arithmetic: bit-identical to it
+constexpr int RP = 64;   // peaks per round
+__device__ __forceinline__ void refine_peaks(float* __restrict__ out, const HeatMap& M, int plane,
+                                             const int* key, int found, float offx, float offy,
+                                             float* win)
+{
+    const int w = M.w, h = M.h, tid = threadIdx.x;
+    for (int r0 = 0; r0 < found; r0 += RP) {
+        const int np = min(RP, found - r0);
+        __syncthreads();   // the previous round's windows are summed
+        for (int i = tid; i < np * 49; i += FT) {
+            const int p = i / 49, k = i - (i / 49) * 49;
+            const int idx = key[r0 + p];
+            const int py = idx / w, px = idx - py * w;
+            const int yy = py + k / 7 - 3, xx = px + k % 7 - 3;
+            win[i] = (yy >= 0 && yy < h && xx >= 0 && xx < w) ? heat_at(M, plane, xx, yy) : 0.f;
+        }
+        __syncthreads();
+        if (tid < np) {
+            const int idx = key[r0 + tid];
+            const int py = idx / w, px = idx - py * w;
+            const float* v = win + tid * 49;
+            float xa = 0.f, ya = 0.f, sa = 0.f;
+            for (int dy = -3; dy <= 3; ++dy) {
+                const int yy = py + dy;
+                if (yy < 0 || yy >= h) continue;
+                for (int dx = -3; dx <= 3; ++dx) {
+                    const int xx = px + dx;
+                    if (xx < 0 || xx >= w) continue;
+                    const float sc = v[(dy + 3) * 7 + dx + 3];
+                    if (sc > 0) {
+                        if (M.cuda) {
+                            xa = fmaf((float)xx, sc, xa);
+                            ya = fmaf((float)yy, sc, ya);
+                        } else {
+                            xa += (float)xx * sc;
+                            ya += (float)yy * sc;
+                        }
+                        sa += sc;
+                    }
+                }
+            }
+            float* o = out + (size_t)(r0 + tid + 1) * 3;
+            o[0] = xa / sa + offx;
+            o[1] = ya / sa + offy;
+            o[2] = v[24];   // heat_at(px, py)
+        }
+    }
+}
+
+#ifndef OPK_NMS_PAR_REFINE   // dev A/B: 0 = one peak per lane, refine_write
+#define OPK_NMS_PAR_REFINE 1
+#endif
+
 __global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ peaks,
                                                           int* __restrict__ scratch,
                                                           const HeatMap M, int parts,
@@ -271,6 +327,7 @@ __global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ pe
 {
     __shared__ int key[CAP];
     __shared__ int wave_tot[FT / 64];
+    __shared__ float win[OPK_NMS_PAR_REFINE ? RP * 49 : 1];
     const int c = blockIdx.x, b = blockIdx.y;
     const int pln = b * M.channels + c;
     const int h = M.h, w = M.w;
@@ -302,7 +359,9 @@ __global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ pe
                 __syncthreads();
             }
         found = n < cap ? n : cap;
-        for (int r = tid; r < found; r += FT) refine_write(out, M, pln, key[r], r, offx, offy);
+        if (OPK_NMS_PAR_REFINE) refine_peaks(out, M, pln, key, found, offx, offy, win);
+        else
+            for (int r = tid; r < found; r += FT) refine_write(out, M, pln, key[r], r, offx, offy);
     } else {
         // overflow: ordered raster scan of the plane by this workgroup
         const int lane = tid & 63, wave = tid >> 6;
@@ -505,6 +564,8 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
         // 62 x 62 walks, one wave (measured: 30-row walks, two-wave 126 / 46-row walks 4-10 %
         // slower; loading the taps two advances ahead instead of one: no change)
         constexpr int lt = 64, rc = 62;
+        // (four walks per workgroup, each wave on its own ring with only lgkmcnt waits between
+        // rows, measured 5-9 % slower on configs 2, 4 and 5: profiles/round3/nms_wpb/)
         const dim3 grid((w + lt - 3) / (lt - 2), (h + rc - 1) / rc, frames * parts);
 #define OPK_NMS_STREAM(NS_)                                                                    \
     hipLaunchKernelGGL((nms_detect_stream_kernel<lt, rc, NS_>), grid, dim3(lt), 0, stream,     \

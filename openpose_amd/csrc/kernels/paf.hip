@@ -20,10 +20,39 @@ namespace {
 
 __device__ __forceinline__ int round_pos(float a) { return int(a + 0.5f); }
 
+// heat_at's cv::resize arithmetic (heat_dev.h, the M.nsrc lazy sources, CPU semantics) with the
+// plane's source images read from their LDS copies: src + loff[n] holds source n's sh x sw plane
+__device__ __forceinline__ float heat_at_lds(const HeatMap& M, const float* src, const int* loff, int x,
+                                            int y)
+{
+    float acc = 0.f;
+    for (int n = 0; n < M.nsrc; ++n) {
+        const ResizeSource& S = M.src[n];
+        const float* pl = src + loff[n];
+        const int x0 = S.xofs[x];
+        const float4 c = *reinterpret_cast<const float4*>(S.xcoef + 4 * x);
+        const float a[4] = {c.x, c.y, c.z, c.w};
+        const float4 b = *reinterpret_cast<const float4*>(S.ycoef + 4 * y);
+        const int yb = S.yofs[y] - 1;
+        float h[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            h[k] = cubic_hpass(pl + heat_clampi(yb + k, 0, S.sh - 1) * S.sw, S.sw, x0, a);
+        const float v = cubic_vpass(h, b.x, b.y, b.z, b.w, cubic_simd_column(x, M.w));
+        acc = (n == 0) ? v : v + acc;
+    }
+    return M.nsrc > 1 ? acc * M.inv_n : acc;
+}
+
+// LDS: the x and y PAF planes' sources staged once per (pair, frame) workgroup; every sample of
+// every candidate line then reads LDS instead of the L2/HBM source rows (dependent loads that set
+// the kernel's pace: ~2.4 ms per 64 BODY_135 frames, 152 pairs of ~20 x 20 candidates)
+template <bool LDS>
 __device__ __forceinline__ float score_ab(const float* a, const float* b, const HeatMap& M,
                                           int plane_x, int plane_y, float inter_th,
                                           float inter_min_above, float reject_score,
-                                          double near_dist)
+                                          double near_dist, const float* lx, const float* ly,
+                                          const int* loff)
 {
     const int W = M.w, H = M.h;
     const float vx = b[0] - a[0];
@@ -39,7 +68,9 @@ __device__ __forceinline__ float score_ab(const float* a, const float* b, const 
     for (int s = 0; s < n; ++s) {
         const int px = max(0, min(W - 1, round_pos(a[0] + (float)s * stepx)));
         const int py = max(0, min(H - 1, round_pos(a[1] + (float)s * stepy)));
-        const float v = ux * heat_at(M, plane_x, px, py) + uy * heat_at(M, plane_y, px, py);
+        const float hx = LDS ? heat_at_lds(M, lx, loff, px, py) : heat_at(M, plane_x, px, py);
+        const float hy = LDS ? heat_at_lds(M, ly, loff, px, py) : heat_at(M, plane_y, px, py);
+        const float v = ux * hx + uy * hy;
         if (v > inter_th) {
             sum += v;
             ++count;
@@ -75,23 +106,61 @@ __device__ __forceinline__ void pair_setup(const PafArgs& A, int b, int q, const
     py = b * A.heat.channels + A.mapy[q];
 }
 
+// dynamic LDS: [x plane of every source][y plane of every source]; loff[n] = source n's offset
+// (host: paf_lds_floats; 0 = not staged: materialised, CUDA-semantics or too large maps)
+extern __shared__ float paf_lds[];
+constexpr int kPafLdsMinLines = 64;
+template <bool LDS>
+__device__ __forceinline__ void stage_planes(const PafArgs& A, int plx, int ply, int* loff,
+                                             const float*& lx, const float*& ly)
+{
+    if constexpr (!LDS) return;
+    const HeatMap& M = A.heat;
+    int tot = 0;
+    for (int n = 0; n < M.nsrc; ++n) {
+        loff[n] = tot;
+        tot += M.src[n].sh * M.src[n].sw;
+    }
+    lx = paf_lds;
+    ly = paf_lds + tot;
+    for (int n = 0; n < M.nsrc; ++n) {
+        const ResizeSource& S = M.src[n];
+        const int cnt = S.sh * S.sw;
+        const float* gx = S.src + (size_t)plx * cnt;
+        const float* gy = S.src + (size_t)ply * cnt;
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+            paf_lds[loff[n] + i] = gx[i];
+            paf_lds[tot + loff[n] + i] = gy[i];
+        }
+    }
+    __syncthreads();
+}
+
+template <bool LDS>
 __global__ __launch_bounds__(256) void paf_dense_kernel(float* __restrict__ scores, PafArgs A)
 {
     const int q = blockIdx.x, b = blockIdx.y;
     const float *ca, *cb;
     int plx, ply, na, nb;
     pair_setup(A, b, q, ca, cb, plx, ply, na, nb);
+    int loff[kMaxResizeSources];
+    const float *lx = nullptr, *ly = nullptr;
+    const bool use = LDS && na * nb >= kPafLdsMinLines;
+    if (use) stage_planes<LDS>(A, plx, ply, loff, lx, ly);
     float* out = scores + ((size_t)b * A.npairs + q) * A.max_peaks * A.max_peaks;
     for (int t = threadIdx.x; t < na * nb; t += blockDim.x) {
         const int i = t / nb, j = t - (t / nb) * nb;
         out[(size_t)i * A.max_peaks + j] =
-            score_ab(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
-                     A.inter_min_above, A.reject_score, A.near_dist);
+            use ? score_ab<true>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
+                                 A.inter_min_above, A.reject_score, A.near_dist, lx, ly, loff)
+                : score_ab<false>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
+                                  A.inter_min_above, A.reject_score, A.near_dist, lx, ly, loff);
     }
 }
 
 // compact records: offset of pair q = sum over earlier pairs of nA*nB (recomputed per block from
 // the 2*q peak counts it needs -- 26 pairs, cheaper than a separate scan launch).
+template <bool LDS>
 __global__ __launch_bounds__(256) void paf_compact_kernel(float* __restrict__ records,
                                                           int rec_floats, PafArgs A)
 {
@@ -111,11 +180,19 @@ __global__ __launch_bounds__(256) void paf_compact_kernel(float* __restrict__ re
     const bool fits = total + 1 <= rec_floats;
     if (q == 0 && threadIdx.x == 0) rec[0] = fits ? (float)total : -1.f;
     if (!fits) return;
+    int loff[kMaxResizeSources];
+    const float *lx = nullptr, *ly = nullptr;
+    // staged only for pairs with many candidate lines (block-uniform): a few lines read fewer
+    // bytes than the two planes hold
+    const bool use = LDS && na * nb >= kPafLdsMinLines;
+    if (use) stage_planes<LDS>(A, plx, ply, loff, lx, ly);
     float* out = rec + 1 + offset;
     for (int t = threadIdx.x; t < na * nb; t += blockDim.x) {
         const int i = t / nb, j = t - (t / nb) * nb;
-        out[t] = score_ab(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
-                          A.inter_min_above, A.reject_score, A.near_dist);
+        out[t] = use ? score_ab<true>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
+                                      A.inter_min_above, A.reject_score, A.near_dist, lx, ly, loff)
+                     : score_ab<false>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
+                                       A.inter_min_above, A.reject_score, A.near_dist, lx, ly, loff);
     }
 }
 
@@ -138,6 +215,20 @@ PafArgs make_args(const HeatMap& heat, const float* peaks, int max_peaks, const 
     return a;
 }
 
+// LDS bytes of a workgroup's staged x / y planes: lazy maps with CPU semantics whose sources fit
+// 40 KiB (BODY_25 / BODY_135 at 368 rows: 2 x 46 x 82 floats = 30 KB); 0 = read the sources (or
+// the materialised map) through heat_at (PAF_LDS=0: always, dev A/B).  Measured
+// (profiles/round3/paf_lds/): BODY_135, 20 people, paf_compact 2.43 -> 0.82 ms per 64 frames;
+// the four-scale map (57 KB: two workgroups per CU) ran 0.75 % slower staged, so it reads L2
+size_t paf_lds_bytes(const HeatMap& M)
+{
+    if (M.heat || M.cuda || M.nsrc < 1 || dev_switch("PAF_LDS", 1) == 0) return 0;
+    size_t n = 0;
+    for (int i = 0; i < M.nsrc; ++i) n += (size_t)M.src[i].sh * M.src[i].sw;
+    const size_t bytes = 2 * n * sizeof(float);
+    return bytes <= 40 * 1024 ? bytes : 0;
+}
+
 }  // namespace
 
 void launch_paf_scores(float* scores, const HeatMap& heat, const float* peaks, int frames,
@@ -148,7 +239,9 @@ void launch_paf_scores(float* scores, const HeatMap& heat, const float* peaks, i
     OPK_CHECK_ARG(frames > 0 && t.npairs > 0 && max_peaks > 0, "bad sizes");
     PafArgs a = make_args(heat, peaks, max_peaks, t, inter_th, inter_min_above, reject_score,
                           near_dist);
-    hipLaunchKernelGGL(paf_dense_kernel, dim3(t.npairs, frames), dim3(256), 0, stream, scores, a);
+    const size_t lds = paf_lds_bytes(heat);
+    if (lds) hipLaunchKernelGGL(paf_dense_kernel<true>, dim3(t.npairs, frames), dim3(256), lds, stream, scores, a);
+    else hipLaunchKernelGGL(paf_dense_kernel<false>, dim3(t.npairs, frames), dim3(256), 0, stream, scores, a);
     OPK_LAUNCH_CHECK();
 }
 
@@ -160,8 +253,13 @@ void launch_paf_scores_compact(float* records, int rec_floats, const HeatMap& he
     OPK_CHECK_ARG(frames > 0 && t.npairs > 0 && max_peaks > 0 && rec_floats > 1, "bad sizes");
     PafArgs a = make_args(heat, peaks, max_peaks, t, inter_th, inter_min_above, reject_score,
                           near_dist);
-    hipLaunchKernelGGL(paf_compact_kernel, dim3(t.npairs, frames), dim3(256), 0, stream, records,
-                       rec_floats, a);
+    const size_t lds = paf_lds_bytes(heat);
+    if (lds)
+        hipLaunchKernelGGL(paf_compact_kernel<true>, dim3(t.npairs, frames), dim3(256), lds, stream,
+                           records, rec_floats, a);
+    else
+        hipLaunchKernelGGL(paf_compact_kernel<false>, dim3(t.npairs, frames), dim3(256), 0, stream,
+                           records, rec_floats, a);
     OPK_LAUNCH_CHECK();
 }
 
