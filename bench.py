@@ -164,8 +164,8 @@ def pmc_traffic(batch):
 # per-step PMC counts of the post-processing kernels (overlay add, NMS detect + finalize, PAF
 # integrals) from the committed rocprofv3 summary (tools/pmc_round.sh + pmc_report.py; its "batch"
 # must equal the bench's frames per step)
-POST_PMC = os.path.join(ROOT, "profiles", "round3", "pmc_r3h", "report.json")
-POST_PMC_B135 = os.path.join(ROOT, "profiles", "round3", "pmc_body135", "report.json")
+POST_PMC = os.path.join(ROOT, "profiles", "round3", "pmc_r3i", "report.json")
+POST_PMC_B135 = os.path.join(ROOT, "profiles", "round3", "pmc_body135_r3i", "report.json")
 VALU_PEAK_GINSTS = 1024 * 0.5 * 2.4   # wave64 VALU instructions: 1 per 2 cycles per SIMD-32, 2.4 GHz
 
 
