@@ -4,6 +4,13 @@
 #pragma once
 #include "conv.h"
 
+// OPK_ZC: a tile's first K step takes the MFMA's zero C operand instead of accumulators zeroed
+// after the previous tile's epilogue (conv3w; 0 = the zeroing, dev A/B builds).  Measured
+// (profiles/round3/zc/): conv3w<96> -1.5 %, conv3w<128> -0.3 %; in conv3w8 +0.6 %, so not there
+#ifndef OPK_ZC
+#define OPK_ZC 1
+#endif
+
 namespace opk {
 namespace conv3dev {
 

@@ -229,7 +229,7 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
     // one tap: fragments of step 0 in flight; step i reads A fragment i+1 and waits for its own
     // (lgkmcnt(1): only the one just issued may still be outstanding; the last step waits for
     // all); then the next tap's step-0 fragments are issued (base nab_, nbb_ + nboff_)
-#define OPKW_TAP(ab_, nab_, nbb_, nboff_, PF_)                                                \
+#define OPKW_TAP(ab_, nab_, nbb_, nboff_, PF_, ZC_)                                           \
     do {                                                                                      \
         _Pragma("unroll") for (int i_ = 0; i_ < MF; ++i_) {                                   \
             half8_t& cur_ = (i_ & 1) ? fa1 : fa0;                                             \
@@ -249,7 +249,8 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
             }                                                                                 \
             _Pragma("unroll") for (int j_ = 0; j_ < NF; ++j_)                                 \
                 acc[i_][j_] = OPKW_ABLATE == 2 ? acc[i_][j_] + (float)cur_[j_]                  \
-                    : __builtin_amdgcn_mfma_f32_16x16x32_f16(fb[j_], cur_, acc[i_][j_], 0, 0, 0); \
+                    : __builtin_amdgcn_mfma_f32_16x16x32_f16(                                   \
+                          fb[j_], cur_, (ZC_) ? float4_t{0.f, 0.f, 0.f, 0.f} : acc[i_][j_], 0, 0, 0); \
             __builtin_amdgcn_sched_barrier(0);   /* keep the issue order as written */       \
         }                                                                                     \
         if (PF_) OPKW_READ_TAP0(nab_, nbb_, nboff_);                                          \
@@ -289,9 +290,12 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
             // tap 0's fragments: unit u was certified at mid-unit u-1 (no barrier here)
             OPKW_READ_TAP0(ab0, bb_u, 0);
             const uint32_t ab1 = OPKW_ABASE(aslot, ky, 1);
-            OPKW_TAP(ab0, ab1, bb_u, BN * 64, true);
+            // a tile's first tap starts its accumulators from the MFMA's zero C operand (no
+            // per-tile zeroing of the 4 x NF accumulators after the epilogue; bit-identical)
+            if (OPK_ZC && u == 0) OPKW_TAP(ab0, ab1, bb_u, BN * 64, true, OPK_ZC);
+            else OPKW_TAP(ab0, ab1, bb_u, BN * 64, true, 0);
             const uint32_t ab2 = OPKW_ABASE(aslot, ky, 2);
-            OPKW_TAP(ab1, ab2, bb_u, 2 * BN * 64, true);
+            OPKW_TAP(ab1, ab2, bb_u, 2 * BN * 64, true, 0);
             // mid-unit: unit u+1's DMA landed (own part; vmcnt(0) also covers the previous
             // tile's epilogue stores, the only younger VMEM ops), then visible to all (barrier);
             // then the DMA of unit u+2 (into the slots of unit u-1 / chunk c-1) -- the next
@@ -322,7 +326,7 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
             if (tcount == 1 && u == 0) OPKW_STAMP(12);
 #endif
             if (!DMA_END && (OPKW_ABLATE != 4 || u + 2 >= U)) OPKW_DMA_U2();
-            OPKW_TAP(ab2, ab2, bb_u, 0, false);
+            OPKW_TAP(ab2, ab2, bb_u, 0, false, 0);
             if (DMA_END && (OPKW_ABLATE != 4 || u + 2 >= U)) OPKW_DMA_U2();
 #undef OPKW_DMA_U2
         }
@@ -362,7 +366,8 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
                     }
                 }
                 const bool in = pbase + i * 16 < g.total;
-                prow[i] = in ? (f * g.Hp + yy) * g.Wp + s * g.sw + xx : 0;
+                // one strip: the virtual image is the padded image (no multiplies)
+                prow[i] = !in ? 0 : g.nstrips == 1 ? pbase + i * 16 : (f * g.Hp + yy) * g.Wp + s * g.sw + xx;
                 pok[i] = in && g.interior(yy, xx, s, a.W);
             }
         }
@@ -441,10 +446,12 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
 #undef OPKW_STORE
 #undef OPKW_BIAS
 #undef OPKW_ACT
+        if (!OPK_ZC) {
 #pragma unroll
-        for (int i = 0; i < MF; ++i)
+            for (int i = 0; i < MF; ++i)
 #pragma unroll
-            for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+                for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
+        }
 #ifdef OPKW_STAMPS
         if (tcount < 2) OPKW_STAMP(3 + 2 * tcount);
         ++tcount;
