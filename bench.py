@@ -63,11 +63,72 @@ def parse():
                          "body135: configs[4] (BODY_135 net-output injection, 20 people)")
     ap.add_argument("--people", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "16")))
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads; 0: the CPUs this process may run on "
+                         "(sched_getaffinity), capped by OMP_NUM_THREADS when the host sets it")
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample")
+    ap.add_argument("--dump-records", default=None, metavar="NPZ",
+                    help="rank 0: write the gathered per-frame records of the timed steps (tests)")
     ap.add_argument("--dev", action="append", default=[], metavar="KEY=VAL",
                     help="kernel-variant switch for A/B runs (opk_dev_set; include/opk.h)")
     return ap.parse_args()
+
+
+def cpu_share():
+    """(threads for the CPU baseline, affinity CPU count, OMP_NUM_THREADS or None).  The GPU box's
+    harness sets OMP_NUM_THREADS to the CPU share of one GPU (16) while os.cpu_count() and even the
+    affinity mask may show the whole machine; the baseline uses the affinity set, capped by that
+    share."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        aff = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    omp = int(env) if env and env.isdigit() and int(env) > 0 else None
+    return (min(aff, omp) if omp else aff), aff, omp
+
+
+def kernel_src_sha():
+    """sha256 over the kernel sources (openpose_amd/csrc/kernels/*): which kernels a committed
+    PMC summary was collected with (tools/pmc_round.sh records the same digest)."""
+    import hashlib
+    d = os.path.join(ROOT, "openpose_amd", "csrc", "kernels")
+    h = hashlib.sha256()
+    for f in sorted(os.listdir(d)):
+        with open(os.path.join(d, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def pmc_provenance(path):
+    """Commit + kernel-source digest a PMC summary was collected at, and whether the kernels are
+    still the ones running now."""
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    sha = d.get("kernel_src_sha")
+    return {"source": os.path.relpath(path, ROOT), "pmc_commit": d.get("commit"),
+            "kernel_src_sha": sha, "kernels_match_this_tree": sha == kernel_src_sha() if sha else None}
+
+
+CONTENTS = 4   # distinct synthetic batches: global batch k carries content k % CONTENTS
+
+
+def contents_of_rank(rank, world, steps=None):
+    """Synthetic contents this rank's batches use (global batch index k = step * world + rank, the
+    frame ids the ordered gather assigns), so that a frame's input depends only on its global
+    frame id: an N-rank run and a 1-rank run over the same frame ids see the same frames."""
+    return sorted({(i * world + rank) % CONTENTS for i in range(CONTENTS)})   # period <= CONTENTS
+
+
+def dump_records(path, ordered):
+    """[(keypoints [people, parts, 3], scores [people])] per frame -> npz (tests)."""
+    counts = np.array([len(ks) for _, ks in ordered], np.int64)
+    kp = np.concatenate([np.asarray(k, np.float32).reshape(-1) for k, _ in ordered] + [np.zeros(0, np.float32)])
+    ks = np.concatenate([np.asarray(s, np.float32).reshape(-1) for _, s in ordered] + [np.zeros(0, np.float32)])
+    np.savez(path, counts=counts, keypoints=kp, scores=ks)
 
 
 def tile_aligned_batch(cus, rounds=4):
@@ -99,13 +160,14 @@ def cpu_baseline(args, params, frames_np, overlays_np):
     import oracle
     from oracle import body25
     graph = body25.layers()
+    threads = args.cpu_threads
     t0 = time.perf_counter()
     done = 0
     people = 0
     while True:
         scales, [(nw, nh)] = oracle.scale_and_size(PRODUCER)
         x = oracle.cvmat_to_input(frames_np[done % len(frames_np)], scales[0], nw, nh)[None]
-        out = body25.forward(x, params, graph=graph, nthreads=args.cpu_threads)[0]
+        out = body25.forward(x, params, graph=graph, nthreads=threads)[0]
         out = out + overlays_np[done % len(overlays_np)]
         heat = oracle.resize_merge([out], NET_H, NET_W)
         scale = 1.959128
@@ -119,17 +181,21 @@ def cpu_baseline(args, params, frames_np, overlays_np):
     # config 1: one 368x368 frame (net input 368x368, output 46x46), the same stages
     t1 = time.perf_counter()
     x1 = np.random.default_rng(0).uniform(-0.5, 0.5, (1, 3, 368, 368)).astype(np.float32)
-    o1 = body25.forward(x1, params, graph=graph, nthreads=args.cpu_threads)[0]
+    o1 = body25.forward(x1, params, graph=graph, nthreads=threads)[0]
     h1 = oracle.resize_merge([o1], 368, 368)
     p1 = oracle.nms(h1, 0.05, 128, (0.25, 0.25))
     oracle.connect(h1, p1, scale=1.0)
     el1 = time.perf_counter() - t1
-    return {"value": done / el, "unit": "frames/s", "cores": args.cpu_threads, "kind": "port",
-            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+    _, aff, omp = cpu_share()
+    return {"value": done / el, "unit": "frames/s", "cores": threads, "kind": "port",
+            "affinity_cpus": aff, "omp_num_threads_env": omp, "host_cpus": os.cpu_count(),
+            "cpu_model": cpu_model(),
+            "cores_note": "threads = the CPUs in this process's affinity mask, capped by "
+                          "OMP_NUM_THREADS (the CPU share the GPU box allots per GPU) when set",
             "sample": "%d frame(s) of the full config-2 pipeline on 1280x720 frames (warpAffine + "
                       "CNN fp32 at 656x368 + resize + NMS + connector), oracle/ CPU restatement, "
                       "%.1f s on %d threads, %d people found"
-                      % (done, el, args.cpu_threads, people),
+                      % (done, el, threads, people),
             "config1": {"value": 1.0 / el1, "unit": "frames/s",
                         "sample": "1 frame, BODY_25 368x368 net input (161.1 GFLOP) + resize + "
                                   "NMS + connector, %.1f s" % el1},
@@ -146,26 +212,47 @@ def host_breakdown(host, steps):
     return out
 
 
+def _first(*rel):
+    for r in rel:
+        p = os.path.join(ROOT, "profiles", r)
+        if os.path.exists(p):
+            return p
+    return os.path.join(ROOT, "profiles", rel[-1])
+
+
+# Committed rocprofv3 PMC summaries (tools/pmc_round.sh + pmc_report.py + pmc_summary.py; each
+# records the commit and kernel-source digest it was collected at, reported beside the numbers
+# read from it): CNN HBM bytes per forward, time-weighted MFMA busy, and the post-processing
+# kernels' per-step VALU / HBM counts.  Their "batch" must equal the bench's frames per step.
+PMC_TRAFFIC = _first("round4/pmc/pmc_traffic.json", "round3/pmc_traffic.json")
+POST_PMC = _first("round4/pmc/report.json", "round3/pmc_r3i/report.json")
+POST_PMC_B135 = _first("round4/pmc_body135/report.json", "round3/pmc_body135_r3i/report.json")
+
+
 def pmc_traffic(batch):
-    """HBM bytes of one CNN forward from the committed rocprofv3 PMC summary (FETCH_SIZE x2 on
-    gfx950 + WRITE_SIZE over every kernel of one forward; tools/pmc_summary.py), or None when the
-    summary was taken at another batch size."""
-    for rnd in ("round3", "round2", "round1"):
-        path = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
-        try:
-            with open(path) as f:
-                d = json.load(f)
-        except (OSError, ValueError):
-            continue
-        return d.get("cnn_forward_hbm_bytes") if d.get("batch") == batch else None
-    return None
+    """HBM bytes of one CNN forward from the committed PMC summary (FETCH_SIZE x2 on gfx950 +
+    WRITE_SIZE over every kernel of one forward), or None when it was taken at another batch."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    return d.get("cnn_forward_hbm_bytes") if d.get("batch") == batch else None
 
 
-# per-step PMC counts of the post-processing kernels (overlay add, NMS detect + finalize, PAF
-# integrals) from the committed rocprofv3 summary (tools/pmc_round.sh + pmc_report.py; its "batch"
-# must equal the bench's frames per step)
-POST_PMC = os.path.join(ROOT, "profiles", "round3", "pmc_r3i", "report.json")
-POST_PMC_B135 = os.path.join(ROOT, "profiles", "round3", "pmc_body135_r3i", "report.json")
+def pmc_mfma_busy(batch):
+    """Time-weighted MFMA busy of the CNN's conv kernels (SQ_VALU_MFMA_BUSY_CYCLES over 1,024
+    SIMDs x the cycles each launch ran) from the committed PMC report, or None at another batch."""
+    try:
+        with open(POST_PMC) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("batch") != batch:
+        return None
+    return round(d["cnn"]["time_weighted_mfma_busy"], 4)
+
+
 VALU_PEAK_GINSTS = 1024 * 0.5 * 2.4   # wave64 VALU instructions: 1 per 2 cycles per SIMD-32, 2.4 GHz
 
 
@@ -209,7 +296,7 @@ def post_roofline(batch, post_ms, pmc_path=POST_PMC, ref_bytes_frame=POST_BYTES_
                     "unit": "GB/s", "frac": round(hf, 4)})
     out.update({"valu_frac": round(vf, 4), "hbm_frac": round(hf, 4),
                 "pmc_per_step": {"valu_wave_insts": pmc["valu_insts"], "hbm_bytes": pmc["hbm_bytes"]},
-                "pmc_source": os.path.relpath(pmc_path, ROOT),
+                "pmc_source": pmc_provenance(pmc_path),
                 "note": "neither bound is near its peak: NMS detect (~70 % of the time) waits on "
                         "dependent loads of its rolling window (latency)"})
     return out
@@ -251,20 +338,22 @@ def rank_main(args, rank, world, local):
 
     B = args.batch or tile_aligned_batch(torch.cuda.get_device_properties(local).multi_processor_count)
     nscales = 4 if args.config == "multiscale" else 1
-    gen = torch.Generator(device="cuda").manual_seed(1234 + rank)
     W_IN, H_IN = PRODUCER
-    frames = [torch.randint(0, 256, (B, H_IN, W_IN, 3), generator=gen, device="cuda",
-                            dtype=torch.uint8) for _ in range(2)]
+    frames = {}
+    for c in contents_of_rank(rank, world, args.steps):
+        gen = torch.Generator(device="cuda").manual_seed(1234 + c)
+        frames[c] = torch.randint(0, 256, (B, H_IN, W_IN, 3), generator=gen, device="cuda",
+                                  dtype=torch.uint8)
+    first_content = min(frames)
     pose.set_input((-1, NET_H), scale_number=nscales, scale_gap=0.25)
     _, net_sizes = scale_and_size(PRODUCER, (-1, NET_H), 1.0, nscales, 0.25)
     assert net_sizes[0] == (NET_W, NET_H)
     flops_frame = sum(net.flops_per_frame(h, w) for (w, h) in net_sizes)
 
     # net-output statistics before any overlay (the overlay is added in place into it)
-    pose.forward_frames(frames[0])
+    pose.forward_frames(frames[first_content])
     out_std = float(net.output_numpy()[:2].std()) if nscales == 1 else None
-    ov_np = np.stack([synth.overlay(args.people, NET_H // 8, NET_W // 8, seed=1000 * rank + f)
-                      for f in range(B)])
+    ov_np = np.stack([synth.overlay(args.people, NET_H // 8, NET_W // 8, seed=f) for f in range(B)])
     overlay = torch.from_numpy(ov_np).cuda()
     pose.set_overlay(overlay)
 
@@ -292,7 +381,7 @@ def rank_main(args, rank, world, local):
 
     def step(i, timed):
         s0 = time.perf_counter()
-        pose.submit_frames(frames[i % 2])
+        pose.submit_frames(frames[(i * world + rank) % CONTENTS])
         if timed:
             host["submit"] += time.perf_counter() - s0
         if pose.pending() > 1:
@@ -322,6 +411,8 @@ def rank_main(args, rank, world, local):
     f0 = time.perf_counter()
     ordered = gather.finish(PARTS)        # rank 0: every frame's record, in frame order
     host["finish"] = time.perf_counter() - f0
+    if rank == 0 and args.dump_records:
+        dump_records(args.dump_records, ordered)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -402,6 +493,8 @@ def rank_main(args, rank, world, local):
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
             "traffic": pmc_traffic(B) if nscales == 1 else None,
+            "mfma_busy": pmc_mfma_busy(B) if nscales == 1 else None,
+            "pmc": {"traffic": pmc_provenance(PMC_TRAFFIC), "mfma_busy": pmc_provenance(POST_PMC)},
             "traffic_unit": "bytes per launch (HBM, PMC)",
             "algorithmic_gflop_per_launch": round(flops_frame * B / 1e9, 2),
             "avg_launch_ms": round(net_ms, 3),
@@ -412,7 +505,7 @@ def rank_main(args, rank, world, local):
         "host_ms": host_breakdown(host, args.steps),
     }
     if rank == 0 and world == 1 and nscales == 1 and not args.no_cpu_baseline:
-        frames_np = frames[0][:2].cpu().numpy()   # uint8 [2][720][1280][3]
+        frames_np = frames[first_content][:2].cpu().numpy()   # uint8 [2][720][1280][3]
         result["cpu_baseline"] = cpu_baseline(args, params, frames_np, ov_np[:2])
     if rank == 0:
         print(json.dumps(result), flush=True)
@@ -436,11 +529,12 @@ def rank_main_body135(args, rank, world, local):
     H8, W8 = NET_H // 8, NET_W // 8
     B = args.batch or 64   # no CNN in this config: no tile alignment
     distinct = 8
-    fields = np.stack([synth.overlay(people, H8, W8, seed=7000 * rank + k, table=t) +
+    fields = np.stack([synth.overlay(people, H8, W8, seed=7000 + k, table=t) +
                        np.random.default_rng(k).normal(0, 0.01, (C, H8, W8)).astype(np.float32)
                        for k in range(distinct)]).astype(np.float32)
-    net_out = [torch.from_numpy(fields[np.arange(B) % distinct]).cuda(),
-               torch.from_numpy(fields[(np.arange(B) + 3) % distinct]).cuda()]
+    # content c of a global batch (contents_of_rank): frame f holds field (f + 3c) % distinct
+    net_out = {c: torch.from_numpy(fields[(np.arange(B) + 3 * c) % distinct]).cuda()
+               for c in contents_of_rank(rank, world, args.steps)}
     ctx = Context(local)
     pose = PoseExtractor(ctx, None, pose_model=BODY_135, semantics=CONNECT_GPU)
     parts = t["parts"]
@@ -464,7 +558,7 @@ def rank_main_body135(args, rank, world, local):
 
     def step(i, timed):
         s0 = time.perf_counter()
-        pose.submit_net_output(net_out[i % 2], (NET_W, NET_H), PRODUCER)
+        pose.submit_net_output(net_out[(i * world + rank) % CONTENTS], (NET_W, NET_H), PRODUCER)
         if timed:
             host["submit"] += time.perf_counter() - s0
         if pose.pending() > 1:
@@ -490,6 +584,8 @@ def rank_main_body135(args, rank, world, local):
     f0 = time.perf_counter()
     ordered = gather.finish(parts)
     host["finish"] = time.perf_counter() - f0
+    if rank == 0 and args.dump_records:
+        dump_records(args.dump_records, ordered)
     torch.cuda.synchronize()
     if dist is not None:
         dist.barrier()
@@ -555,7 +651,7 @@ def rank_main_body135(args, rank, world, local):
                 break
         result["cpu_baseline"] = {
             "value": done / el, "unit": "frames/s", "cores": 1, "kind": "port",
-            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+            "affinity_cpus": cpu_share()[1], "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
             "sample": "%d frame(s): oracle/ resize (439 maps) + NMS + pair scores + GPU-path "
                       "assembly, %.1f s, single-threaded" % (done, el)}
     if rank == 0:
@@ -566,6 +662,8 @@ def rank_main_body135(args, rank, world, local):
 
 def main():
     args = parse()
+    if args.cpu_threads <= 0:
+        args.cpu_threads = cpu_share()[0]
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # direct start with --gpus N: one child process per GPU, this process touches no GPU
         sys.exit(parallel.launch_ranks(args.gpus, [os.path.abspath(__file__)] + sys.argv[1:]))

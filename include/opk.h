@@ -275,6 +275,19 @@ int opk_net_read_timing(opk_net* net, int* forwards, double* total_ms);
  * {0, out_channels, 0, 0}.  The buffer of one input shape is stable across forwards of that
  * shape (the values are the latest forward's). */
 int opk_net_output(opk_net* net, float** output_dev, int shape[4]);
+/* Inspection (caffe::Net::blob_by_name, which NetCaffe does not expose; used by the per-layer
+ * parity tests): frames [frame0, frame0 + nframes) of the named top of the last forward -- a
+ * conv, pool or concat top, or net_output -- converted from its padded NHWC fp16 buffer (the fp32
+ * output for net_output) to fp32 NCHW host memory [nframes][channels][h][w]; host_out NULL:
+ * shape only.  Synchronises the context stream.  Blobs that fused kernels keep on chip
+ * (conv1_1 / conv1_2 with the fused first layers, a pooled conv's un-pooled output, Mconv6 of a
+ * fused head pair) fail with the "kept on chip" message. */
+int opk_net_blob(opk_net* net, const char* name, int frame0, int nframes, float* host_out,
+                 int shape[4]);
+/* Kernels launched by the last forward run while the dev switch LAUNCH_LOG was 1, one
+ * "<layer>\t<kernel instantiation>\n" line per launch.  *needed = bytes incl. the NUL; the text
+ * is copied when size >= *needed. */
+int opk_net_launch_log(opk_net* net, char* buf, size_t size, size_t* needed);
 
 /* ---- Pose extractor: replaces op::PoseExtractorCaffe::forwardPass
  *      (src/openpose/pose/poseExtractorCaffe.cpp:200-334) for a batch of frames:

@@ -65,6 +65,8 @@ _SIGS = {
     "opk_net_forward": (_i, [_p, _p, _i, _i, _i]),
     "opk_net_flops_per_frame": (_i, [_p, _i, _i, _c.POINTER(_d)]),
     "opk_net_output": (_i, [_p, _c.POINTER(_p), _ip]),
+    "opk_net_blob": (_i, [_p, _c.c_char_p, _i, _i, _p, _ip]),
+    "opk_net_launch_log": (_i, [_p, _c.c_char_p, _c.c_size_t, _c.POINTER(_c.c_size_t)]),
     "opk_pose_create": (_i, [_p, _p, _i, _c.POINTER(_p)]),
     "opk_pose_create_model": (_i, [_p, _p, _i, _i, _i, _c.POINTER(_p)]),
     "opk_pose_destroy": (_i, [_p]),

@@ -462,6 +462,25 @@ class Net:
                                     ctypes.c_void_p(p), out.nbytes))
         return out
 
+    def blob(self, name, frames=None):
+        """Named top of the last forward (opk_net_blob) as fp32 NCHW numpy: frames = (first, count),
+        default all.  Values are the fp16 activations the kernels stored (net_output: fp32)."""
+        shape = (ctypes.c_int * 4)()
+        f0, nf = frames if frames is not None else (0, self.output()[1][0])
+        check(self.L.opk_net_blob(self.h, name.encode(), f0, nf, None, shape))
+        out = np.empty(tuple(shape), np.float32)
+        check(self.L.opk_net_blob(self.h, name.encode(), f0, nf,
+                                  out.ctypes.data_as(ctypes.c_void_p), shape))
+        return out
+
+    def launch_log(self):
+        """[(layer, kernel instantiation)] of the last forward run under dev_switches(LAUNCH_LOG=1)."""
+        need = ctypes.c_size_t()
+        check(self.L.opk_net_launch_log(self.h, None, 0, ctypes.byref(need)))
+        buf = ctypes.create_string_buffer(need.value)
+        check(self.L.opk_net_launch_log(self.h, buf, need.value, ctypes.byref(need)))
+        return [tuple(line.split("\t", 1)) for line in buf.value.decode().splitlines()]
+
 
 class PoseExtractor:
     """op::PoseExtractorCaffe replacement for batches of frames (PoseHip)."""

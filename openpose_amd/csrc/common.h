@@ -38,6 +38,18 @@ struct Error : std::runtime_error {
 // exports can change which kernels run.  Unset keys give dflt (the product configuration).
 int dev_switch(const char* key, int dflt);
 
+// Launch log (tests and profiling: which kernel instantiation ran for which layer).  While a
+// log is attached to the calling thread, note_launch() appends "<layer>\t<kernel>" lines to it;
+// otherwise it returns at once.  NetHip attaches its log for the forwards run while the dev
+// switch LAUNCH_LOG is 1 (opk_net_launch_log).
+struct LaunchLog {
+    std::string layer;
+    std::vector<std::string> lines;
+};
+void attach_launch_log(LaunchLog* log);   // nullptr detaches
+LaunchLog* launch_log();
+void note_launch(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+
 // Device scratch that only grows (one per context and purpose); never freed inside a launch
 // sequence so the launch functions stay graph-capturable.
 struct DevBuf {

@@ -126,6 +126,26 @@ int opk_net_output(opk_net* net, float** out, int shape[4])
     });
 }
 
+int opk_net_blob(opk_net* net, const char* name, int frame0, int nframes, float* host_out,
+                 int shape[4])
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net && name && shape, "NULL argument");
+        net->net->blob(name, frame0, nframes, host_out, shape);
+    });
+}
+
+int opk_net_launch_log(opk_net* net, char* buf, size_t size, size_t* needed)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net && needed, "NULL argument");
+        std::string text;
+        for (const auto& l : net->net->launches()) text += l + "\n";
+        *needed = text.size() + 1;
+        if (buf && size >= *needed) std::memcpy(buf, text.c_str(), text.size() + 1);
+    });
+}
+
 int opk_pose_create(opk_ctx* ctx, opk_net* net, int maxpos, opk_pose** out)
 {
     return guarded_net([&] {

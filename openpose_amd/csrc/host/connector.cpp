@@ -18,7 +18,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#if defined(__SSE__)
 #include <immintrin.h>
+#endif
 #include <limits>
 #include <string>
 
@@ -246,7 +248,9 @@ void people_global_sort(People& people, AssemblyScratch& sc, const PoseModelInfo
     conn.clear();
     // s > 1e-6 (a double compare in the reference) == s >= thr for every float s (NaN fails both)
     const float thr = kPafMinFloat;
+#if defined(__SSE__)
     const __m128 vthr = _mm_set1_ps(thr);
+#endif
     for (int q = 0; q < m.npairs(); ++q) {
         const int pa = m.pairs[2 * q], pb = m.pairs[2 * q + 1];
         const int na = round_pos(peaks[pa * stride]);
@@ -261,6 +265,7 @@ void people_global_sort(People& people, AssemblyScratch& sc, const PoseModelInfo
                                 (uint64_t)q << 32 | (uint64_t)i << 16 | (uint64_t)(j0 + 1)});
             };
             int j = 0;
+#if defined(__SSE__)
             for (; j + 4 <= nb; j += 4) {   // 4 scores per compare; most fail
                 unsigned mk = (unsigned)_mm_movemask_ps(_mm_cmpge_ps(_mm_loadu_ps(r + j), vthr));
                 while (mk) {
@@ -268,6 +273,7 @@ void people_global_sort(People& people, AssemblyScratch& sc, const PoseModelInfo
                     mk &= mk - 1;
                 }
             }
+#endif
             for (; j < nb; ++j)
                 if (r[j] >= thr) take(j);
         }

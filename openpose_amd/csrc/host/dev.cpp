@@ -1,4 +1,6 @@
 // dev.cpp -- kernel-variant switch table behind opk_dev_set / opk::dev_switch (common.h).
+#include <cstdarg>
+#include <cstdio>
 #include <map>
 #include <mutex>
 #include <string>
@@ -22,6 +24,24 @@ int dev_switch(const char* key, int dflt)
     std::lock_guard<std::mutex> lock(g_mu);
     const auto it = table().find(key);
     return it == table().end() ? dflt : it->second;
+}
+
+namespace {
+thread_local LaunchLog* t_log = nullptr;
+}
+
+void attach_launch_log(LaunchLog* log) { t_log = log; }
+LaunchLog* launch_log() { return t_log; }
+
+void note_launch(const char* fmt, ...)
+{
+    if (!t_log) return;
+    char buf[160];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_log->lines.push_back(t_log->layer + "\t" + buf);
 }
 
 }  // namespace opk

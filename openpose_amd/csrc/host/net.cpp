@@ -183,6 +183,26 @@ void NetHip::plan(const std::vector<LayerDesc>& layers)
     }
     image_buf_ = (int)bufs_.size();
     bufs_.push_back(BufSpec{0, 32});
+    // where every named top lives (blob(): inspection and per-layer tests)
+    for (const auto& kv : blobs) {
+        const Blob& B = kv.second;
+        BlobLoc loc;
+        loc.ch = B.ch;
+        loc.level = B.level;
+        if (kv.first == "image") continue;
+        if (out_concat && kv.first == output_blob_) {
+            loc.out32 = true;
+        } else if (!B.places.empty()) {
+            loc.buf = B.places[0].buf;
+            loc.coff = B.places[0].coff;
+        } else if (B.conv >= 0 && convs_[B.conv].out32_coff >= 0) {
+            loc.out32 = true;
+            loc.coff = convs_[B.conv].out32_coff;
+        } else {
+            continue;
+        }
+        blob_loc_[kv.first] = loc;
+    }
     for (auto& c : convs_) {
         if (c.from_image) {
             c.in = Placement{image_buf_, 0};
@@ -416,7 +436,13 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
     S.fused1 = fuse1_.a >= 0 && dev_switch("CONV1_FUSED", 1) != 0 && border_ == 1 &&
                conv1_fused_supported(h, w, 64, 64);
     // HEAD_FUSE=0 (opk_dev_set, A/B tests): Mconv6 and Mconv7 as two conv3 launches
+    // Positions are decoded by float-reciprocal division in conv_head_kernel, exact below 2^24:
+    // larger batches run the pairs unfused.
     S.fusedh = !heads_.empty() && dev_switch("HEAD_FUSE", 1) != 0;
+    for (const auto& fh : heads_) {
+        const int L = convs_[fh.a].level;
+        S.fusedh = S.fusedh && (long)n * (lh_[L] + 2) * (lw_[L] + 2) < (1L << 24);
+    }
     // POOL_FUSE=0 (opk_dev_set, A/B tests): the pools as their own kernels
     S.poolfused.assign(pools_.size(), 0);
     for (size_t q = 0; q < pools_.size(); ++q) {
@@ -543,8 +569,63 @@ void NetHip::forward_on(const float* input, int n, int h, int w, hipStream_t st,
     if (timed) timer_.end(st);
 }
 
+void NetHip::blob(const std::string& name, int f0, int nf, float* host, int shape[4]) const
+{
+    OPK_CHECK_ARG(cur_ != nullptr, "no forward yet");
+    const auto it = blob_loc_.find(name);
+    OPK_CHECK_ARG(it != blob_loc_.end(), "no blob named " + name);
+    const BlobLoc& L = it->second;
+    const ShapePlan& S = *cur_;
+    OPK_CHECK_ARG(f0 >= 0 && nf > 0 && f0 + nf <= S.n, "frames out of range");
+    const int H = S.lh[L.level], W = S.lw[L.level];
+    if (shape) {
+        shape[0] = nf; shape[1] = L.ch; shape[2] = H; shape[3] = W;
+    }
+    if (!host) return;
+    ctx_->bind();
+    OPK_HIP(hipStreamSynchronize(ctx_->stream));
+    const size_t hw = (size_t)H * W;
+    if (L.out32) {
+        OPK_CHECK_ARG(L.level == out_level_, name + ": not at the output resolution");
+        for (int f = 0; f < nf; ++f)
+            OPK_HIP(hipMemcpy(host + (size_t)f * L.ch * hw,
+                              S.out32 + ((size_t)(f0 + f) * out_c_ + L.coff) * hw,
+                              (size_t)L.ch * hw * 4, hipMemcpyDeviceToHost));
+        return;
+    }
+    OPK_CHECK_ARG(S.base[L.buf] != nullptr,
+                  name + ": kept on chip by a fused kernel (not materialised at this shape)");
+    const int B = border_, Wp = W + 2 * B, Hp = H + 2 * B, cs = bufs_[L.buf].cs;
+    const size_t frame_elems = (size_t)Hp * Wp * cs;
+    std::vector<uint16_t> raw(frame_elems * nf);
+    OPK_HIP(hipMemcpy(raw.data(), S.base[L.buf] + (size_t)f0 * frame_elems, raw.size() * 2,
+                      hipMemcpyDeviceToHost));
+    for (int f = 0; f < nf; ++f)
+        for (int y = 0; y < H; ++y)
+            for (int x = 0; x < W; ++x) {
+                const uint16_t* src = raw.data() + f * frame_elems + ((size_t)(y + B) * Wp + x + B) * cs + L.coff;
+                for (int c = 0; c < L.ch; ++c)
+                    host[((size_t)f * L.ch + c) * hw + (size_t)y * W + x] = (float)__builtin_bit_cast(_Float16, src[c]);
+            }
+}
+
 void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, int w, hipStream_t st)
 {
+    const bool logging = dev_switch("LAUNCH_LOG", 0) != 0;
+    if (logging) {
+        log_.lines.clear();
+        attach_launch_log(&log_);
+    }
+    struct Detach {
+        bool on;
+        ~Detach() { if (on) attach_launch_log(nullptr); }
+    } detach{logging};
+    forward_steps(S, input, n, h, w, st);
+}
+
+void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w, hipStream_t st)
+{
+    LaunchLog* log = launch_log();
     const std::vector<uint16_t*>& ptr = S.base;
     const std::vector<int>& lh_ = S.lh;
     const std::vector<int>& lw_ = S.lw;
@@ -572,6 +653,7 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
         fa.OH = lh_[1];
         fa.OW = lw_[1];
         fa.actmax = a.slope01 && b.slope01 && dev_switch("EPI_MAX", 1) != 0;
+        if (log) log->layer = a.info.name + "+" + b.info.name + "+pool";
         launch_conv1_fused(fa, std::min(cus_, std::max(1, dev_switch("GRID_CUS", cus_))), st);
         first = 3;
     }
@@ -612,10 +694,12 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
                 h.out32_coff = b.out32_coff;
                 // persistent grid (HEAD_PERSIST=0: one workgroup per tile, dev A/B)
                 h.cus = dev_switch("HEAD_PERSIST", 1) != 0 ? a.cus : 0;
+                if (log) log->layer = c.info.name + "+" + cb.info.name;
                 launch_conv_head(h, st);
                 ++si;   // Mconv7 ran inside
                 continue;
             }
+            if (log) log->layer = c.info.name + (a.pool ? "+pool" : "");
             if (c.from_image) {
                 launch_conv_image(a, input, st);
             } else {
@@ -627,6 +711,7 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
             if (S.poolfused[s.idx]) continue;   // ran in its conv's epilogue
             const PoolPlan& p = pools_[s.idx];
             const int L = p.level_in;
+            if (log) log->layer = "pool";
             launch_maxpool2(ptr[p.out_buf], ptr[p.in_buf], n, lh_[L], lw_[L],
                             bufs_[p.in_buf].cs, lh_[L + 1], lw_[L + 1], st, border_);
         }

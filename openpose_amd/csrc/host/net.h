@@ -55,6 +55,15 @@ public:
     void set_timing(bool on);
     void read_timing(int* count, double* total_ms);
 
+    // caffe::Net::blob_by_name for the last forward (inspection / per-layer tests): frames
+    // [f0, f0 + nf) of a named conv / pool / concat top as fp32 NCHW host [nf][ch][h][w], read from
+    // its padded NHWC fp16 buffer (or the fp32 net output).  Blobs the fused kernels keep on chip
+    // (conv1_1 / conv1_2 in conv1_fused, a pooled conv's un-pooled output, Mconv6 in conv_head)
+    // throw.  host == nullptr: shape only.
+    void blob(const std::string& name, int f0, int nf, float* host, int shape[4]) const;
+    // kernels launched by the last forward run while the dev switch LAUNCH_LOG was 1
+    const std::vector<std::string>& launches() const { return log_.lines; }
+
 private:
     struct Placement { int buf; int coff; };
     struct BufSpec { int level; int cs; };
@@ -94,6 +103,7 @@ private:
 
     void plan(const std::vector<LayerDesc>& layers);
     void forward_launches(ShapePlan& S, const float* input, int n, int h, int w, hipStream_t st);
+    void forward_steps(ShapePlan& S, const float* input, int n, int h, int w, hipStream_t st);
     ShapePlan* shape_plan(int n, int h, int w, hipStream_t zero_stream = nullptr);
 
     Context* ctx_;
@@ -117,6 +127,10 @@ private:
     std::vector<int> pool_conv_;
     int cus_ = 256;               // compute units (persistent-kernel grid)
     int border_ = 1;              // zero border of every padded image (widest conv pad, >= 1)
+
+    struct BlobLoc { int buf = -1, coff = 0, ch = 0, level = 0; bool out32 = false; };
+    std::map<std::string, BlobLoc> blob_loc_;   // every named top (plan)
+    LaunchLog log_;
 
     std::vector<std::unique_ptr<ShapePlan>> shapes_;   // oldest first
     ShapePlan* cur_ = nullptr;    // shape of the last forward

@@ -59,11 +59,11 @@ PoseHip::~PoseHip()
         (void)hipStreamSynchronize(ctx_->stream);
         (void)hipStreamDestroy(copy_);
     }
-    if (warp_) {
-        (void)hipStreamSynchronize(warp_);
-        (void)hipStreamDestroy(warp_);
-        (void)hipEventDestroy(warp_done_);
+    if (post_) {
+        (void)hipStreamSynchronize(post_);
+        (void)hipStreamDestroy(post_);
         (void)hipEventDestroy(nets_done_);
+        (void)hipEventDestroy(post_done_);
     }
     for (auto& s : slots_)
         if (s.done) (void)hipEventDestroy(s.done);
@@ -206,10 +206,33 @@ void PoseHip::submit(const float* frames, int n, int net_h, int net_w, int prod_
 {
     OPK_CHECK_ARG(net_ != nullptr, "no network: use forward_net_output (poseNetOutput path)");
     OPK_CHECK_ARG(count_ < 2, "two batches already in flight: collect first");
+    ctx_->bind();
+    wait_post(ctx_->stream);   // the net overwrites the output the last post-processing reads
     net_->forward(frames, n, net_h, net_w);
-    mark_nets_done();
-    submit_net_output(net_->output(), n, net_->out_h(), net_->out_w(), net_h, net_w, prod_w,
-                      prod_h);
+    const NetOutput o{net_->output(), net_->out_h(), net_->out_w()};
+    submit_outputs(&o, 1, n, net_h, net_w, prod_w, prod_h, true);
+}
+
+hipStream_t PoseHip::post_stream(bool own_net)
+{
+    if (!own_net || ctx_->device < 0 || dev_switch("POST_STREAM", 1) == 0) {
+        wait_post(ctx_->stream);   // shared scratch / slots with a post-processing on post_
+        return ctx_->stream;
+    }
+    if (!post_) {
+        OPK_HIP(hipStreamCreateWithFlags(&post_, hipStreamNonBlocking));
+        OPK_HIP(hipEventCreateWithFlags(&nets_done_, hipEventDisableTiming));
+        OPK_HIP(hipEventCreateWithFlags(&post_done_, hipEventDisableTiming));
+    }
+    // everything on the context stream so far: the caller's work and this batch's nets
+    OPK_HIP(hipEventRecord(nets_done_, ctx_->stream));
+    OPK_HIP(hipStreamWaitEvent(post_, nets_done_, 0));
+    return post_;
+}
+
+void PoseHip::wait_post(hipStream_t s)
+{
+    if (post_recorded_) OPK_HIP(hipStreamWaitEvent(s, post_done_, 0));
 }
 
 void PoseHip::set_input(int net_w, int net_h, float dyn, int scale_number, double scale_gap)
@@ -236,32 +259,17 @@ void PoseHip::submit_frames(const uint8_t* frames, int n, int w, int h, size_t s
     scale_and_size(w, h, in_net_w_, in_net_h_, dyn_, scale_number_, scale_gap_, scales, input_hw_);
     const float* ptrs[kMaxResizeSources];
     int hw[2 * kMaxResizeSources];
-    // the warps run on their own stream after the previous batch's nets (the readers of these
-    // input buffers), i.e. beside that batch's post-processing; the nets wait for them
-    const bool side = dev_switch("WARP_STREAM", 1) != 0;
-    if (side && !warp_) {
-        ctx_->bind();
-        OPK_HIP(hipStreamCreateWithFlags(&warp_, hipStreamNonBlocking));
-        OPK_HIP(hipEventCreateWithFlags(&warp_done_, hipEventDisableTiming));
-        OPK_HIP(hipEventCreateWithFlags(&nets_done_, hipEventDisableTiming));
-    }
-    hipStream_t ws = side ? warp_ : ctx_->stream;
-    if (side) {
-        // (no batch recorded yet: everything queued on the context stream so far)
-        if (!nets_recorded_) OPK_HIP(hipEventRecord(nets_done_, ctx_->stream));
-        OPK_HIP(hipStreamWaitEvent(warp_, nets_done_, 0));
-    }
+    // the warps run on the context stream, after whatever the caller queued there (e.g. the
+    // upload of these frames) and after the previous batch's nets (the readers of the input
+    // buffers); the previous batch's post-processing runs beside them on post_
+    ctx_->bind();
     for (int i = 0; i < scale_number_; ++i) {
         const int nw = input_hw_[2 * i], nh = input_hw_[2 * i + 1];
         float* x = static_cast<float*>(inputs_[i].get((size_t)n * 3 * nh * nw * sizeof(float)));
-        cvmat_to_input(ctx_, x, frames, n, w, h, step, scales[i], nw, nh, 1, ws);
+        cvmat_to_input(ctx_, x, frames, n, w, h, step, scales[i], nw, nh, 1, ctx_->stream);
         ptrs[i] = x;
         hw[2 * i] = nh;
         hw[2 * i + 1] = nw;
-    }
-    if (side) {
-        OPK_HIP(hipEventRecord(warp_done_, warp_));
-        OPK_HIP(hipStreamWaitEvent(ctx_->stream, warp_done_, 0));
     }
     inputs_n_ = n;
     for (int i = 0; i < scale_number_; ++i) map_ratios_[i] = (float)scales[i];
@@ -304,6 +312,8 @@ void PoseHip::submit_multi(const float* const* frames, const int* net_hw, int ns
     // plan and output buffer in NetHip, so the outputs coexist until the merge reads them
     std::vector<NetOutput> outs(nscales);
     for (int i = 0; i < nscales; ++i) OPK_CHECK_ARG(frames[i] != nullptr, "NULL scale input");
+    ctx_->bind();
+    wait_post(ctx_->stream);   // the nets overwrite the outputs the last post-processing reads
     // the scales' nets are independent until the merge: scales 1.. run on streams of their own
     // beside scale 0 (small nets leave most CUs idle on their own), each shape with its own plan
     // and buffers; the context stream waits for all of them before the merge.  Shapes that repeat
@@ -341,27 +351,18 @@ void PoseHip::submit_multi(const float* const* frames, const int* net_hw, int ns
         for (int i = 1; i < nscales; ++i) OPK_HIP(hipStreamWaitEvent(s, join_[i - 1], 0));
         net_->time_end(s);
     }
-    mark_nets_done();
-    submit_outputs(outs.data(), nscales, n, net_hw[0], net_hw[1], prod_w, prod_h);
-}
-
-void PoseHip::mark_nets_done()
-{
-    // the nets of this batch have read their inputs: the next batch's warps may overwrite them
-    if (!warp_) return;
-    OPK_HIP(hipEventRecord(nets_done_, ctx_->stream));
-    nets_recorded_ = true;
+    submit_outputs(outs.data(), nscales, n, net_hw[0], net_hw[1], prod_w, prod_h, true);
 }
 
 void PoseHip::submit_net_output(const float* net_out, int n, int oh, int ow, int net_h,
                                 int net_w, int prod_w, int prod_h)
 {
     const NetOutput o{net_out, oh, ow};
-    submit_outputs(&o, 1, n, net_h, net_w, prod_w, prod_h);
+    submit_outputs(&o, 1, n, net_h, net_w, prod_w, prod_h, false);
 }
 
 void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_h, int net_w,
-                             int prod_w, int prod_h)
+                             int prod_w, int prod_h, bool own_net)
 {
     const PoseModelInfo& m = pose_model(model_);
     const int C = m.heat_channels();
@@ -370,8 +371,8 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
         OPK_CHECK_ARG(outs[i].ptr && outs[i].h > 0 && outs[i].w > 0, "empty net output");
     OPK_CHECK_ARG(count_ < 2, "two batches already in flight: collect first");
     ctx_->bind();
-    hipStream_t s = ctx_->stream;
     Slot& sl = slots_[(head_ + count_) & 1];
+    const hipStream_t s = post_stream(own_net);
     timer_.begin(s);
     if (overlay_) {   // synthetic people on the first scale's output
         const size_t out_elems = (size_t)n * C * outs[0].h * outs[0].w;
@@ -429,7 +430,12 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
     const int P1 = kMaxPeaks + 1;
     const size_t peak_floats = (size_t)m.parts * P1 * 3;
     float* peaks = static_cast<float*>(sl.peaks.get((size_t)n * peak_floats * 4));
-    launch_nms(peaks, ctx_->nms_candidates(n, m.parts), heat, n, m.parts, P1, nms_th, off, off, s,
+    const size_t cand_bytes = nms_scratch_ints(n, m.parts) * sizeof(int);
+    if (cand_bytes > cand_.bytes) {   // the counters reset themselves after every launch
+        cand_.get(cand_bytes);
+        OPK_HIP(hipMemsetAsync(cand_.ptr, 0, cand_bytes, s));
+    }
+    launch_nms(peaks, static_cast<int*>(cand_.ptr), heat, n, m.parts, P1, nms_th, off, off, s,
                maps_ == kMapsCuda);
 
     // 4. connector, device half: PAF integrals of every candidate pair into compact records
@@ -445,6 +451,10 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
                               reject, near, s);
     timer_.end(s);
     OPK_HIP(hipEventRecord(sl.done, s));
+    if (s == post_) {
+        OPK_HIP(hipEventRecord(post_done_, post_));
+        post_recorded_ = true;
+    }
     sl.n = n;
     sl.H = H;
     sl.W = W;
@@ -482,27 +492,36 @@ int PoseHip::collect()
     // whole below
     std::vector<std::vector<int>> offsets(n);
     std::vector<size_t> over_at(n, (size_t)-1);
-    int over_first = -1, over_last = -1;
-    size_t over_w = 0;
+    std::vector<int> total(n);
     for (int f = 0; f < n; ++f) {
-        const int total = compact_offsets(m, hp + (size_t)f * peak_floats, kMaxPeaks, offsets[f]);
-        OPK_CHECK_ARG((int)hr[(size_t)f * K] == total, "PAF record count differs from the peak counts");
-        if ((size_t)total + 1 > K) {
-            if (over_first < 0) over_first = f;
-            over_last = f;
-            over_w = std::max(over_w, (size_t)total + 1);
-        }
+        total[f] = compact_offsets(m, hp + (size_t)f * peak_floats, kMaxPeaks, offsets[f]);
+        OPK_CHECK_ARG((int)hr[(size_t)f * K] == total[f], "PAF record count differs from the peak counts");
     }
-    if (over_first >= 0) {
-        // records longer than the eagerly copied head (many-people / BODY_135 frames): one 2-D
-        // copy of the longest such record's length for the frame range that holds them
-        const size_t rows = (size_t)(over_last - over_first + 1);
-        float* ho = static_cast<float*>(overflow_.get(rows * over_w * 4));
-        OPK_HIP(hipMemcpy2DAsync(ho, over_w * 4,
-                                 static_cast<const float*>(sl.records.ptr) + (size_t)over_first * rf,
-                                 rf * 4, over_w * 4, rows, hipMemcpyDeviceToHost, copy_));
-        for (int f = over_first; f <= over_last; ++f)
-            if ((int)hr[(size_t)f * K] + 1 > (int)K) over_at[f] = (size_t)(f - over_first) * over_w;
+    // records longer than the eagerly copied head (many-people / BODY_135 frames): one 2-D copy
+    // per run of consecutive long frames, at the width of the run's longest record, so frames
+    // between two distant long ones are not copied
+    struct Run { int f0, f1; size_t w, at; };
+    std::vector<Run> runs;
+    size_t over_floats = 0;
+    for (int f = 0; f < n; ++f) {
+        if ((size_t)total[f] + 1 <= K) continue;
+        if (runs.empty() || runs.back().f1 != f - 1) runs.push_back(Run{f, f, 0, 0});
+        runs.back().f1 = f;
+        runs.back().w = std::max(runs.back().w, (size_t)total[f] + 1);
+    }
+    for (auto& r : runs) {
+        r.at = over_floats;
+        over_floats += (size_t)(r.f1 - r.f0 + 1) * r.w;
+    }
+    if (!runs.empty()) {
+        float* ho = static_cast<float*>(overflow_.get(over_floats * 4));
+        for (const auto& r : runs) {
+            OPK_HIP(hipMemcpy2DAsync(ho + r.at, r.w * 4,
+                                     static_cast<const float*>(sl.records.ptr) + (size_t)r.f0 * rf,
+                                     rf * 4, r.w * 4, (size_t)(r.f1 - r.f0 + 1),
+                                     hipMemcpyDeviceToHost, copy_));
+            for (int f = r.f0; f <= r.f1; ++f) over_at[f] = r.at + (size_t)(f - r.f0) * r.w;
+        }
         OPK_HIP(hipStreamSynchronize(copy_));
     }
     // people assembly: frames are independent (connectBodyParts* per frame), so they run on the

@@ -16,6 +16,8 @@ namespace opk {
 //              the context stream and return;
 //   collect -- wait for the oldest submitted batch and assemble its people on the host.
 // With one batch in flight, the host assembly of batch i overlaps the device work of batch i+1.
+// Stream contract: every input (frames, net inputs, an injected net output, the overlay) is read
+// in order after the work the caller queued on the context stream before the submit call.
 // forward() = submit + collect.
 class PoseHip {
 public:
@@ -99,7 +101,7 @@ private:
         int h, w;
     };
     void submit_outputs(const NetOutput* outs, int nscales, int n, int net_h, int net_w,
-                        int prod_w, int prod_h);
+                        int prod_w, int prod_h, bool own_net);
     size_t record_floats() const;        // per frame: 1 + every candidate pair of the model
 
     Context* ctx_;
@@ -120,12 +122,20 @@ private:
     const float* overlay_ = nullptr;
     float upsampling_ = 0.f;
     hipStream_t copy_ = nullptr;         // D2H of collected batches (overlaps the next batch)
-    // raw-frame path: the warp of batch i+1 runs on its own stream once the nets of batch i are
-    // done with the net inputs, beside batch i's post-processing (WARP_STREAM=0: in order)
-    hipStream_t warp_ = nullptr;
-    hipEvent_t warp_done_ = nullptr, nets_done_ = nullptr;
-    bool nets_recorded_ = false;
-    void mark_nets_done();
+    // When this PoseHip runs the net itself (submit, submit_multi, submit_frames), the
+    // post-processing of a batch (overlay, NMS, PAF integrals) runs on post_, ordered after the
+    // batch's nets on the context stream.  Everything the caller enqueues on the context stream
+    // -- frame uploads included -- stays ordered before the next batch's warp and nets, and the
+    // next batch's warp overlaps this batch's post-processing; the next nets (which overwrite
+    // the net output post_ reads) wait for post_done_.  POST_STREAM=0: all on the context stream.
+    // The injection path (submit_net_output: a caller-owned net output) stays on the context
+    // stream, so a caller may rewrite that buffer on its stream after submit.
+    hipStream_t post_ = nullptr;
+    hipEvent_t nets_done_ = nullptr, post_done_ = nullptr;
+    bool post_recorded_ = false;
+    hipStream_t post_stream(bool own_net);   // the stream a batch's post-processing runs on
+    void wait_post(hipStream_t s);           // s after the last recorded post-processing
+    DevBuf cand_;                            // NMS candidate counters (zeroed once, self-resetting)
     // multi-scale: the nets of scales 1.. run on their own streams beside scale 0's
     hipStream_t scale_streams_[kMaxResizeSources - 1] = {};
     hipEvent_t fork_ = nullptr, join_[kMaxResizeSources - 1] = {};

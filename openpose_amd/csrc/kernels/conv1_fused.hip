@@ -334,6 +334,7 @@ void launch_conv1_fused(const Conv1FusedArgs& a, int workgroups, hipStream_t str
     const long tiles = (long)a.frames * ((a.W + TC - 1) / TC) * ((a.H + TR - 1) / TR);
     OPK_CHECK_ARG(tiles < (1L << 31), "conv1 fusion: too many tiles");
     const int grid = (int)std::min<long>(tiles, workgroups > 0 ? workgroups : 256);
+    note_launch("conv1_fused_kernel<%d>", a.actmax ? 1 : 0);
     if (a.actmax) hipLaunchKernelGGL(conv1_fused_kernel<true>, dim3(grid), dim3(NT), 0, stream, a);
     else hipLaunchKernelGGL(conv1_fused_kernel<false>, dim3(grid), dim3(NT), 0, stream, a);
     OPK_LAUNCH_CHECK();

@@ -814,7 +814,10 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
             // 16-byte epilogue stores (measured in tools/ab_asmr.sh; CONV3P_WIDE=0: dwordx2)
             const bool wide = dev_switch("CONV3P_WIDE", 1) != 0;
 #define OPK3P_LAUNCH(BN_, ASMR_, WIDE_)                                                        \
-    hipLaunchKernelGGL((conv3p_kernel<BN_, ASMR_, WIDE_>), dim3(G), dim3(1024), 0, stream, a)
+    do {                                                                                       \
+        note_launch("conv3p_kernel<%d,%d,%d>", BN_, (int)ASMR_, (int)WIDE_);                   \
+        hipLaunchKernelGGL((conv3p_kernel<BN_, ASMR_, WIDE_>), dim3(G), dim3(1024), 0, stream, a); \
+    } while (0)
             if (s.bn == 96) {
                 if (asmr) { if (wide) OPK3P_LAUNCH(96, true, true); else OPK3P_LAUNCH(96, true, false); }
                 else OPK3P_LAUNCH(96, false, true);
@@ -828,22 +831,25 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
         }
     }
 #define OPK3_LAUNCH(BM_, BN_, HR_, TAPU_, MINB_, KS_)                                          \
-    hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, MINB_, KS_>), grid, dim3(512), 0,   \
-                       stream, a)
+    do {                                                                                       \
+        note_launch("conv3_kernel<%d,%d,%d,%d,%d,%d>", BM_, BN_, HR_, TAPU_, MINB_, KS_);       \
+        hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, MINB_, KS_>), grid, dim3(512), 0, \
+                           stream, a);                                                         \
+    } while (0)
+#define OPK3_LAUNCH16(BM_, BN_, HR_, TAPU_, KS_)                                                \
+    do {                                                                                       \
+        note_launch("conv3_kernel<%d,%d,%d,%d,1,%d,16>", BM_, BN_, HR_, TAPU_, KS_);           \
+        hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, 1, KS_, 16>), grid, dim3(1024), 0, \
+                           stream, a);                                                         \
+    } while (0)
     if (ks == 7) {
         if (s.bn == 64) OPK3_LAUNCH(256, 64, 1024, 1, 1, 7);
         else if (s.bn == 96) OPK3_LAUNCH(256, 96, 1024, 1, 1, 7);
         else OPK3_LAUNCH(256, 128, 1024, 1, 1, 7);
     } else if (ks == 1) {
-        if (s.nw == 16 && s.bn == 256)
-            hipLaunchKernelGGL((conv3_kernel<256, 256, 256, 1, 1, 1, 16>), grid, dim3(1024), 0,
-                               stream, a);
-        else if (s.nw == 16 && s.bn == 64)
-            hipLaunchKernelGGL((conv3_kernel<512, 64, 512, 1, 1, 1, 16>), grid, dim3(1024), 0,
-                               stream, a);
-        else if (s.nw == 16)
-            hipLaunchKernelGGL((conv3_kernel<512, 128, 512, 1, 1, 1, 16>), grid, dim3(1024), 0,
-                               stream, a);
+        if (s.nw == 16 && s.bn == 256) OPK3_LAUNCH16(256, 256, 256, 1, 1);
+        else if (s.nw == 16 && s.bn == 64) OPK3_LAUNCH16(512, 64, 512, 1, 1);
+        else if (s.nw == 16) OPK3_LAUNCH16(512, 128, 512, 1, 1);
         else if (s.bn == 64) OPK3_LAUNCH(256, 64, 256, 1, 2, 1);
         else if (s.bn == 96) OPK3_LAUNCH(256, 96, 256, 1, 2, 1);
         else OPK3_LAUNCH(256, 128, 256, 1, 2, 1);
@@ -851,19 +857,16 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
         if (s.minb == 2) OPK3_LAUNCH(256, 64, 448, 1, 2, 3);
         else OPK3_LAUNCH(512, 64, 768, 3, 1, 3);
     } else if (s.bn == 96) {
-        if (s.nw == 16)
-            hipLaunchKernelGGL((conv3_kernel<512, 96, 704, 3, 1, 3, 16>), grid, dim3(1024), 0,
-                               stream, a);
+        if (s.nw == 16) OPK3_LAUNCH16(512, 96, 704, 3, 3);
         else if (s.minb == 2) OPK3_LAUNCH(256, 96, 448, 1, 2, 3);
         else OPK3_LAUNCH(256, 96, 512, 3, 1, 3);
     } else {
-        if (s.nw == 16)
-            hipLaunchKernelGGL((conv3_kernel<512, 128, 704, 3, 1, 3, 16>), grid, dim3(1024), 0,
-                               stream, a);
+        if (s.nw == 16) OPK3_LAUNCH16(512, 128, 704, 3, 3);
         else if (s.minb == 2) OPK3_LAUNCH(256, 128, 448, 1, 2, 3);
         else OPK3_LAUNCH(256, 128, 512, 3, 1, 3);
     }
 #undef OPK3_LAUNCH
+#undef OPK3_LAUNCH16
     OPK_LAUNCH_CHECK();
 }
 

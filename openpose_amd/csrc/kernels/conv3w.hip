@@ -503,6 +503,7 @@ void launch_conv3w(const ConvArgs& a, hipStream_t stream)
     // (the DMA-after-barrier A/B variant only with the select activation)
 #define OPKW_LAUNCH(BN_, DE_, MX_)                                                                 \
     do {                                                                                          \
+        note_launch("conv3w_kernel<%d,%d,%d,%d>", BN_, (int)DE_, (int)MX_, b.bufst);              \
         if (b.bufst)                                                                              \
             hipLaunchKernelGGL((conv3w_kernel<BN_, DE_, MX_, true>), dim3(G), dim3(64 * kW_NW), 0, stream, b); \
         else                                                                                      \

@@ -56,6 +56,10 @@ constexpr int k8_BM = 512, k8_HR = 688, k8_NW = 8;
 // MX: the activation as max(t, t*m) (ConvArgs::actmax; conv3_dev.h act_pick)
 // BST: one destination, epilogue stores through a buffer resource (ConvArgs::bufst)
 typedef unsigned int opk8_u4 __attribute__((ext_vector_type(4)));
+#ifndef OPK_FAULT_POOL
+#define OPK_FAULT_POOL 0
+#endif
+
 template <int BN, int NB, bool POOL, bool MX, bool BST>
 __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a)
 {
@@ -386,15 +390,19 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                     for (int h = 0; h < 2; ++h) {
                         const float4_t t = acc[i][j + h] + bq[h];
                         const float4_t tm = t * mq[h];
-                        float v[4];
+                        float v[4], o[4];
 #pragma unroll
                         for (int r = 0; r < 4; ++r) {
                             v[r] = act_pick<MX>(t[r], tm[r]);
                             // the column pair's max: lane ^ 1 holds the next position
-                            const float o = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                            o[r] = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
                                 __builtin_bit_cast(int, v[r]), 0xB1, 0xF, 0xF, false));
-                            v[r] = fmaxf(v[r], o);
                         }
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)   // (OPK_FAULT_POOL: a dev variant that
+                            // reproduces round 3's miscompile -- element 0's partner for all four
+                            // -- to show the per-layer test catches it; never built for the product)
+                            v[r] = fmaxf(v[r], o[OPK_FAULT_POOL ? 0 : r]);
                         pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
                         pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
                     }
@@ -555,6 +563,7 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
     b.bufst = a.ndst == 1 && (pool ? pextent : extent) < (1L << 31) - 4096 && dev_switch("BUFST", 1) != 0;
 #define OPK8_LAUNCH2(BN_, NB_, P_, MX_)                                                          \
     do {                                                                                        \
+        note_launch("conv3w8_kernel<%d,%d,%d,%d,%d>", BN_, NB_, (int)P_, (int)MX_, b.bufst);      \
         if (b.bufst)                                                                            \
             hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, MX_, true>), dim3(G), dim3(64 * k8_NW), 0, stream, b); \
         else                                                                                    \

@@ -437,7 +437,8 @@ void launch_conv_head(const HeadArgs& a, hipStream_t stream)
     OPK_CHECK_ARG(conv_head_supported(a.n1, a.n2, a.cin_pad), "conv_head: N1 256/512, N2 <= 64");
     OPK_CHECK_ARG(a.ndst <= kConvMaxDst, "conv_head: too many destinations");
     const long total = (long)a.frames * (a.H + 2) * (a.W + 2);
-    OPK_CHECK_ARG(total < (1L << 30), "conv_head: too many positions");
+    // phase 3 decodes positions by float-reciprocal division, exact below 2^24 (conv3_dev.h)
+    OPK_CHECK_ARG(total < (1L << 24), "conv_head: too many positions (split the batch)");
     const long ntiles = (total + kH_BM - 1) / kH_BM;
     // persistent at N1 = 512 (one 143 KB workgroup per CU: 4-5 % faster than one workgroup per
     // tile); at N1 = 256 two per-tile workgroups share a CU and the persistent grid measured
@@ -447,6 +448,7 @@ void launch_conv_head(const HeadArgs& a, hipStream_t stream)
     const dim3 blk(64 * kH_NW);
 #define OPKH_LAUNCH2(N1_, NF2_, MX_)                                                            \
     do {                                                                                       \
+        note_launch("conv_head_kernel<%d,%d,%d,%d>", N1_, NF2_, (int)persist, (int)MX_);        \
         if (persist) hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, true, MX_>), dim3(G), blk, 0, stream, a); \
         else hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, false, MX_>), dim3(G), blk, 0, stream, a); \
     } while (0)

@@ -126,6 +126,7 @@ void launch_conv_image(const ConvArgs& a, const float* image, hipStream_t stream
         OPK_CHECK_ARG(((a.dst_cs[d] | a.dst_coff[d]) & 3) == 0, "conv_image: 8-byte aligned slices");
     const long blocks = (long)a.frames * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
     OPK_CHECK_ARG(blocks > 0 && blocks < (1L << 31), "conv_image: bad sizes");
+    note_launch("conv_image_kernel");
     hipLaunchKernelGGL(conv_image_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a, image);
     OPK_LAUNCH_CHECK();
 }

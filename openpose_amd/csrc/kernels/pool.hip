@@ -63,6 +63,7 @@ void launch_maxpool2(uint16_t* out, const uint16_t* in, int frames, int H, int W
     OPK_CHECK_ARG(border >= 1, "border >= 1");
     OPK_CHECK_ARG(C % 8 == 0, "pool channels must be a multiple of 8");
     const size_t total = (size_t)frames * OH * OW * (C / 8);
+    note_launch("maxpool2_kernel");
     hipLaunchKernelGGL(maxpool2_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream,
                        out, in, frames, H, W, C, OH, OW, border);
     OPK_LAUNCH_CHECK();

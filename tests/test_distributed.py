@@ -136,3 +136,17 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, bench, "--gpus", "4"], env=env, capture_output=True,
                        text=True, timeout=120)
     assert r.returncode != 0 and "WORLD_SIZE=2" in r.stderr
+
+
+def test_bench_content_depends_on_global_batch_only():
+    """bench.py's synthetic input of a frame depends only on its global batch index (step x world
+    + rank, the frame ids RecordGather assigns): every world size sees the same content per global
+    batch, and each rank holds exactly the contents its batches use."""
+    import bench
+    for world in (1, 2, 4, 8):
+        for rank in range(world):
+            have = set(bench.contents_of_rank(rank, world))
+            for step in range(12):
+                k = step * world + rank
+                assert k % bench.CONTENTS in have
+            assert have == {(s * world + rank) % bench.CONTENTS for s in range(12)}

@@ -22,6 +22,7 @@ pytestmark = pytest.mark.gpu
 SMALL_TOL = 4e-3      # relative L2, graphs of <= 6 layers
 BODY25_TOL = 5e-3     # relative L2, the full 114-conv network (measured 1.5-2.5e-3)
 CHANNEL_TOL = 2e-2    # relative L2 of any single output channel of a frame (measured < 6e-3)
+FP16_EMU_TOL = 5e-4   # relative L2 vs the fp16-storage emulation (only summation order differs)
 
 
 def rel_l2(a, b):
@@ -110,13 +111,19 @@ def channel_errors(got, ref):
 
 
 def test_body25_bench_geometry_vs_oracle(ctx):
-    """The net at the bench's shape (64 x 3 x 368 x 656: the persistent 16-wave 512-row tiles,
-    the 256x256 1x1 tiles, the fused conv1 kernel and the strip geometry the bench runs), frames
-    0, 31 and 63 against the fp32 oracle (frames are independent; every tile row of the first
-    and last frames is covered), whole-frame and per-channel tolerance."""
+    """The net at the bench's shape (the tile-aligned batch of bench.py -- 130 x 3 x 368 x 656 on a
+    256-CU MI355X: the persistent stage-layer kernels, the 8-wave VGG / pooled kernels, the fused
+    heads and conv1, with the bench's grids and tile walk), frames 0, the middle one and the last
+    (first, middle and last tile rounds) against the fp32 oracle, whole-frame and per-channel
+    tolerance; and against the fp16-storage emulation (oracle/fp16.py: what the kernels compute up
+    to the fp32 summation order), which it must match ~10x more closely than the fp32 oracle.
+    Layer-by-layer bounds: tests/test_gpu_layers.py."""
+    from bench import tile_aligned_batch
+    from oracle import fp16 as emu
     graph = body25.layers()
     params = synth.he_weights(graph, seed=13)
-    n, h, w = 64, 368, 656
+    n = tile_aligned_batch(torch.cuda.get_device_properties(0).multi_processor_count)
+    h, w = 368, 656
     rng = np.random.default_rng(14)
     x = rng.uniform(-0.5, 0.5, (n, 3, h, w)).astype(np.float32)
     net = Net(ctx, "builtin:BODY_25")
@@ -124,13 +131,17 @@ def test_body25_bench_geometry_vs_oracle(ctx):
     net.forward(torch.from_numpy(x).cuda())
     got = net.output_numpy()
     assert got.shape == (n, 78, h // 8, w // 8)
-    pick = [0, 31, 63]
+    pick = [0, n // 2 - 1, n - 1]
     ref = body25.forward(x[pick], params, graph=graph)
     err = rel_l2(got[pick], ref)
     ch = channel_errors(got[pick], ref)
-    print("BODY_25 64x368x656 frames %s rel-L2 %.3e, worst channel %.3e" % (pick, err, ch.max()))
+    ref16 = emu.forward(x[pick], params, graph)
+    err16 = rel_l2(got[pick], ref16)
+    print("BODY_25 %dx368x656 frames %s rel-L2 %.3e (fp32 oracle), %.3e (fp16-storage emulation), "
+          "worst channel %.3e" % (n, pick, err, err16, ch.max()))
     assert err < BODY25_TOL
     assert ch.max() < CHANNEL_TOL
+    assert err16 < FP16_EMU_TOL
 
 
 def test_net_output_query_follows_addCaffeNetOnThread(ctx):

@@ -3,33 +3,54 @@ process per GPU, per-frame records gathered to rank 0 in frame order inside the 
 openpose_amd/parallel.py) run on the real pipelines.  The box has one GPU, so
 bench.py runs in its rehearsal mode (OPK_BENCH_REHEARSE=1): the parent spawns the ranks before any
 GPU call, every rank puts its pipeline on GPU 0 and the gather runs over gloo -- the code path of
-an N-GPU run except the RCCL transport.  The N-rank throughput of such a run means nothing."""
+an N-GPU run except the RCCL transport.  The N-rank throughput of such a run means nothing.
+
+Results, not just plumbing: a frame's synthetic input depends only on its global frame id
+(bench.contents_of_rank), so rank 0's gathered records of a 2-rank run must equal, frame for frame
+and bit for bit, those of a 1-rank run over the same frame ids (the reference's WQueueOrderer
+contract: the sharded pipeline's output is the single pipeline's, in order --
+include/openpose/thread/wQueueOrderer.hpp:62-141, wrapperAuxiliary.hpp:1050-1067)."""
 import json
 import os
 import subprocess
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("config", ["body25", "body135"])
-def test_sharded_bench_two_ranks(config):
+def _run(config, gpus, steps, batch, dump):
     env = dict(os.environ, OPK_BENCH_REHEARSE="1", MASTER_ADDR="127.0.0.1")
     env.pop("RANK", None)
     env.pop("WORLD_SIZE", None)
-    batch, steps = 8, 3
-    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", str(steps),
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", str(gpus), "--steps", str(steps),
                         "--warmup", "1", "--batch", str(batch), "--no-cpu-baseline",
-                        "--config", config],
+                        "--config", config, "--dump-records", dump],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
-    line = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["body25", "body135"])
+def test_sharded_bench_two_ranks(config, tmp_path):
+    batch, steps = 8, 2
+    d2, d1 = str(tmp_path / "r2.npz"), str(tmp_path / "r1.npz")
+    line = _run(config, 2, steps, batch, d2)
     assert line["n_gpus"] == 2 and line["steps"] == steps
     # rank 0 received every frame of both ranks exactly once, in frame order (RecordGather
     # raises on a missing or duplicated frame)
     assert line["config"]["frames_gathered_in_order"] == 2 * batch * steps
     assert line["value"] > 0 and line["ms_per_step"] > 0
     assert "REHEARSAL" in line["config"]["parallelism"]
+    # the same frame ids through one rank: identical records, frame for frame
+    one = _run(config, 1, 2 * steps, batch, d1)
+    assert one["config"]["frames_gathered_in_order"] == 2 * batch * steps
+    a, b = np.load(d2), np.load(d1)
+    assert len(a["counts"]) == 2 * batch * steps
+    np.testing.assert_array_equal(a["counts"], b["counts"])
+    np.testing.assert_array_equal(a["keypoints"], b["keypoints"])
+    np.testing.assert_array_equal(a["scores"], b["scores"])
+    assert a["counts"].sum() >= batch   # people were found

@@ -199,3 +199,58 @@ def test_gpu_pose_forward_frames_equals_prepared_input(ctx, size):
         np.testing.assert_array_equal(got[f][0], kp)
         np.testing.assert_array_equal(got[f][1], ks)
     assert sum(len(g[1]) for g in got) > 0
+
+
+@pytest.mark.gpu
+def test_gpu_pose_frames_rewritten_between_submits(ctx):
+    """Pipelined raw-frame submits that reuse ONE device frame buffer, refilled on the context
+    stream (torch's current stream) before every submit, as a serving loop would: each batch must
+    see its own frames (the warp had run on a side stream ordered only after the previous
+    nets).  Every batch's people equal a synchronous forward of the same frames with all device
+    work on the context stream (POST_STREAM=0), bit for bit."""
+    import torch
+    from oracle import body25
+    from openpose_amd import synth
+    from openpose_amd.api import Net, PoseExtractor, dev_switches
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(synth.he_weights(body25.layers(), seed=3, out_scale=0.02))
+    size, n, batches = (256, 144), 3, 5
+    _, [(w, h)] = api.scale_and_size(size, (-1, 128))
+    ov = torch.from_numpy(np.stack([synth.overlay(3, h // 8, w // 8, seed=40 + f)
+                                    for f in range(n)])).cuda()
+    host = [_frames(n, size[1], size[0], 100 + b).pin_memory() for b in range(batches)]
+
+    def people(pose):
+        return [pose.keypoints(f) for f in range(n)]
+
+    ref = []
+    with dev_switches(POST_STREAM=0):
+        pose = PoseExtractor(ctx, net)
+        pose.set_input((-1, 128))
+        pose.set_overlay(ov)
+        for b in range(batches):
+            pose.forward_frames(host[b].cuda())
+            ref.append(people(pose))
+        pose.close()
+    # the frames matter: the batches' scores differ (the net output shifts the refined peaks)
+    assert any(not np.array_equal(ref[0][f][1], ref[1][f][1]) for f in range(n))
+
+    pose = PoseExtractor(ctx, net)
+    pose.set_input((-1, 128))
+    pose.set_overlay(ov)
+    buf = torch.empty_like(host[0], device="cuda")
+    got = []
+    for b in range(batches):
+        buf.copy_(host[b], non_blocking=True)   # queued on the context stream behind batch b-1
+        pose.submit_frames(buf)
+        if pose.pending() == 2:
+            pose.collect()
+            got.append(people(pose))
+    while pose.pending():
+        pose.collect()
+        got.append(people(pose))
+    assert len(got) == batches
+    for b in range(batches):
+        for f in range(n):
+            np.testing.assert_array_equal(got[b][f][0], ref[b][f][0])
+            np.testing.assert_array_equal(got[b][f][1], ref[b][f][1])

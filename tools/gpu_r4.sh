@@ -1,0 +1,39 @@
+#!/bin/bash
+# round-4 GPU call: new parity tests (+ the fault-injected variant, expected to fail), the GPU
+# suite, smoke, bench.  OUT_TAG=<dir>  STEPS=<env,new,fault,tests,smoke,bench,multi,b135,prof>
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+OUT=gpurun_out/${OUT_TAG:-r4}
+STEPS=${STEPS:-env,new,fault,tests,smoke,bench}
+mkdir -p $OUT
+run() { case ",$STEPS," in *",$1,"*) return 0;; *) return 1;; esac; }
+PYT="python -u -m pytest -x -v -s --timeout 300 --timeout-method thread"
+if run env; then
+  { nproc; python -c "import os; print('cpu_count', os.cpu_count(), 'affinity', len(os.sched_getaffinity(0)), 'OMP', os.environ.get('OMP_NUM_THREADS'))"; } > $OUT/env.log 2>&1
+fi
+if run new; then
+  timeout -k 10 500 $PYT -m gpu tests/test_gpu_layers.py "tests/test_gpu_net.py::test_body25_bench_geometry_vs_oracle" tests/test_preprocess.py > $OUT/pytest_new.log 2>&1 || exit 1
+fi
+if run fault; then
+  # the round-3 miscompile reproduced in a dev variant: the per-layer test must FAIL on it
+  OPK_LIB_PATH=openpose_amd/variants/libopk_faultpool.so timeout -k 10 300 $PYT -m gpu tests/test_gpu_layers.py > $OUT/pytest_fault_variant.log 2>&1
+  rc=$?; echo "exit $rc (1 = test failed as expected)" >> $OUT/pytest_fault_variant.log
+  [ $rc -ge 2 ] && exit 1
+fi
+if run tests; then
+  timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu.log 2>&1 || exit 1
+fi
+if run smoke; then
+  timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1 || exit 1
+fi
+if run bench; then
+  timeout -k 10 300 python -u bench.py > $OUT/bench.log 2>&1 || exit 1
+fi
+if run multi; then
+  timeout -k 10 300 python -u bench.py --config multiscale --steps 20 > $OUT/bench_multiscale.log 2>&1 || exit 1
+fi
+if run b135; then
+  timeout -k 10 300 python -u bench.py --config body135 > $OUT/bench_body135.log 2>&1 || exit 1
+fi
+if run prof; then
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/bench_prof.log 2>&1 || exit 1
+fi
