@@ -451,7 +451,7 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
                               reject, near, s);
     timer_.end(s);
     OPK_HIP(hipEventRecord(sl.done, s));
-    if (s == post_) {
+    if (post_ && s == post_) {   // (the context stream may be the null stream)
         OPK_HIP(hipEventRecord(post_done_, post_));
         post_recorded_ = true;
     }

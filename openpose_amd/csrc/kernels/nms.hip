@@ -431,10 +431,25 @@ __global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ pe
 // per 16-row window it touches (2.5x at x8), and the row tables are read from LDS.  Same
 // hpass/vpass arithmetic and peak rules, so the candidate set is identical (the finalize kernel
 // orders it).
-template <int LT, int RC, int NS>
+//
+// FL (variant flags, dev switch NMS_WALK):
+//   bit 0 (parallel test): the row above is tested with all of its side neighbours' ring reads in
+//     flight at once (6 ds_reads, one wait; the lane's own column above / below from registers)
+//     and only when some lane of the wave holds a candidate (v > th on a testable pixel); without
+//     it the test is nmsCpu's short-circuit chain (peak_at): one LDS round trip per neighbour;
+//   bit 1 (with bit 0): no wait after the ring write -- one wave's LDS operations execute in
+//     order, so a compiler barrier replaces the workgroup barrier;
+//   bit 2 (staged sources): the walk's source footprint (the rows and columns its taps reach, e.g.
+//     13 x 12 floats of a 46 x 82 source at x8) is copied to LDS once, and every advance reads
+//     its four taps from there instead of from L2 / HBM (sources whose footprint exceeds kNmsFP
+//     floats keep the global reads).
+// Same rules and values in every variant, so the same candidates.
+constexpr int kNmsFP = 256;
+template <int LT, int RC, int NS, int FL>
 __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__ scratch,
                                                                const HeatMap M, int parts, float th)
 {
+    constexpr bool PT = (FL & 1) != 0, NOWAIT = (FL & 3) == 3, ST = (FL & 4) != 0;
     static_assert(RC + 2 <= LT, "one lane per window row loads the row tables");
     __shared__ float ring[4 * LT];
     __shared__ float4 rcoef[NS][RC + 2];
@@ -476,7 +491,15 @@ __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__
 #pragma unroll
         for (int k = 0; k < 4; ++k) t[n][k] = heat_clampi(xo - 1 + k, 0, ssw[n] - 1);
     }
-    auto taps = [&src, &ssh, &ssw, &t](int n, int r, float v[4]) {   // source row r's taps
+    __shared__ float fp[ST ? NS : 1][ST ? kNmsFP : 1];
+    int fr0[NS], fc0[NS], fcn[NS];
+    bool stg[NS];
+    auto taps = [&](int n, int r, float v[4]) {   // source row r's taps
+        if (ST && stg[n]) {
+            const float* row = fp[n] + (heat_clampi(r, 0, ssh[n] - 1) - fr0[n]) * fcn[n] - fc0[n];
+            v[0] = row[t[n][0]]; v[1] = row[t[n][1]]; v[2] = row[t[n][2]]; v[3] = row[t[n][3]];
+            return;
+        }
         const float* row = src[n] + (size_t)heat_clampi(r, 0, ssh[n] - 1) * ssw[n];
         v[0] = row[t[n][0]]; v[1] = row[t[n][1]]; v[2] = row[t[n][2]]; v[3] = row[t[n][3]];
     };
@@ -490,6 +513,29 @@ __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
         cur[n] = rsrc[n][wy0 < 0 ? 1 : 0];                   // source row of the first map row
+        stg[n] = false;
+        if constexpr (ST) {
+            // rows cur-1 .. (last map row's source row)+3 (the prefetch), columns of the first and
+            // last in-map lanes' outer taps (xofs is non-decreasing), all clamped as the taps are
+            const int r0 = heat_clampi(cur[n] - 1, 0, ssh[n] - 1);
+            const int r1 = heat_clampi(rsrc[n][min(ye, H - 1) - wy0] + 3, 0, ssh[n] - 1);
+            const int c0 = __shfl(t[n][0], max(xw0, 0) - xw0, LT);
+            const int c1 = __shfl(t[n][3], min(xw0 + LT - 1, W - 1) - xw0, LT);
+            fr0[n] = r0;
+            fc0[n] = c0;
+            fcn[n] = c1 - c0 + 1;
+            const int cnt = (r1 - r0 + 1) * fcn[n];
+            stg[n] = cnt <= kNmsFP;
+            if (stg[n])
+                for (int i = tid; i < cnt; i += LT) {
+                    const int rr = i / fcn[n];
+                    fp[n][i] = src[n][(size_t)(r0 + rr) * ssw[n] + c0 + (i - rr * fcn[n])];
+                }
+        }
+    }
+    if constexpr (ST) __syncthreads();                       // staged footprints
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) h[n][k] = nv[n][k] = 0.f;
         if (xin) {
@@ -503,7 +549,11 @@ __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__
         }
     }
     int* pl = scratch + ((size_t)b * parts + c) * (CAP + 1);
-    float vprev = th;
+    float vprev = th, vprev2 = th;
+    // PT: side-neighbour lanes (clamped at the window's first / last lane, whose tests never run)
+    const int tl = tid > 0 ? tid - 1 : 0, tr = tid < LT - 1 ? tid + 1 : LT - 1;
+    const bool xtest = tid > 0 && tid < LT - 1 && xin;
+    const bool xinner = x > 1 && x < W - 2, xedge = x == 1 || x == W - 2;
     for (int y = wy0; y <= ye; ++y) {
         float v = th;
         if (y >= 0 && y < H) {
@@ -526,12 +576,40 @@ __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__
             if (xin) v = NS > 1 ? acc * inv_n : acc;
         }
         ring[(y & 3) * LT + tid] = v;                        // y >= -1: (y & 3) is y mod 4
-        __syncthreads();                                     // rows y-2 .. y visible
         const int ty = y - 1;                                // row tested now
-        if (ty >= ys && tid > 0 && tid < LT - 1 && xin) {
-            auto get = [xw0](int xx, int yy) { return ring[(yy & 3) * LT + (xx - xw0)]; };
-            if (peak_at(get, W, H, th, x, ty, vprev, false)) push_candidate(pl, ty * W + x);
+        if constexpr (PT) {
+            // nmsCpu's rules (OPK_PEAK_RULES): interior pixels strictly above all 8 neighbours;
+            // pixels on row / column 1 or h-2 / w-2 at least equal, neighbours outside the map = th
+            // (the ring holds th there); any other pixel never
+            const bool inner = xinner && ty > 1 && ty < H - 2;
+            const bool cand = ty >= ys && xtest && vprev > th &&
+                              (inner || xedge || ty == 1 || ty == H - 2);
+            if constexpr (NOWAIT)
+                asm volatile("" ::: "memory");   // the ring reads stay after the write (one wave:
+                                                 // its LDS operations execute in order)
+            else
+                __syncthreads();
+            if (__ballot(cand) != 0) {                                // wave-uniform
+                const float* r0 = ring + ((ty - 1) & 3) * LT;
+                const float* r1 = ring + (ty & 3) * LT;
+                const float* r2 = ring + (y & 3) * LT;
+                const float n0 = r0[tl], n1 = r0[tr], n2 = r1[tl], n3 = r1[tr], n4 = r2[tl], n5 = r2[tr];
+                const float p = vprev;
+                const bool gt = (p > n0) & (p > n1) & (p > n2) & (p > n3) & (p > n4) & (p > n5) &
+                                (p > vprev2) & (p > v);
+                const bool ge = (p >= n0) & (p >= n1) & (p >= n2) & (p >= n3) & (p >= n4) &
+                                (p >= n5) & (p >= vprev2) & (p >= v);
+                if (cand && (inner ? gt : ge)) push_candidate(pl, ty * W + x);
+            }
+            if constexpr (NOWAIT) asm volatile("" ::: "memory");   // next write after these reads
+        } else {
+            __syncthreads();                                 // rows y-2 .. y visible
+            if (ty >= ys && tid > 0 && tid < LT - 1 && xin) {
+                auto get = [xw0](int xx, int yy) { return ring[(yy & 3) * LT + (xx - xw0)]; };
+                if (peak_at(get, W, H, th, x, ty, vprev, false)) push_candidate(pl, ty * W + x);
+            }
         }
+        vprev2 = vprev;
         vprev = v;
         // the ring slot written next ((y+1) & 3) was last read when row y-4 was tested
     }
@@ -567,9 +645,22 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
         // (four walks per workgroup, each wave on its own ring with only lgkmcnt waits between
         // rows, measured 5-9 % slower on configs 2, 4 and 5: profiles/round3/nms_wpb/)
         const dim3 grid((w + lt - 3) / (lt - 2), (h + rc - 1) / rc, frames * parts);
-#define OPK_NMS_STREAM(NS_)                                                                    \
-    hipLaunchKernelGGL((nms_detect_stream_kernel<lt, rc, NS_>), grid, dim3(lt), 0, stream,     \
+        // NMS_WALK (dev A/B): the walk's variant flags (nms_detect_stream_kernel FL)
+        const int fl = dev_switch("NMS_WALK", 0);
+#define OPK_NMS_WALK(NS_, FL_)                                                                 \
+    hipLaunchKernelGGL((nms_detect_stream_kernel<lt, rc, NS_, FL_>), grid, dim3(lt), 0, stream, \
                        scratch, heat, parts, threshold)
+#define OPK_NMS_STREAM(NS_)                                                                    \
+    do {                                                                                       \
+        switch (fl) {                                                                          \
+        case 1: OPK_NMS_WALK(NS_, 1); break;                                                   \
+        case 3: OPK_NMS_WALK(NS_, 3); break;                                                   \
+        case 4: OPK_NMS_WALK(NS_, 4); break;                                                   \
+        case 5: OPK_NMS_WALK(NS_, 5); break;                                                   \
+        case 7: OPK_NMS_WALK(NS_, 7); break;                                                   \
+        default: OPK_NMS_WALK(NS_, 0); break;                                                  \
+        }                                                                                      \
+    } while (0)
         switch (heat.nsrc) {
         case 1: OPK_NMS_STREAM(1); break;
         case 2: OPK_NMS_STREAM(2); break;
@@ -577,6 +668,7 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
         default: OPK_NMS_STREAM(4); break;
         }
 #undef OPK_NMS_STREAM
+#undef OPK_NMS_WALK
     } else {
         constexpr int loy = 16;
         // one-wave workgroups (64 columns, 62 tested): no workgroup barrier holds four waves on

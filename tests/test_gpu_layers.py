@@ -106,8 +106,12 @@ def _check_unit(bench_net, layer, kernel):
                                  "gpu %r ref %r tol %r" % (layer, kernel, f, int(bad.sum()), d.size,
                                                            i, float(got[i]), float(ref[i]),
                                                            float(tol[i])))
+        # in ulp16 where the output rounding dominates the bound (no cancellation)
         ulp = emu.ulp16(ref)
-        worst = max(worst, (float((d / ulp).max()), float((d / tol).max()), float(np.abs(ref).max())))
+        dom = tol <= 3 * ulp
+        ulps = float((d[dom] / ulp[dom]).max()) if dom.any() else 0.0
+        worst = tuple(max(a, b) for a, b in zip(worst, (ulps, float((d / tol).max()),
+                                                        float(np.abs(ref).max()))))
     return worst
 
 
@@ -120,8 +124,8 @@ def test_every_launch_within_fp16_bound(bench_net, record_property):
         w = _check_unit(bench_net, layer, kernel)
         rows.append((layer, kernel) + w)
     for layer, kernel, ulps, frac, amax in rows:
-        print("%-40s %-36s max %.2f ulp16  %.3f of bound  |ref| <= %.3g" % (layer, kernel, ulps,
-                                                                               frac, amax))
+        print("%-40s %-30s %.2f ulp16 (rounding-dominated elements)  %.3f of bound  |ref| <= %.3g"
+              % (layer, kernel, ulps, frac, amax))
     record_property("max_ulp16", max(r[2] for r in rows))
     record_property("max_frac_of_bound", max(r[3] for r in rows))
     # net_output (fp32): the last heads' slices against the emulation from their own inputs

@@ -321,7 +321,7 @@ def test_pose_injection_mixed_record_lengths(ctx):
             assert (len(kp) > 0) == (people[src] > 0)
 
 
-def _multiscale_case(ctx, nscales, gap, seed, nms_stream=1):
+def _multiscale_case(ctx, nscales, gap, seed, nms_stream=1, nms_walk=None):
     """--scale_number nscales --scale_gap gap through opk_pose_forward_multi, sizes from
     ScaleAndSizeExtractor (scaleAndSizeExtractor.cpp:74-88); merged heat maps (resizeAndMergeCpu
     average, resizeAndMergeBase.cpp:55-106), peaks and people bit-identical to the oracle chain fed
@@ -347,7 +347,10 @@ def _multiscale_case(ctx, nscales, gap, seed, nms_stream=1):
     pose = PoseExtractor(ctx, net)
     ovd = _dev(ov)
     pose.set_overlay(ovd)
-    with dev_switches(NMS_STREAM=nms_stream):
+    sw = dict(NMS_STREAM=nms_stream)
+    if nms_walk is not None:
+        sw["NMS_WALK"] = nms_walk
+    with dev_switches(**sw):
         pose.forward_multi([_dev(x) for x in xs], (1280, 720))
     s = pose.scale_net_to_output()
     assert abs(s - 1.959128) < 1e-5
@@ -381,6 +384,14 @@ def test_multiscale_other_scale_numbers_bitexact(ctx, nscales, gap, nms_stream):
     """--scale_number 2 / 3 (the 2- and 3-source streaming NMS walks) and 6 (more than 4 sources:
     the windowed lazy NMS), and the windowed kernel for 2-4 sources (NMS_STREAM=0)."""
     _multiscale_case(ctx, nscales, gap, 40 + nscales, nms_stream)
+
+
+@pytest.mark.parametrize("walk", [1, 3, 4, 5, 7])
+@pytest.mark.parametrize("nscales", [1, 4])
+def test_nms_walk_variants_bitexact(ctx, walk, nscales):
+    """Every variant of the streaming NMS walk (nms_detect_stream_kernel FL: parallel peak test,
+    no-wait ring, LDS-staged source footprint) gives the oracle's peaks and people, 1 and 4 sources."""
+    _multiscale_case(ctx, nscales, 0.25, 90 + nscales, 1, walk)
 
 
 def _resize_get_scale_factor(init, target):

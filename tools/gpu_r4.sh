@@ -37,3 +37,12 @@ fi
 if run prof; then
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $OUT/bench_prof.log 2>&1 || exit 1
 fi
+if run nmsab; then   # NMS walk A/B (NMS_WALK variants), post-processing ms per step from the bench line
+  timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_pipeline.py -k "nms_walk or multiscale or upsampling or fixture" > $OUT/pytest_nms.log 2>&1 || exit 1
+  for i in 1 2; do
+    for v in ${NMS_VARIANTS:-0 1 3 4 5 7}; do
+      timeout -k 10 200 python -u bench.py --steps 20 --no-cpu-baseline --dev NMS_WALK=$v > $OUT/nmsab_b25_w${v}_$i.log 2>&1 || exit 1
+      timeout -k 10 200 python -u bench.py --config body135 --steps 20 --no-cpu-baseline --dev NMS_WALK=$v > $OUT/nmsab_b135_w${v}_$i.log 2>&1 || exit 1
+    done
+  done
+fi
