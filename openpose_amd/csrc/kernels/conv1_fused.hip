@@ -42,18 +42,31 @@ typedef float float2_t __attribute__((ext_vector_type(2)));
 constexpr int TR = 6, TC = 62, VW = 64;       // tile rows / columns; virtual row width
 constexpr int MT = TR * VW;                   // GEMM rows per tile (384)
 constexpr int HROWS = (TR + 2) * VW + 8;      // halo rows (+ overflow of the last taps)
-constexpr int PR = TR + 4, PC = TC + 4;       // image patch
-constexpr int PATCH = 3 * PR * PC;            // floats
+constexpr int PR = TR + 4, PCW = TC + 4;      // image patch rows / columns
+constexpr int PATCH = 3 * PR * PCW;           // patch floats
+// LDS patch layout, chosen so that conv1_1's K gathers are free of bank conflicts: row stride PC
+// and plane stride PS with PS = 11, PC = 3 (mod 32) give every K pair (k, k + 8) of a lane pair
+// q, q + 1 the same offset difference (24 mod 32), and lane rows q = 1, 3 read a second copy of
+// the patch at D = 24 (mod 32) -- so the 16-float runs of the two lane rows of a ds_read_b32 group
+// fall on opposite bank halves (tools/lds_conflicts.py models it)
+constexpr int PC = 67, PS = 683, PD = 2072;
+static_assert(PC >= PCW && PS >= PR * PC && PC % 32 == 3 && PS % 32 == 11 && PD % 32 == 24, "patch layout");
+constexpr int PATCH_LDS = PD + 3 * PS;        // floats, both copies
 constexpr int NT = 512;                       // lanes per workgroup (8 waves)
 constexpr int PPL = (PATCH + NT - 1) / NT;    // patch floats per lane
 constexpr int TSTRIDE = 72;                   // epilogue tile row stride in halves (16-B rows)
 constexpr int W2_PIECES = 18 * 64 * 4;        // 2 chunks x 9 taps x 64 rows x 4 x 16 B
 constexpr int HALO_PIECES = 2 * HROWS * 4;
-constexpr int LDS_BYTES = (W2_PIECES + HALO_PIECES) * 16 + (PATCH * 4 + 15) / 16 * 16;
+constexpr int LDS_BYTES = (W2_PIECES + HALO_PIECES) * 16 + (PATCH_LDS * 4 + 15) / 16 * 16;
 static_assert(MT * TSTRIDE * 2 <= HALO_PIECES * 16, "epilogue tile fits in the halo");
 static_assert(LDS_BYTES <= 160 * 1024, "LDS budget");
 
+// conv1_2's weights: the conv3 packing's swizzle (DMA'd as packed on the host)
 __device__ __forceinline__ int swz64(int row, int piece) { return row * 4 + (piece ^ (((row >> 2) & 1) << 1)); }
+// the halo (written by conv1_1's epilogue, read as conv1_2's A fragments): piece ^ ((row >> 1) & 3)
+// keeps the fragment reads conflict-free and also the epilogue's ds_write_b128 (8 consecutive rows
+// of one piece per lane group land on 8 distinct 16-byte bank slots)
+__device__ __forceinline__ int swzh(int row, int piece) { return row * 4 + (piece ^ ((row >> 1) & 3)); }
 
 __device__ __forceinline__ uint32_t hmax4(uint32_t a, uint32_t b, uint32_t c, uint32_t d)
 {
@@ -108,15 +121,19 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
         const float4_t s2 = *reinterpret_cast<const float4_t*>(a.s2 + ch);
         m2[g] = a.act2 == 2 ? s2 : float4_t{neg2, neg2, neg2, neg2};
     }
-    // this lane's 8 conv1_1 K values: patch offset of (ci, ky, kx) for k = 8q + e; K padding
-    // (k > 26) reads offset 0 and is zeroed after the read, so the eight reads issue back to back
+    // this lane's 8 conv1_1 K values: patch offset of (ci, ky, kx) for k = 8q + e (lane rows
+    // q = 1, 3 in the second copy); K padding (k > 26, lane row 3) reads a dummy word 16 banks from
+    // its lane-row-2 partner's and is zeroed after the read, so the eight reads issue back to back
+    auto poff = [](int k) {
+        const int t = k / 3, ci = k - 3 * (k / 3);
+        return ci * PS + (t / 3) * PC + (t - 3 * (t / 3));
+    };
     int off[8];
     unsigned kvalid = 0;
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
         const int k = 8 * q + e;
-        const int t = k / 3, ci = k - 3 * (k / 3);
-        off[e] = k < 27 ? (ci * PR + t / 3) * PC + (t - 3 * (t / 3)) : 0;
+        off[e] = k < 27 ? poff(k) + (q & 1) * PD : poff(k - 8) + 16;
         kvalid |= (k < 27 ? 1u : 0u) << e;
     }
 
@@ -139,9 +156,9 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
             const int i_ = tid + k_ * NT;                                                     \
             float v_ = 0.f;                                                                   \
             if (i_ < PATCH && (tile_) < ntiles) {                                             \
-                const int ci_ = i_ / (PR * PC);                                               \
-                const int rem_ = i_ - ci_ * (PR * PC);                                        \
-                const int r_ = rem_ / PC, c_ = rem_ - (rem_ / PC) * PC;                       \
+                const int ci_ = i_ / (PR * PCW);                                              \
+                const int rem_ = i_ - ci_ * (PR * PCW);                                       \
+                const int r_ = rem_ / PCW, c_ = rem_ - (rem_ / PCW) * PCW;                    \
                 const int y_ = y0_ - 2 + r_, x_ = x0_ - 2 + c_;                               \
                 if (y_ >= 0 && y_ < H && x_ >= 0 && x_ < W)                                   \
                     v_ = src_[((size_t)ci_ * H + y_) * W + x_];                               \
@@ -149,6 +166,29 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
             pre[k_] = v_;                                                                     \
         }                                                                                     \
     } while (0)
+
+    // pool pass lane roles: ds_read_b128 lane group g (0-3) of this lane and its index k in the
+    // group -> pixel g + 4 (k >> 3), channel group k & 7
+    int pool_dp, pool_cg;
+    {
+        const unsigned g1m = 0xF00F0FF0u;          // lanes {4-11, 16-19, 28-31} of each half
+        const int lo = lane & 31;
+        const bool g1 = (g1m >> lo) & 1u;
+        const unsigned same = g1 ? g1m : ~g1m;
+        const int k = __popc(same & ((1u << lo) - 1u));
+        pool_dp = (g1 ? 1 : 0) + 2 * (lane >> 5) + 4 * (k >> 3);
+        pool_cg = k & 7;
+    }
+
+    // LDS index of this lane's patch floats (element tid + k * NT of [3][PR][PCW]), -1 past the end
+    int pli[PPL];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+        const int i = tid + k * NT;
+        const int ci = i / (PR * PCW), rem = i - ci * (PR * PCW);
+        const int r = rem / PCW, cc = rem - r * PCW;
+        pli[k] = i < PATCH ? ci * PS + r * PC + cc : -1;
+    }
 
     int tile = blockIdx.x;
     OPK1_LOAD_PATCH(tile);
@@ -158,7 +198,10 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
         __syncthreads();   // previous tile's pooling reads of T (aliasing the halo) are done
 #pragma unroll
         for (int k = 0; k < PPL; ++k)
-            if (tid + k * NT < PATCH) patch[tid + k * NT] = pre[k];
+            if (pli[k] >= 0) {
+                patch[pli[k]] = pre[k];
+                patch[PD + pli[k]] = pre[k];
+            }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // resident weights (first tile)
         __syncthreads();
 
@@ -168,7 +211,7 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
 #pragma unroll
         for (int gi = 0; gi < 4; ++gi) {
             const int mh = (wave * 4 + gi) * 16 + r16;
-            const int base = (mh >> 6) * PC + (mh & 63);
+            const int base = (mh >> 6) * PC + (mh & 63);   // patch row / column of the halo position
 #pragma unroll
             for (int e = 0; e < 8; ++e) xv[gi][e] = patch[off[e] + base];
         }
@@ -211,7 +254,7 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
             for (int c = 0; c < 2; ++c) {
                 const auto sl = __builtin_amdgcn_permlane16_swap(pk[2 * c][0], pk[2 * c + 1][0], false, false);
                 const auto sh = __builtin_amdgcn_permlane16_swap(pk[2 * c][1], pk[2 * c + 1][1], false, false);
-                HALO[c * HROWS * 4 + swz64(mh, 2 * (q & 1) + (q >> 1))] = make_uint4(sl[0], sh[0], sl[1], sh[1]);
+                HALO[c * HROWS * 4 + swzh(mh, 2 * (q & 1) + (q >> 1))] = make_uint4(sl[0], sh[0], sl[1], sh[1]);
             }
         }
         __syncthreads();
@@ -234,7 +277,7 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
         const uint4* Bs_ = W2 + (c_ * 9 + tap_) * 256;                                        \
         _Pragma("unroll") for (int i_ = 0; i_ < 3; ++i_)                                      \
             fa[buf_][i_] = __builtin_bit_cast(                                                \
-                half8_t, As_[swz64(wave * 48 + i_ * 16 + r16 + ky_ * VW + kx_, q)]);            \
+                half8_t, As_[swzh(wave * 48 + i_ * 16 + r16 + ky_ * VW + kx_, q)]);             \
         _Pragma("unroll") for (int j_ = 0; j_ < 4; ++j_)                                      \
             fb[buf_][j_] = __builtin_bit_cast(half8_t, Bs_[swz64(j_ * 16 + r16, q)]);           \
     } while (0)
@@ -289,12 +332,16 @@ __global__ __launch_bounds__(NT, 1) void conv1_fused_kernel(const Conv1FusedArgs
         __syncthreads();
 
         // ---- 2x2 max pool: (TR/2) x (TC/2) pooled pixels x 8 channel groups ---------------------
-        for (int task = tid; task < (TR / 2) * (TC / 2) * 8; task += NT) {
-            const int cg = task & 7;
-            const int pp = task >> 3;
-            const int pr = pp / (TC / 2), pc = pp - (pp / (TC / 2)) * (TC / 2);
+        // A wave takes 8 pixels of one pooled row at a time (slots of 32 per row, the 32nd unused);
+        // each 16-lane group of ds_read_b128 (MI355X_MICROARCH.md §LDS) reads pixels p and p + 4,
+        // 8 channel groups each: 2 x 128 contiguous bytes 8 positions (= 32 banks mod 64) apart,
+        // so the reads are free of bank conflicts (tools/lds_conflicts.py)
+        for (int it = wave; it < (TR / 2) * 4; it += NT / 64) {
+            const int slot = it * 8 + pool_dp;
+            const int cg = pool_cg;
+            const int pr = slot >> 5, pc = slot & 31;
             const int oy = y0 / 2 + pr, ox = x0 / 2 + pc;
-            if (2 * oy + 1 >= H || 2 * ox + 1 >= W) continue;
+            if (pc >= TC / 2 || 2 * oy + 1 >= H || 2 * ox + 1 >= W) continue;
             const int m0 = (2 * pr) * VW + 2 * pc;
             const uint16_t* s0 = T + m0 * TSTRIDE + cg * 8;
             uint4 v0 = *reinterpret_cast<const uint4*>(s0);

@@ -20,6 +20,7 @@
 //      raster order by its workgroup, so the result never depends on the candidate capacity.
 // -ffp-contract=off keeps the centroid sums bit-identical to the CPU.
 #include <cstdlib>
+#include <type_traits>
 #include "kernels.h"
 #include "heat_dev.h"
 #include "../common.h"
@@ -27,6 +28,8 @@
 namespace opk {
 
 namespace {
+
+typedef float float2_t __attribute__((ext_vector_type(2)));
 
 constexpr int DT = 256;   // detect lanes per block
 constexpr int FT = 256;   // finalize lanes per block
@@ -615,6 +618,196 @@ __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__
     }
 }
 
+
+// Two columns per lane, no LDS ring (NMS_WALK 8 / the default below): one wave owns the 128 map
+// columns xw0 .. xw0 + 127 (126 tested) of RC rows and walks down them.  A lane keeps its two
+// columns' horizontal passes as float2 registers, so every pass, vertical combination and merge
+// is one packed v_pk_mul_f32 / v_pk_add_f32 per two pixels with resize.hip's operations in its
+// order (-ffp-contract=off: the same bits).  The three rows a test needs (row above, the tested
+// row, row below) stay in registers; the two side columns of the neighbouring lanes come by
+// wave-wide DPP shifts, and only on rows where some lane holds a candidate (v > th on a testable
+// pixel).  Measured on the ring walk: its cost is the instruction stream, not LDS latency (a test
+// with all its reads in flight but more instructions ran 30 % slower: profiles/round4/nms_walk/),
+// so this walk spends ~10 instructions per pixel row on the common path instead of ~30.
+// A pixel passes the nmsCpu rules as peak_at: interior pixels strictly above, row / column 1 or
+// h-2 / w-2 pixels at least equal to, all 8 neighbours (th outside the map); the neighbours are
+// compared through their maximum, which is the same test for NaN-free maps.
+__device__ __forceinline__ float dpp_from_left(float v)    // lane i gets lane i-1's value
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x138, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_from_right(float v)   // lane i gets lane i+1's value
+{
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, false));
+}
+
+template <int RC, int NS>
+__global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ scratch,
+                                                              const HeatMap M, int parts, float th)
+{
+    constexpr int LT = 64, CW = 2 * LT - 2;
+    static_assert(RC + 2 <= LT, "one lane per window row holds the row tables");
+    const int tid = threadIdx.x;
+    const int c = blockIdx.z % parts, b = blockIdx.z / parts;
+    const int plane = b * M.channels + c;
+    const int H = M.h, W = M.w;
+    const int xw0 = blockIdx.x * CW - 1;                     // map column of lane 0's first column
+    const int xa = xw0 + 2 * tid, xb = xa + 1;
+    const bool ina = xa >= 0 && xa < W, inb = xb >= 0 && xb < W;
+    // OpenCV's SIMD body covers every in-map column of this wave: the one vertical order for both
+    const bool wave_simd = min(xw0 + 2 * LT - 1, W - 1) < W - W % kCvVResizeLanes;
+    const bool sa = cubic_simd_column(xa, W), sb = cubic_simd_column(xb, W);
+    const float inv_n = M.inv_n;
+    const int ys = blockIdx.y * RC, ye = min(ys + RC, H);
+    const int wy0 = ys - 1;
+    // row tables of the window's rows wy0 .. wy0 + RC + 1, one row per lane (read by v_readlane,
+    // no LDS round trip per row)
+    int lrsrc[NS];
+    float lrc[NS][4];
+    const float* src[NS];
+    int ssh[NS], ssw[NS], ta[NS][4], tb[NS][4];
+    float2_t A[NS][4];
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+        const ResizeSource& S = M.src[n];
+        {
+            const int y = heat_clampi(wy0 + tid, 0, H - 1);
+            const float4 cq = *reinterpret_cast<const float4*>(S.ycoef + 4 * y);
+            lrc[n][0] = cq.x; lrc[n][1] = cq.y; lrc[n][2] = cq.z; lrc[n][3] = cq.w;
+            lrsrc[n] = S.yofs[y];
+        }
+        src[n] = S.src + (size_t)plane * S.sh * S.sw;
+        ssh[n] = S.sh;
+        ssw[n] = S.sw;
+        int xo_a = 0, xo_b = 0;
+        float4 ca = make_float4(0.f, 0.f, 0.f, 0.f), cb = ca;
+        if (ina) {
+            xo_a = S.xofs[xa];
+            ca = *reinterpret_cast<const float4*>(S.xcoef + 4 * xa);
+        }
+        if (inb) {
+            xo_b = S.xofs[xb];
+            cb = *reinterpret_cast<const float4*>(S.xcoef + 4 * xb);
+        }
+        A[n][0] = float2_t{ca.x, cb.x};
+        A[n][1] = float2_t{ca.y, cb.y};
+        A[n][2] = float2_t{ca.z, cb.z};
+        A[n][3] = float2_t{ca.w, cb.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ta[n][k] = heat_clampi(xo_a - 1 + k, 0, ssw[n] - 1);
+            tb[n][k] = heat_clampi(xo_b - 1 + k, 0, ssw[n] - 1);
+        }
+    }
+    auto taps = [&](int n, int r, float2_t v[4]) {   // source row r's taps of both columns
+        const float* row = src[n] + (size_t)heat_clampi(r, 0, ssh[n] - 1) * ssw[n];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = float2_t{row[ta[n][k]], row[tb[n][k]]};
+    };
+    auto hsum = [&A](int n, const float2_t v[4]) {   // cubic_hpass's sum, in its order
+        return v[0] * A[n][0] + v[1] * A[n][1] + v[2] * A[n][2] + v[3] * A[n][3];
+    };
+    auto rdl_i = [](int v, int l) { return __builtin_amdgcn_readlane(v, l); };
+    auto rdl_f = [](float v, int l) {
+        return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+    };
+    int cur[NS];
+    float2_t h[NS][4], nv[NS][4];
+#pragma unroll
+    for (int n = 0; n < NS; ++n) {
+        cur[n] = rdl_i(lrsrc[n], wy0 < 0 ? 1 : 0);
+        float2_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            taps(n, cur[n] - 1 + k, v);
+            h[n][k] = hsum(n, v);
+        }
+        taps(n, cur[n] + 3, nv[n]);                          // next advance's row, in flight
+    }
+    int* pl = scratch + ((size_t)b * parts + c) * (CAP + 1);
+    const float2_t thv = float2_t{th, th};
+    // which lanes test a column, by the row's kind in nmsCpu's rules (testable: not the window's
+    // halo columns, inside the map): an inner row tests inner and edge columns, an edge row (1,
+    // h-2) every in-map column, an outer row (0, h-1) the edge columns only -- as wave masks.
+    // Out-of-map COLUMNS need no value: no tested pixel has one as a neighbour (x = 0 and w-1 are
+    // never tested); out-of-map ROWS hold th (the border rule's outside value).
+    const bool ta_ok = tid > 0 && ina, tb_ok = tid < LT - 1 && inb;
+    const bool a_inner = xa > 1 && xa < W - 2, b_inner = xb > 1 && xb < W - 2;
+    const bool a_edge = xa == 1 || xa == W - 2, b_edge = xb == 1 || xb == W - 2;
+    const uint64_t Ma_in = __ballot(ta_ok && (a_inner || a_edge)), Mb_in = __ballot(tb_ok && (b_inner || b_edge));
+    const uint64_t Ma_ok = __ballot(ta_ok), Mb_ok = __ballot(tb_ok);
+    const uint64_t Ma_out = __ballot(ta_ok && a_edge), Mb_out = __ballot(tb_ok && b_edge);
+    // The walk with the vertical order fixed (WS: SIMD order for every column of the wave) and no
+    // per-row range checks: rows wy0 (above the first tested row) and ys are computed before the
+    // loop, the loop covers y = ys + 1 .. ye - 1 (inside the map), row ye after it -- most of a
+    // row's scalar work is gone (the SALU, one per CU cycle, had set the pace).
+    auto walk = [&](auto ws) {
+        constexpr bool WS = decltype(ws)::value;
+        auto row = [&](int y) {                              // merged value of map row y (in the map)
+            float2_t acc;
+#pragma unroll
+            for (int n = 0; n < NS; ++n) {
+                const int tr = rdl_i(lrsrc[n], y - wy0);
+                while (cur[n] < tr) {                        // uniform
+                    h[n][0] = h[n][1]; h[n][1] = h[n][2]; h[n][2] = h[n][3];
+                    ++cur[n];
+                    h[n][3] = hsum(n, nv[n]);
+                    taps(n, cur[n] + 3, nv[n]);
+                }
+                const float b0 = rdl_f(lrc[n][0], y - wy0), b1 = rdl_f(lrc[n][1], y - wy0);
+                const float b2 = rdl_f(lrc[n][2], y - wy0), b3 = rdl_f(lrc[n][3], y - wy0);
+                float2_t vn;
+                if constexpr (WS) {   // cubic_vpass, SIMD order
+                    const float2_t t3 = h[n][3] * b3;
+                    const float2_t t2 = h[n][2] * b2 + t3;
+                    const float2_t t1 = h[n][1] * b1 + t2;
+                    vn = h[n][0] * b0 + t1;
+                } else {
+                    const float ha[4] = {h[n][0].x, h[n][1].x, h[n][2].x, h[n][3].x};
+                    const float hb[4] = {h[n][0].y, h[n][1].y, h[n][2].y, h[n][3].y};
+                    vn = float2_t{cubic_vpass(ha, b0, b1, b2, b3, sa), cubic_vpass(hb, b0, b1, b2, b3, sb)};
+                }
+                acc = (n == 0) ? vn : vn + acc;
+            }
+            return NS > 1 ? acc * inv_n : acc;
+        };
+        // test row ty (values mid) with its neighbour rows up / dn
+        auto test = [&](int ty, float2_t up, float2_t mid, float2_t dn) {
+            uint64_t ma = Ma_in, mb = Mb_in;
+            const bool row_inner = (unsigned)(ty - 2) < (unsigned)(H - 4);
+            if (!row_inner) {                                // rows 0, 1, h-2, h-1 (uniform, rare)
+                const bool row_edge = ty == 1 || ty == H - 2;
+                ma = row_edge ? Ma_ok : Ma_out;
+                mb = row_edge ? Mb_ok : Mb_out;
+            }
+            const uint64_t ca = ma & __ballot(mid.x > th), cb = mb & __ballot(mid.y > th);
+            if ((ca | cb) == 0) return;                      // uniform
+            // side neighbours from the adjacent lanes: left of column a, right of column b
+            const float la0 = dpp_from_left(up.y), la1 = dpp_from_left(mid.y), la2 = dpp_from_left(dn.y);
+            const float rb0 = dpp_from_right(up.x), rb1 = dpp_from_right(mid.x), rb2 = dpp_from_right(dn.x);
+            const float na = fmaxf(fmaxf(fmaxf(la0, up.x), fmaxf(up.y, la1)),
+                                   fmaxf(fmaxf(mid.y, la2), fmaxf(dn.x, dn.y)));
+            const float nb = fmaxf(fmaxf(fmaxf(up.x, up.y), fmaxf(rb0, mid.x)),
+                                   fmaxf(fmaxf(rb1, dn.x), fmaxf(dn.y, rb2)));
+            const bool pa = ((ca >> tid) & 1) && ((a_inner && row_inner) ? mid.x > na : mid.x >= na);
+            const bool pb = ((cb >> tid) & 1) && ((b_inner && row_inner) ? mid.y > nb : mid.y >= nb);
+            if (pa) push_candidate(pl, ty * W + xa);
+            if (pb) push_candidate(pl, ty * W + xb);
+        };
+        float2_t up = wy0 >= 0 ? row(wy0) : thv;             // row ys - 1
+        float2_t mid = row(ys);                              // ys < ye <= H
+        for (int y = ys + 1; y < ye; ++y) {
+            const float2_t v = row(y);
+            test(y - 1, up, mid, v);
+            up = mid;
+            mid = v;
+        }
+        test(ye - 1, up, mid, ye < H ? row(ye) : thv);
+    };
+    if (wave_simd) walk(std::true_type{});
+    else walk(std::false_type{});
+}
+
 }  // namespace
 
 size_t nms_scratch_ints(int frames, int parts) { return (size_t)frames * parts * (CAP + 1); }
@@ -645,6 +838,7 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
         // (four walks per workgroup, each wave on its own ring with only lgkmcnt waits between
         // rows, measured 5-9 % slower on configs 2, 4 and 5: profiles/round3/nms_wpb/)
         const dim3 grid((w + lt - 3) / (lt - 2), (h + rc - 1) / rc, frames * parts);
+        const dim3 grid2((w + 2 * lt - 3) / (2 * lt - 2), (h + rc - 1) / rc, frames * parts);
         // NMS_WALK (dev A/B): the walk's variant flags (nms_detect_stream_kernel FL)
         const int fl = dev_switch("NMS_WALK", 0);
 #define OPK_NMS_WALK(NS_, FL_)                                                                 \
@@ -653,6 +847,10 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
 #define OPK_NMS_STREAM(NS_)                                                                    \
     do {                                                                                       \
         switch (fl) {                                                                          \
+        case 8:                                                                                \
+            hipLaunchKernelGGL((nms_detect_walk2_kernel<rc, NS_>), grid2, dim3(64), 0, stream,  \
+                               scratch, heat, parts, threshold);                               \
+            break;                                                                             \
         case 1: OPK_NMS_WALK(NS_, 1); break;                                                   \
         case 3: OPK_NMS_WALK(NS_, 3); break;                                                   \
         case 4: OPK_NMS_WALK(NS_, 4); break;                                                   \

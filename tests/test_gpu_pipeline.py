@@ -386,7 +386,7 @@ def test_multiscale_other_scale_numbers_bitexact(ctx, nscales, gap, nms_stream):
     _multiscale_case(ctx, nscales, gap, 40 + nscales, nms_stream)
 
 
-@pytest.mark.parametrize("walk", [1, 3, 4, 5, 7])
+@pytest.mark.parametrize("walk", [1, 3, 4, 5, 7, 8])
 @pytest.mark.parametrize("nscales", [1, 4])
 def test_nms_walk_variants_bitexact(ctx, walk, nscales):
     """Every variant of the streaming NMS walk (nms_detect_stream_kernel FL: parallel peak test,

@@ -46,3 +46,21 @@ if run nmsab; then   # NMS walk A/B (NMS_WALK variants), post-processing ms per 
     done
   done
 fi
+if run ab; then   # build A/B: AB_LIBS (variant names; "default" = the product build), interleaved
+  for i in 1 2; do
+    for v in ${AB_LIBS:-base default}; do
+      if [ "$v" = default ]; then L=""; else L="OPK_LIB_PATH=openpose_amd/variants/libopk_$v.so"; fi
+      env $L timeout -k 10 200 python -u bench.py --steps 30 --no-cpu-baseline $AB_ARGS > $OUT/ab_${v}_$i.log 2>&1 || exit 1
+    done
+  done
+fi
+if run abprof; then   # per-kernel statistics of each A/B build (rocprofv3 kernel trace, 10 steps)
+  for v in ${AB_LIBS:-base default}; do
+    if [ "$v" = default ]; then export -n OPK_LIB_PATH; unset OPK_LIB_PATH; else export OPK_LIB_PATH=openpose_amd/variants/libopk_$v.so; fi
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$v -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline $AB_ARGS > $OUT/prof_$v.log 2>&1 || exit 1
+  done
+  unset OPK_LIB_PATH
+fi
+if run convtests; then
+  timeout -k 10 400 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu tests/test_gpu_net.py tests/test_gpu_layers.py > $OUT/pytest_conv.log 2>&1 || exit 1
+fi
