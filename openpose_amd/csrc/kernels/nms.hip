@@ -435,24 +435,14 @@ __global__ __launch_bounds__(FT) void nms_finalize_kernel(float* __restrict__ pe
 // hpass/vpass arithmetic and peak rules, so the candidate set is identical (the finalize kernel
 // orders it).
 //
-// FL (variant flags, dev switch NMS_WALK):
-//   bit 0 (parallel test): the row above is tested with all of its side neighbours' ring reads in
-//     flight at once (6 ds_reads, one wait; the lane's own column above / below from registers)
-//     and only when some lane of the wave holds a candidate (v > th on a testable pixel); without
-//     it the test is nmsCpu's short-circuit chain (peak_at): one LDS round trip per neighbour;
-//   bit 1 (with bit 0): no wait after the ring write -- one wave's LDS operations execute in
-//     order, so a compiler barrier replaces the workgroup barrier;
-//   bit 2 (staged sources): the walk's source footprint (the rows and columns its taps reach, e.g.
-//     13 x 12 floats of a 46 x 82 source at x8) is copied to LDS once, and every advance reads
-//     its four taps from there instead of from L2 / HBM (sources whose footprint exceeds kNmsFP
-//     floats keep the global reads).
-// Same rules and values in every variant, so the same candidates.
-constexpr int kNmsFP = 256;
-template <int LT, int RC, int NS, int FL>
+// Round 4 measured three variants of this walk, bit-identical, none kept (profiles/round4/
+// nms_walk/): the peak test with all neighbour reads in flight at once (+30 %: more instructions
+// per tested row), without the wait after the ring write (the same), the walk's source footprint
+// staged in LDS (neutral).  nms_detect_walk2_kernel below replaced it for 1-4 sources.
+template <int LT, int RC, int NS>
 __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__ scratch,
                                                                const HeatMap M, int parts, float th)
 {
-    constexpr bool PT = (FL & 1) != 0, NOWAIT = (FL & 3) == 3, ST = (FL & 4) != 0;
     static_assert(RC + 2 <= LT, "one lane per window row loads the row tables");
     __shared__ float ring[4 * LT];
     __shared__ float4 rcoef[NS][RC + 2];
@@ -494,15 +484,7 @@ __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__
 #pragma unroll
         for (int k = 0; k < 4; ++k) t[n][k] = heat_clampi(xo - 1 + k, 0, ssw[n] - 1);
     }
-    __shared__ float fp[ST ? NS : 1][ST ? kNmsFP : 1];
-    int fr0[NS], fc0[NS], fcn[NS];
-    bool stg[NS];
-    auto taps = [&](int n, int r, float v[4]) {   // source row r's taps
-        if (ST && stg[n]) {
-            const float* row = fp[n] + (heat_clampi(r, 0, ssh[n] - 1) - fr0[n]) * fcn[n] - fc0[n];
-            v[0] = row[t[n][0]]; v[1] = row[t[n][1]]; v[2] = row[t[n][2]]; v[3] = row[t[n][3]];
-            return;
-        }
+    auto taps = [&src, &ssh, &ssw, &t](int n, int r, float v[4]) {   // source row r's taps
         const float* row = src[n] + (size_t)heat_clampi(r, 0, ssh[n] - 1) * ssw[n];
         v[0] = row[t[n][0]]; v[1] = row[t[n][1]]; v[2] = row[t[n][2]]; v[3] = row[t[n][3]];
     };
@@ -516,29 +498,6 @@ __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
         cur[n] = rsrc[n][wy0 < 0 ? 1 : 0];                   // source row of the first map row
-        stg[n] = false;
-        if constexpr (ST) {
-            // rows cur-1 .. (last map row's source row)+3 (the prefetch), columns of the first and
-            // last in-map lanes' outer taps (xofs is non-decreasing), all clamped as the taps are
-            const int r0 = heat_clampi(cur[n] - 1, 0, ssh[n] - 1);
-            const int r1 = heat_clampi(rsrc[n][min(ye, H - 1) - wy0] + 3, 0, ssh[n] - 1);
-            const int c0 = __shfl(t[n][0], max(xw0, 0) - xw0, LT);
-            const int c1 = __shfl(t[n][3], min(xw0 + LT - 1, W - 1) - xw0, LT);
-            fr0[n] = r0;
-            fc0[n] = c0;
-            fcn[n] = c1 - c0 + 1;
-            const int cnt = (r1 - r0 + 1) * fcn[n];
-            stg[n] = cnt <= kNmsFP;
-            if (stg[n])
-                for (int i = tid; i < cnt; i += LT) {
-                    const int rr = i / fcn[n];
-                    fp[n][i] = src[n][(size_t)(r0 + rr) * ssw[n] + c0 + (i - rr * fcn[n])];
-                }
-        }
-    }
-    if constexpr (ST) __syncthreads();                       // staged footprints
-#pragma unroll
-    for (int n = 0; n < NS; ++n) {
 #pragma unroll
         for (int k = 0; k < 4; ++k) h[n][k] = nv[n][k] = 0.f;
         if (xin) {
@@ -552,11 +511,7 @@ __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__
         }
     }
     int* pl = scratch + ((size_t)b * parts + c) * (CAP + 1);
-    float vprev = th, vprev2 = th;
-    // PT: side-neighbour lanes (clamped at the window's first / last lane, whose tests never run)
-    const int tl = tid > 0 ? tid - 1 : 0, tr = tid < LT - 1 ? tid + 1 : LT - 1;
-    const bool xtest = tid > 0 && tid < LT - 1 && xin;
-    const bool xinner = x > 1 && x < W - 2, xedge = x == 1 || x == W - 2;
+    float vprev = th;
     for (int y = wy0; y <= ye; ++y) {
         float v = th;
         if (y >= 0 && y < H) {
@@ -579,45 +534,16 @@ __global__ __launch_bounds__(LT) void nms_detect_stream_kernel(int* __restrict__
             if (xin) v = NS > 1 ? acc * inv_n : acc;
         }
         ring[(y & 3) * LT + tid] = v;                        // y >= -1: (y & 3) is y mod 4
+        __syncthreads();                                     // rows y-2 .. y visible
         const int ty = y - 1;                                // row tested now
-        if constexpr (PT) {
-            // nmsCpu's rules (OPK_PEAK_RULES): interior pixels strictly above all 8 neighbours;
-            // pixels on row / column 1 or h-2 / w-2 at least equal, neighbours outside the map = th
-            // (the ring holds th there); any other pixel never
-            const bool inner = xinner && ty > 1 && ty < H - 2;
-            const bool cand = ty >= ys && xtest && vprev > th &&
-                              (inner || xedge || ty == 1 || ty == H - 2);
-            if constexpr (NOWAIT)
-                asm volatile("" ::: "memory");   // the ring reads stay after the write (one wave:
-                                                 // its LDS operations execute in order)
-            else
-                __syncthreads();
-            if (__ballot(cand) != 0) {                                // wave-uniform
-                const float* r0 = ring + ((ty - 1) & 3) * LT;
-                const float* r1 = ring + (ty & 3) * LT;
-                const float* r2 = ring + (y & 3) * LT;
-                const float n0 = r0[tl], n1 = r0[tr], n2 = r1[tl], n3 = r1[tr], n4 = r2[tl], n5 = r2[tr];
-                const float p = vprev;
-                const bool gt = (p > n0) & (p > n1) & (p > n2) & (p > n3) & (p > n4) & (p > n5) &
-                                (p > vprev2) & (p > v);
-                const bool ge = (p >= n0) & (p >= n1) & (p >= n2) & (p >= n3) & (p >= n4) &
-                                (p >= n5) & (p >= vprev2) & (p >= v);
-                if (cand && (inner ? gt : ge)) push_candidate(pl, ty * W + x);
-            }
-            if constexpr (NOWAIT) asm volatile("" ::: "memory");   // next write after these reads
-        } else {
-            __syncthreads();                                 // rows y-2 .. y visible
-            if (ty >= ys && tid > 0 && tid < LT - 1 && xin) {
-                auto get = [xw0](int xx, int yy) { return ring[(yy & 3) * LT + (xx - xw0)]; };
-                if (peak_at(get, W, H, th, x, ty, vprev, false)) push_candidate(pl, ty * W + x);
-            }
+        if (ty >= ys && tid > 0 && tid < LT - 1 && xin) {
+            auto get = [xw0](int xx, int yy) { return ring[(yy & 3) * LT + (xx - xw0)]; };
+            if (peak_at(get, W, H, th, x, ty, vprev, false)) push_candidate(pl, ty * W + x);
         }
-        vprev2 = vprev;
         vprev = v;
         // the ring slot written next ((y+1) & 3) was last read when row y-4 was tested
     }
 }
-
 
 // Two columns per lane, no LDS ring (NMS_WALK 8 / the default below): one wave owns the 128 map
 // columns xw0 .. xw0 + 127 (126 tested) of RC rows and walks down them.  A lane keeps its two
@@ -641,168 +567,276 @@ __device__ __forceinline__ float dpp_from_right(float v)   // lane i gets lane i
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, false));
 }
 
-template <int RC, int NS>
+template <int RC, int NS, int CPL>
 __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ scratch,
                                                               const HeatMap M, int parts, float th)
 {
-    constexpr int LT = 64, CW = 2 * LT - 2;
-    static_assert(RC + 2 <= LT, "one lane per window row holds the row tables");
+    // (CPL 4 measured 1.5x slower than 2 on config 5: 136 VGPRs, and the wider test costs more
+    // than the halved scalar work saves -- profiles/round4/nms_walk/ r4i)
+    static_assert(CPL == 2 || CPL == 4, "columns per lane");
+    constexpr int LT = 64, CW = CPL * LT - 2, NP = CPL / 2;   // NP column pairs per lane
     const int tid = threadIdx.x;
     const int c = blockIdx.z % parts, b = blockIdx.z / parts;
     const int plane = b * M.channels + c;
     const int H = M.h, W = M.w;
     const int xw0 = blockIdx.x * CW - 1;                     // map column of lane 0's first column
-    const int xa = xw0 + 2 * tid, xb = xa + 1;
-    const bool ina = xa >= 0 && xa < W, inb = xb >= 0 && xb < W;
-    // OpenCV's SIMD body covers every in-map column of this wave: the one vertical order for both
-    const bool wave_simd = min(xw0 + 2 * LT - 1, W - 1) < W - W % kCvVResizeLanes;
-    const bool sa = cubic_simd_column(xa, W), sb = cubic_simd_column(xb, W);
+    const int x0 = xw0 + CPL * tid;                          // this lane's columns x0 .. x0 + CPL-1
+    // OpenCV's SIMD body covers every in-map column of this wave: the one vertical order for all
+    const bool wave_simd = min(xw0 + CPL * LT - 1, W - 1) < W - W % kCvVResizeLanes;
     const float inv_n = M.inv_n;
     const int ys = blockIdx.y * RC, ye = min(ys + RC, H);
     const int wy0 = ys - 1;
-    // row tables of the window's rows wy0 .. wy0 + RC + 1, one row per lane (read by v_readlane,
-    // no LDS round trip per row)
-    int lrsrc[NS];
-    float lrc[NS][4];
-    const float* src[NS];
-    int ssh[NS], ssw[NS], ta[NS][4], tb[NS][4];
-    float2_t A[NS][4];
+    // per source: the plane as a buffer resource (taps: a row's byte offset in an SGPR, the lane's
+    // column offsets in VGPRs -- no address arithmetic per advance), the row tables as plain
+    // pointers (uniform rows: scalar loads), the lane's column coefficients as column pairs
+    __amdgpu_buffer_rsrc_t rs[NS];
+    const int* yofs[NS];
+    const float* ycoef[NS];
+    int ssh[NS], ssw[NS], off[NS][CPL][4];
+    float2_t A[NS][NP][4];
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
         const ResizeSource& S = M.src[n];
-        {
-            const int y = heat_clampi(wy0 + tid, 0, H - 1);
-            const float4 cq = *reinterpret_cast<const float4*>(S.ycoef + 4 * y);
-            lrc[n][0] = cq.x; lrc[n][1] = cq.y; lrc[n][2] = cq.z; lrc[n][3] = cq.w;
-            lrsrc[n] = S.yofs[y];
-        }
-        src[n] = S.src + (size_t)plane * S.sh * S.sw;
+        yofs[n] = S.yofs;
+        ycoef[n] = S.ycoef;
         ssh[n] = S.sh;
         ssw[n] = S.sw;
-        int xo_a = 0, xo_b = 0;
-        float4 ca = make_float4(0.f, 0.f, 0.f, 0.f), cb = ca;
-        if (ina) {
-            xo_a = S.xofs[xa];
-            ca = *reinterpret_cast<const float4*>(S.xcoef + 4 * xa);
-        }
-        if (inb) {
-            xo_b = S.xofs[xb];
-            cb = *reinterpret_cast<const float4*>(S.xcoef + 4 * xb);
-        }
-        A[n][0] = float2_t{ca.x, cb.x};
-        A[n][1] = float2_t{ca.y, cb.y};
-        A[n][2] = float2_t{ca.z, cb.z};
-        A[n][3] = float2_t{ca.w, cb.w};
+        rs[n] = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(S.src + (size_t)plane * S.sh * S.sw), 0,
+                                                  S.sh * S.sw * 4, 0x00020000);
+        float cf[CPL][4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            ta[n][k] = heat_clampi(xo_a - 1 + k, 0, ssw[n] - 1);
-            tb[n][k] = heat_clampi(xo_b - 1 + k, 0, ssw[n] - 1);
+        for (int k = 0; k < CPL; ++k) {
+            const int x = x0 + k;
+            int xo = 0;
+            float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (x >= 0 && x < W) {
+                xo = S.xofs[x];
+                q = *reinterpret_cast<const float4*>(S.xcoef + 4 * x);
+            }
+            cf[k][0] = q.x; cf[k][1] = q.y; cf[k][2] = q.z; cf[k][3] = q.w;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) off[n][k][t] = heat_clampi(xo - 1 + t, 0, ssw[n] - 1) * 4;
         }
+#pragma unroll
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int t = 0; t < 4; ++t) A[n][p][t] = float2_t{cf[2 * p][t], cf[2 * p + 1][t]};
     }
-    auto taps = [&](int n, int r, float2_t v[4]) {   // source row r's taps of both columns
-        const float* row = src[n] + (size_t)heat_clampi(r, 0, ssh[n] - 1) * ssw[n];
+    auto taps = [&](int n, int r, float2_t v[NP][4]) {   // source row r's taps of every column
+        const int so = heat_clampi(r, 0, ssh[n] - 1) * ssw[n] * 4;
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = float2_t{row[ta[n][k]], row[tb[n][k]]};
+        for (int p = 0; p < NP; ++p)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+                v[p][t] = float2_t{
+                    __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs[n], off[n][2 * p][t], so, 0)),
+                    __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rs[n], off[n][2 * p + 1][t], so, 0))};
     };
-    auto hsum = [&A](int n, const float2_t v[4]) {   // cubic_hpass's sum, in its order
-        return v[0] * A[n][0] + v[1] * A[n][1] + v[2] * A[n][2] + v[3] * A[n][3];
-    };
-    auto rdl_i = [](int v, int l) { return __builtin_amdgcn_readlane(v, l); };
-    auto rdl_f = [](float v, int l) {
-        return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+    auto hsum = [&A](int n, int p, const float2_t v[4]) {   // cubic_hpass's sum, in its order
+        return v[0] * A[n][p][0] + v[1] * A[n][p][1] + v[2] * A[n][p][2] + v[3] * A[n][p][3];
     };
     int cur[NS];
-    float2_t h[NS][4], nv[NS][4];
+    float2_t h[NS][NP][4], nv[NS][NP][4];
 #pragma unroll
     for (int n = 0; n < NS; ++n) {
-        cur[n] = rdl_i(lrsrc[n], wy0 < 0 ? 1 : 0);
-        float2_t v[4];
+        cur[n] = yofs[n][heat_clampi(wy0 < 0 ? 0 : wy0, 0, H - 1)];
+        float2_t v[NP][4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             taps(n, cur[n] - 1 + k, v);
-            h[n][k] = hsum(n, v);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) h[n][p][k] = hsum(n, p, v[p]);
         }
         taps(n, cur[n] + 3, nv[n]);                          // next advance's row, in flight
     }
     int* pl = scratch + ((size_t)b * parts + c) * (CAP + 1);
-    const float2_t thv = float2_t{th, th};
     // which lanes test a column, by the row's kind in nmsCpu's rules (testable: not the window's
     // halo columns, inside the map): an inner row tests inner and edge columns, an edge row (1,
     // h-2) every in-map column, an outer row (0, h-1) the edge columns only -- as wave masks.
     // Out-of-map COLUMNS need no value: no tested pixel has one as a neighbour (x = 0 and w-1 are
     // never tested); out-of-map ROWS hold th (the border rule's outside value).
-    const bool ta_ok = tid > 0 && ina, tb_ok = tid < LT - 1 && inb;
-    const bool a_inner = xa > 1 && xa < W - 2, b_inner = xb > 1 && xb < W - 2;
-    const bool a_edge = xa == 1 || xa == W - 2, b_edge = xb == 1 || xb == W - 2;
-    const uint64_t Ma_in = __ballot(ta_ok && (a_inner || a_edge)), Mb_in = __ballot(tb_ok && (b_inner || b_edge));
-    const uint64_t Ma_ok = __ballot(ta_ok), Mb_ok = __ballot(tb_ok);
-    const uint64_t Ma_out = __ballot(ta_ok && a_edge), Mb_out = __ballot(tb_ok && b_edge);
-    // The walk with the vertical order fixed (WS: SIMD order for every column of the wave) and no
-    // per-row range checks: rows wy0 (above the first tested row) and ys are computed before the
-    // loop, the loop covers y = ys + 1 .. ye - 1 (inside the map), row ye after it -- most of a
-    // row's scalar work is gone (the SALU, one per CU cycle, had set the pace).
+    uint64_t Min[CPL], Mok[CPL], Mout[CPL];
+    bool cinner[CPL];
+#pragma unroll
+    for (int k = 0; k < CPL; ++k) {
+        const int x = x0 + k;
+        const bool ok = x >= 0 && x < W && !(tid == 0 && k == 0) && !(tid == LT - 1 && k == CPL - 1);
+        cinner[k] = x > 1 && x < W - 2;
+        const bool edge = x == 1 || x == W - 2;
+        Min[k] = __ballot(ok && (cinner[k] || edge));
+        Mok[k] = __ballot(ok);
+        Mout[k] = __ballot(ok && edge);
+    }
+    typedef float2_t Row[NP];
+    // The walk with the vertical order fixed (WS: SIMD order for every column of the wave), no
+    // per-row range checks and the row kind hoisted: rows wy0 (above the first tested row) and ys
+    // are computed before the loops; the tested rows 2 .. h-3 (inner rows, almost all of them) run
+    // in a loop of two rows per trip that tests only against the inner-row masks; the few rows at
+    // the map's top and bottom take the generic test.  The row tables come by scalar loads one
+    // trip ahead.  (PMC, round 4: the SALU, one instruction per CU cycle, had set the walk's pace
+    // -- two scalar instructions per vector one -- so this keeps a row's scalar work small.)
     auto walk = [&](auto ws) {
         constexpr bool WS = decltype(ws)::value;
-        auto row = [&](int y) {                              // merged value of map row y (in the map)
-            float2_t acc;
+        // merged values of map row y (in the map) from its table entries tr (source row per
+        // source) and bq (vertical coefficients per source)
+        auto row = [&](const int tr[NS], const float4 bq[NS], Row out) {
+            float2_t acc[NP];
 #pragma unroll
             for (int n = 0; n < NS; ++n) {
-                const int tr = rdl_i(lrsrc[n], y - wy0);
-                while (cur[n] < tr) {                        // uniform
-                    h[n][0] = h[n][1]; h[n][1] = h[n][2]; h[n][2] = h[n][3];
+                while (cur[n] < tr[n]) {                     // uniform
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) {
+                        h[n][p][0] = h[n][p][1]; h[n][p][1] = h[n][p][2]; h[n][p][2] = h[n][p][3];
+                        h[n][p][3] = hsum(n, p, nv[n][p]);
+                    }
                     ++cur[n];
-                    h[n][3] = hsum(n, nv[n]);
                     taps(n, cur[n] + 3, nv[n]);
                 }
-                const float b0 = rdl_f(lrc[n][0], y - wy0), b1 = rdl_f(lrc[n][1], y - wy0);
-                const float b2 = rdl_f(lrc[n][2], y - wy0), b3 = rdl_f(lrc[n][3], y - wy0);
-                float2_t vn;
-                if constexpr (WS) {   // cubic_vpass, SIMD order
-                    const float2_t t3 = h[n][3] * b3;
-                    const float2_t t2 = h[n][2] * b2 + t3;
-                    const float2_t t1 = h[n][1] * b1 + t2;
-                    vn = h[n][0] * b0 + t1;
-                } else {
-                    const float ha[4] = {h[n][0].x, h[n][1].x, h[n][2].x, h[n][3].x};
-                    const float hb[4] = {h[n][0].y, h[n][1].y, h[n][2].y, h[n][3].y};
-                    vn = float2_t{cubic_vpass(ha, b0, b1, b2, b3, sa), cubic_vpass(hb, b0, b1, b2, b3, sb)};
+#pragma unroll
+                for (int p = 0; p < NP; ++p) {
+                    float2_t vn;
+                    if constexpr (WS) {   // cubic_vpass, SIMD order
+                        const float2_t t3 = h[n][p][3] * bq[n].w;
+                        const float2_t t2 = h[n][p][2] * bq[n].z + t3;
+                        const float2_t t1 = h[n][p][1] * bq[n].y + t2;
+                        vn = h[n][p][0] * bq[n].x + t1;
+                    } else {
+                        const float ha[4] = {h[n][p][0].x, h[n][p][1].x, h[n][p][2].x, h[n][p][3].x};
+                        const float hb[4] = {h[n][p][0].y, h[n][p][1].y, h[n][p][2].y, h[n][p][3].y};
+                        vn = float2_t{cubic_vpass(ha, bq[n].x, bq[n].y, bq[n].z, bq[n].w, cubic_simd_column(x0 + 2 * p, W)),
+                                      cubic_vpass(hb, bq[n].x, bq[n].y, bq[n].z, bq[n].w, cubic_simd_column(x0 + 2 * p + 1, W))};
+                    }
+                    acc[p] = (n == 0) ? vn : vn + acc[p];
                 }
-                acc = (n == 0) ? vn : vn + acc;
             }
-            return NS > 1 ? acc * inv_n : acc;
+#pragma unroll
+            for (int p = 0; p < NP; ++p) out[p] = NS > 1 ? acc[p] * inv_n : acc[p];
         };
-        // test row ty (values mid) with its neighbour rows up / dn
-        auto test = [&](int ty, float2_t up, float2_t mid, float2_t dn) {
-            uint64_t ma = Ma_in, mb = Mb_in;
-            const bool row_inner = (unsigned)(ty - 2) < (unsigned)(H - 4);
-            if (!row_inner) {                                // rows 0, 1, h-2, h-1 (uniform, rare)
-                const bool row_edge = ty == 1 || ty == H - 2;
-                ma = row_edge ? Ma_ok : Ma_out;
-                mb = row_edge ? Mb_ok : Mb_out;
+        auto rowy = [&](int y, Row out) {                    // table entries loaded here
+            int tr[NS];
+            float4 bq[NS];
+#pragma unroll
+            for (int n = 0; n < NS; ++n) {
+                tr[n] = yofs[n][y];
+                bq[n] = *reinterpret_cast<const float4*>(ycoef[n] + 4 * y);
             }
-            const uint64_t ca = ma & __ballot(mid.x > th), cb = mb & __ballot(mid.y > th);
-            if ((ca | cb) == 0) return;                      // uniform
-            // side neighbours from the adjacent lanes: left of column a, right of column b
-            const float la0 = dpp_from_left(up.y), la1 = dpp_from_left(mid.y), la2 = dpp_from_left(dn.y);
-            const float rb0 = dpp_from_right(up.x), rb1 = dpp_from_right(mid.x), rb2 = dpp_from_right(dn.x);
-            const float na = fmaxf(fmaxf(fmaxf(la0, up.x), fmaxf(up.y, la1)),
-                                   fmaxf(fmaxf(mid.y, la2), fmaxf(dn.x, dn.y)));
-            const float nb = fmaxf(fmaxf(fmaxf(up.x, up.y), fmaxf(rb0, mid.x)),
-                                   fmaxf(fmaxf(rb1, dn.x), fmaxf(dn.y, rb2)));
-            const bool pa = ((ca >> tid) & 1) && ((a_inner && row_inner) ? mid.x > na : mid.x >= na);
-            const bool pb = ((cb >> tid) & 1) && ((b_inner && row_inner) ? mid.y > nb : mid.y >= nb);
-            if (pa) push_candidate(pl, ty * W + xa);
-            if (pb) push_candidate(pl, ty * W + xb);
+            row(tr, bq, out);
         };
-        float2_t up = wy0 >= 0 ? row(wy0) : thv;             // row ys - 1
-        float2_t mid = row(ys);                              // ys < ye <= H
-        for (int y = ys + 1; y < ye; ++y) {
-            const float2_t v = row(y);
-            test(y - 1, up, mid, v);
-            up = mid;
-            mid = v;
+        auto val = [](const Row r, int k) { return r[k >> 1][k & 1]; };
+        // test row ty (values mid) with its neighbour rows up / dn; INNER: ty in 2 .. h-3
+        auto test = [&](auto inner, int ty, const Row up, const Row mid, const Row dn) {
+            constexpr bool INNER = decltype(inner)::value;
+            const bool row_inner = INNER || (unsigned)(ty - 2) < (unsigned)(H - 4);
+            const bool row_edge = !INNER && (ty == 1 || ty == H - 2);
+            uint64_t cand[CPL], any = 0;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const uint64_t m = INNER ? Min[k] : row_inner ? Min[k] : row_edge ? Mok[k] : Mout[k];
+                cand[k] = m & __ballot(val(mid, k) > th);
+                any |= cand[k];
+            }
+            if (any == 0) return;                            // uniform
+            // side neighbours from the adjacent lanes: left of column 0, right of column CPL-1
+            const float lu = dpp_from_left(val(up, CPL - 1)), lm = dpp_from_left(val(mid, CPL - 1));
+            const float ld = dpp_from_left(val(dn, CPL - 1));
+            const float ru = dpp_from_right(val(up, 0)), rm = dpp_from_right(val(mid, 0));
+            const float rd = dpp_from_right(val(dn, 0));
+            bool pk[CPL], anyp = false;
+#pragma unroll
+            for (int k = 0; k < CPL; ++k) {
+                const float L0 = k > 0 ? val(up, k - 1) : lu, L1 = k > 0 ? val(mid, k - 1) : lm;
+                const float L2 = k > 0 ? val(dn, k - 1) : ld;
+                const float R0 = k < CPL - 1 ? val(up, k + 1) : ru, R1 = k < CPL - 1 ? val(mid, k + 1) : rm;
+                const float R2 = k < CPL - 1 ? val(dn, k + 1) : rd;
+                const float nm = fmaxf(fmaxf(fmaxf(L0, val(up, k)), fmaxf(R0, L1)),
+                                       fmaxf(fmaxf(R1, L2), fmaxf(val(dn, k), R2)));
+                const float p = val(mid, k);
+                pk[k] = ((cand[k] >> tid) & 1) && ((cinner[k] && row_inner) ? p > nm : p >= nm);
+                anyp = anyp || pk[k];
+            }
+            if (anyp) {
+#pragma unroll
+                for (int k = 0; k < CPL; ++k)
+                    if (pk[k]) push_candidate(pl, ty * W + x0 + k);
+            }
+        };
+        const auto G = std::false_type{};                    // generic row kind
+        const auto I = std::true_type{};                     // inner row
+        Row up, mid, v, w;
+        if (wy0 >= 0) rowy(wy0, up);                         // row ys - 1
+        else
+#pragma unroll
+            for (int p = 0; p < NP; ++p) up[p] = float2_t{th, th};
+        rowy(ys, mid);                                       // ys < ye <= H
+        int y = ys + 1;
+        // rows y whose tested row y - 1 is 0 or 1 (top window only)
+        for (; y < ye && y < 3; ++y) {
+            rowy(y, v);
+            test(G, y - 1, up, mid, v);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                up[p] = mid[p];
+                mid[p] = v[p];
+            }
         }
-        test(ye - 1, up, mid, ye < H ? row(ye) : thv);
+        // inner tested rows: y - 1 <= h - 3, two per trip, tables loaded a trip ahead through
+        // pointers that step two rows a trip (immediate offsets).  The last trip's look-ahead reads
+        // rows up to h: one entry past yofs / ycoef, still inside the context's table buffer
+        // (ycoef | xcoef | yofs | xofs, Context::tables), and never used
+        const int ylast = min(ye - 1, H - 2);                // last y of the inner loop
+        if (y + 1 <= ylast) {
+            const int* yp[NS];
+            const float4* cp[NS];
+            int tr0[NS], tr1[NS];
+            float4 bq0[NS], bq1[NS];
+#pragma unroll
+            for (int n = 0; n < NS; ++n) {
+                yp[n] = yofs[n] + y;
+                cp[n] = reinterpret_cast<const float4*>(ycoef[n]) + y;
+                tr0[n] = yp[n][0]; tr1[n] = yp[n][1];
+                bq0[n] = cp[n][0]; bq1[n] = cp[n][1];
+            }
+            for (; y + 1 <= ylast; y += 2) {
+                int ntr0[NS], ntr1[NS];
+                float4 nbq0[NS], nbq1[NS];
+#pragma unroll
+                for (int n = 0; n < NS; ++n) {
+                    ntr0[n] = yp[n][2]; ntr1[n] = yp[n][3];
+                    nbq0[n] = cp[n][2]; nbq1[n] = cp[n][3];
+                    yp[n] += 2;
+                    cp[n] += 2;
+                }
+                row(tr0, bq0, v);
+                test(I, y - 1, up, mid, v);
+                row(tr1, bq1, w);
+                test(I, y, mid, v, w);
+#pragma unroll
+                for (int p = 0; p < NP; ++p) {
+                    up[p] = v[p];
+                    mid[p] = w[p];
+                }
+#pragma unroll
+                for (int n = 0; n < NS; ++n) {
+                    tr0[n] = ntr0[n]; tr1[n] = ntr1[n];
+                    bq0[n] = nbq0[n]; bq1[n] = nbq1[n];
+                }
+            }
+        }
+        for (; y < ye; ++y) {                                // the rest (tested rows h-2, h-1 among them)
+            rowy(y, v);
+            if (y - 1 >= 2 && y - 1 <= H - 3) test(I, y - 1, up, mid, v);
+            else test(G, y - 1, up, mid, v);
+#pragma unroll
+            for (int p = 0; p < NP; ++p) {
+                up[p] = mid[p];
+                mid[p] = v[p];
+            }
+        }
+        if (ye < H) rowy(ye, v);
+        else
+#pragma unroll
+            for (int p = 0; p < NP; ++p) v[p] = float2_t{th, th};
+        test(G, ye - 1, up, mid, v);
     };
     if (wave_simd) walk(std::true_type{});
     else walk(std::false_type{});
@@ -838,26 +872,19 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
         // (four walks per workgroup, each wave on its own ring with only lgkmcnt waits between
         // rows, measured 5-9 % slower on configs 2, 4 and 5: profiles/round3/nms_wpb/)
         const dim3 grid((w + lt - 3) / (lt - 2), (h + rc - 1) / rc, frames * parts);
+        // the two-columns-per-lane walk (nms_detect_walk2_kernel) for 1-4 sources: nms_detect
+        // 2.2-2.4x faster than the ring walk on configs 2 and 5, +0.8 % frames/s on config 4
+        // (profiles/round4/nms_walk2/); NMS_WALK=0 (dev A/B): the ring walk
+        const bool walk2 = dev_switch("NMS_WALK", 8) != 0;
         const dim3 grid2((w + 2 * lt - 3) / (2 * lt - 2), (h + rc - 1) / rc, frames * parts);
-        // NMS_WALK (dev A/B): the walk's variant flags (nms_detect_stream_kernel FL)
-        const int fl = dev_switch("NMS_WALK", 0);
-#define OPK_NMS_WALK(NS_, FL_)                                                                 \
-    hipLaunchKernelGGL((nms_detect_stream_kernel<lt, rc, NS_, FL_>), grid, dim3(lt), 0, stream, \
-                       scratch, heat, parts, threshold)
 #define OPK_NMS_STREAM(NS_)                                                                    \
     do {                                                                                       \
-        switch (fl) {                                                                          \
-        case 8:                                                                                \
-            hipLaunchKernelGGL((nms_detect_walk2_kernel<rc, NS_>), grid2, dim3(64), 0, stream,  \
+        if (walk2)                                                                             \
+            hipLaunchKernelGGL((nms_detect_walk2_kernel<rc, NS_, 2>), grid2, dim3(64), 0, stream, \
                                scratch, heat, parts, threshold);                               \
-            break;                                                                             \
-        case 1: OPK_NMS_WALK(NS_, 1); break;                                                   \
-        case 3: OPK_NMS_WALK(NS_, 3); break;                                                   \
-        case 4: OPK_NMS_WALK(NS_, 4); break;                                                   \
-        case 5: OPK_NMS_WALK(NS_, 5); break;                                                   \
-        case 7: OPK_NMS_WALK(NS_, 7); break;                                                   \
-        default: OPK_NMS_WALK(NS_, 0); break;                                                  \
-        }                                                                                      \
+        else                                                                                   \
+            hipLaunchKernelGGL((nms_detect_stream_kernel<lt, rc, NS_>), grid, dim3(lt), 0, stream, \
+                               scratch, heat, parts, threshold);                               \
     } while (0)
         switch (heat.nsrc) {
         case 1: OPK_NMS_STREAM(1); break;
@@ -866,7 +893,6 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
         default: OPK_NMS_STREAM(4); break;
         }
 #undef OPK_NMS_STREAM
-#undef OPK_NMS_WALK
     } else {
         constexpr int loy = 16;
         // one-wave workgroups (64 columns, 62 tested): no workgroup barrier holds four waves on

@@ -64,3 +64,21 @@ fi
 if run convtests; then
   timeout -k 10 400 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread -m gpu tests/test_gpu_net.py tests/test_gpu_layers.py > $OUT/pytest_conv.log 2>&1 || exit 1
 fi
+if run nmsprof; then   # per-kernel statistics of the NMS walk variants (NMS_VARIANTS), body25 + body135
+  for v in ${NMS_VARIANTS:-0 8}; do
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/nprof_b135_$v -o run -- python bench.py --config body135 --steps 10 --warmup 2 --no-cpu-baseline --dev NMS_WALK=$v > $OUT/nprof_b135_$v.log 2>&1 || exit 1
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/nprof_b25_$v -o run -- python bench.py --steps 10 --warmup 2 --no-cpu-baseline --dev NMS_WALK=$v > $OUT/nprof_b25_$v.log 2>&1 || exit 1
+  done
+fi
+if run nmspmc; then   # instruction mix of the NMS walks (body135), one counter pass per variant
+  for v in ${NMS_VARIANTS:-0 8}; do
+    timeout -s KILL 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU --output-format csv -d $OUT/npmc_$v -o run -- python bench.py --config body135 --steps 3 --warmup 1 --no-cpu-baseline --dev NMS_WALK=$v > $OUT/npmc_$v.log 2>&1 || exit 1
+  done
+fi
+if run msab; then   # multi-scale (config 4, 4 sources) NMS walk A/B
+  for i in 1 2; do
+    for v in ${NMS_VARIANTS:-0 8}; do
+      timeout -k 10 200 python -u bench.py --config multiscale --steps 15 --no-cpu-baseline --dev NMS_WALK=$v > $OUT/msab_w${v}_$i.log 2>&1 || exit 1
+    done
+  done
+fi
