@@ -21,6 +21,7 @@
 using namespace opk;
 
 static int g_dma_end = 0;
+void opk::note_launch(const char*, ...) {}
 int opk::dev_switch(const char* key, int dflt)
 {
     return std::string(key) == "CONV3W" ? (g_dma_end ? 1 : 2) : dflt;
