@@ -4,6 +4,8 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude -o tools/conv3w_probe_bin tools/conv3w_probe.hip
 //   conv3w_probe [frames H W cin cout iters dma_end zero_operands variant]
 //   variant 1 (NOSTAMPS builds): conv3w8, checked bit for bit against conv3w
+//   variant 3 (NOSTAMPS builds): conv3w8 with the halo-early schedule, checked against conv3w
+//   variant 2: conv3w with the halo-early DMA schedule (CONV3W_HE), checked bit for bit against conv3w
 #ifndef NOSTAMPS
 #define OPKW_STAMPS
 #endif
@@ -20,11 +22,14 @@
 
 using namespace opk;
 
-static int g_dma_end = 0;
+static int g_dma_end = 0, g_e2 = 0;
 void opk::note_launch(const char*, ...) {}
 int opk::dev_switch(const char* key, int dflt)
 {
-    return std::string(key) == "CONV3W" ? (g_dma_end ? 1 : 2) : dflt;
+    if (std::string(key) == "CONV3W") return g_dma_end ? 1 : 2;
+    if ((std::string(key) == "CONV3W_HE" || std::string(key) == "CONV3W8_HE") && g_e2) return 1;
+    const char* e = std::getenv((std::string("OPK_") + key).c_str());
+    return e ? std::atoi(e) : dflt;
 }
 
 #define CK(x)                                                                  \
@@ -106,6 +111,10 @@ int main(int argc, char** argv)
     CK(hipMemset(dst, 0, (size_t)G * 16 * 8));
 #ifdef OPKW_STAMPS
     CK(hipMemcpyToSymbol(HIP_SYMBOL(opkw_stamps), &dst, sizeof(dst)));
+    unsigned long long* dus;
+    CK(hipMalloc(&dus, (size_t)G * 32 * 8));
+    CK(hipMemset(dus, 0, (size_t)G * 32 * 8));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(opkw_ustamps), &dus, sizeof(dus)));
 #endif
 
     hipEvent_t e0, e1;
@@ -113,9 +122,16 @@ int main(int argc, char** argv)
     CK(hipEventCreate(&e1));
     auto launch = [&](const ConvArgs& x) {
 #ifdef NOSTAMPS
-        if (variant == 1) { launch_conv3w8(x, 0); return; }
+        if (variant == 1 || variant == 3) {
+            g_e2 = variant == 3;
+            launch_conv3w8(x, 0);
+            g_e2 = 0;
+            return;
+        }
 #endif
+        g_e2 = variant == 2;
         launch_conv3w(x, 0);
+        g_e2 = 0;
     };
     CK(hipMemset(dout, 0, out_elems * 2));
     for (int i = 0; i < 5; ++i) launch(a);
@@ -128,7 +144,7 @@ int main(int argc, char** argv)
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / iters;
     const double flops = 2.0 * frames * H * W * (double)cout * cin * 9;
-    if (variant == 1) {   // bit-identity against conv3w
+    if (variant >= 1) {   // bit-identity against conv3w
         uint16_t* dref;
         CK(hipMalloc(&dref, out_elems * 2));
         CK(hipMemset(dref, 0, out_elems * 2));
@@ -141,7 +157,8 @@ int main(int argc, char** argv)
         CK(hipMemcpy(h2.data(), dref, out_elems * 2, hipMemcpyDeviceToHost));
         long diff = 0, nz = 0;
         for (long i = 0; i < out_elems; ++i) { diff += h1[i] != h2[i]; nz += h2[i] != 0; }
-        std::printf("  variant 1 vs conv3w: %ld of %ld fp16 values differ (%ld nonzero)\n", diff, out_elems, nz);
+        std::printf("  variant %d vs conv3w", variant);
+        std::printf(": %ld of %ld fp16 values differ (%ld nonzero)\n", diff, out_elems, nz);
     }
     std::printf("conv3w v%d dma_end=%d frames=%d %dx%d cin=%d cout=%d tiles=%ld grid=%d: %.2f us/launch %.1f TFLOP/s\n",
                 variant, g_dma_end, frames, H, W, cin, cout, ntm, G, us, flops / us / 1e6);
@@ -176,6 +193,29 @@ int main(int argc, char** argv)
         if (nb) std::printf("  %-14s mean %8.0f cyc = %7.2f us  (min %8.0f max %8.0f, %d blocks)\n", nm[k],
                             sum / nb, sum / nb / mhz, mn, mx, nb);
     }
+#ifdef OPKW_STAMPS
+    {   // per unit of the second tile: wait + barrier at the mid-unit, and the mid-to-mid period
+        std::vector<unsigned long long> u((size_t)G * 32);
+        CK(hipMemcpy(u.data(), dus, u.size() * 8, hipMemcpyDeviceToHost));
+        const int U = 3 * (cin_pad / 32);
+        std::printf("  tile 1 per unit (cycles, block means): unit  wait+barrier  mid->mid\n");
+        for (int k = 0; k < U && 2 * k + 1 < 32; ++k) {
+            double wb = 0, per = 0;
+            int nb = 0, np = 0;
+            for (int b = 0; b < G; ++b) {
+                const auto x0 = u[b * 32 + 2 * k], x1 = u[b * 32 + 2 * k + 1];
+                if (!x0 || !x1) continue;
+                wb += (double)(x1 - x0);
+                ++nb;
+                if (k + 1 < U && 2 * k + 3 < 32 && u[b * 32 + 2 * k + 3]) {
+                    per += (double)(u[b * 32 + 2 * k + 3] - x1);
+                    ++np;
+                }
+            }
+            if (nb) std::printf("    u%-3d %8.0f  %8.0f\n", k, wb / nb, np ? per / np : 0.0);
+        }
+    }
+#endif
     unsigned long long t0 = ~0ull, t1 = 0;
     for (int b = 0; b < G; ++b) {
         t0 = std::min(t0, h[b * 16 + 14]);
