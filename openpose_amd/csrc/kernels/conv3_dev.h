@@ -62,7 +62,7 @@ __device__ __forceinline__ void vm_wait_rt(int n)
 __device__ __forceinline__ int fdiv(int n, int d, float rd)
 {
     int q = (int)((float)n * rd);
-    const int r = n - q * d;
+    const int r = n - (int)__umul24((unsigned)q, (unsigned)d);   // q, d < 2^24
     q += (r >= d) ? 1 : 0;
     q -= (r < 0) ? 1 : 0;
     return q;
@@ -104,6 +104,32 @@ struct Strips {
         f = FAST ? fdiv(vf, nstrips, rs) : vf / nstrips;
         s = vf - f * nstrips;
         return (long)(f * Hp + yy) * Wp + s * sw + xx;
+    }
+    // one strip (the virtual image is the padded image): the MF epilogue rows p0 + 16 i of a lane
+    // -- their padded positions (0 past the end) and whether they are output pixels -- with one
+    // float-reciprocal division pair for row 0 and branch-free 16-position steps after it, 24-bit
+    // multiplies (positions < 2^24, launch checks) instead of the divergent per-row carries of map()
+    template <int MF>
+    __device__ void rows1(int p0, int W, int (&prow)[MF], bool (&pok)[MF]) const
+    {
+        const int fr = fdiv(p0, fposV, rf);
+        const int rem = p0 - (int)__umul24((unsigned)fr, (unsigned)fposV);
+        int yy = fdiv(rem, VW, rv);
+        int xx = rem - (int)__umul24((unsigned)yy, (unsigned)VW);
+#pragma unroll
+        for (int i = 0; i < MF; ++i) {
+            if (i > 0) {   // VW > 16 (host): at most one row carry per step
+                xx += 16;
+                const bool w = xx >= VW;
+                xx = w ? xx - VW : xx;
+                yy += w ? 1 : 0;
+                yy = yy == Hp ? 0 : yy;
+            }
+            const int p = p0 + 16 * i;
+            const bool in = p < total;
+            prow[i] = in ? p : 0;
+            pok[i] = in && (unsigned)(yy - B) < (unsigned)H && (unsigned)(xx - B) < (unsigned)W;
+        }
     }
     // padded-image position of virtual position v only (halo rows): with one strip the virtual
     // image IS the padded image (sw = W, VW = Wp), so no division is needed

@@ -119,15 +119,7 @@ __device__ __forceinline__ void opkw_bst(const uint2& v, __amdgpu_buffer_rsrc_t 
 // time; measured 2-3 % faster on the stage layers.  CONV3W=2 selects the other placement (A/B).
 // MX: the activation as max(t, t*m) (ConvArgs::actmax; conv3_dev.h act_pick)
 // BST: one destination, epilogue stores through a buffer resource (ConvArgs::bufst)
-// HE (halo early): a chunk's halo DMA is issued one K unit earlier -- at the end of the previous
-// chunk's first unit, right after that unit's weight DMA, instead of with the weights of its own
-// first unit -- so it has 1 2/3 units to land instead of 2/3 (the halo is the HBM part of the
-// stream, all CUs issue it at once).  Its slot (chunk c-1's) is free once every wave passed the
-// mid-unit barrier of chunk c's first unit.  vmcnt retires in issue order: the mid-unit wait of
-// the chunk's second unit, which needs only the older weight DMA, leaves this wave's halo
-// instructions (ai) in flight; the third unit's wait retires them.  Only the DMA timing changes
-// (bit-identical; dev switch CONV3W_HE, A/B).
-template <int BN, bool DMA_END, bool MX, bool BST, bool HE = false>
+template <int BN, bool DMA_END, bool MX, bool BST>
 __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
 {
     constexpr int NW = kW_NW, BM = kW_BM, HR = kW_HR;
@@ -173,8 +165,6 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
     const int cpt = a.cin_pad >> 5;
     const int U = 3 * cpt;
     const int bi = (BPI - wave + NW - 1) / NW;
-    const int ai = (API - wave + NW - 1) / NW;   // halo DMA instructions of this wave
-    (void)ai;
     int boff[BIW];
 #pragma unroll
     for (int j = 0; j < BIW; ++j) {
@@ -196,10 +186,9 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
     } while (0)
     // DMA of K unit (chunk c_, tap row ky_) into halo slot aslot_ / weight slot bslot_; the
     // halo rows of the current (nt_ = false) or the next tile
-#define OPKW_ISSUE(c_, ky_, aslot_, bslot_, nt_) OPKW_ISSUE2(c_, ky_, aslot_, bslot_, nt_, (ky_) == 0, true)
-#define OPKW_ISSUE2(c_, ky_, aslot_, bslot_, nt_, HALO_, WTS_)                                \
+#define OPKW_ISSUE(c_, ky_, aslot_, bslot_, nt_)                                              \
     do {                                                                                      \
-        if (HALO_) {                                                                          \
+        if ((ky_) == 0) {                                                                     \
             const int as_ = (aslot_) * ASLOT;                                                 \
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
                 if (API % NW == 0 || i_ * NW + wave < API)                                    \
@@ -211,7 +200,7 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
         const int bs_ = 2 * ASLOT + (bslot_) * BSLOT;                                         \
         const uint16_t* ub_ = a.w + (size_t)((c_) * 3 + (ky_)) * BROWS * 32;                  \
         _Pragma("unroll") for (int j_ = 0; j_ < BIW; ++j_)                                    \
-            if ((WTS_) && (BPI % NW == 0 || j_ * NW + wave < BPI)) {                          \
+            if (BPI % NW == 0 || j_ * NW + wave < BPI) {                                      \
                 int bo_ = boff[j_];                                                           \
                 asm volatile("" : "+v"(bo_));                                                 \
                 __builtin_amdgcn_global_load_lds(                                             \
@@ -333,14 +322,7 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
         const bool nt_ = u + 2 >= U;                                                          \
         const int u2_ = nt_ ? u + 2 - U : u + 2;                                              \
         const int c2_ = u2_ / 3;                                                              \
-        OPKW_ISSUE2(c2_, u2_ - 3 * c2_, (gc + (nt_ ? cpt : 0) + c2_) & 1, (u + 2) % 3, nt_,   \
-                    !HE && u2_ - 3 * c2_ == 0, true);                                         \
-    } while (0)
-            // HE: the halo of chunk c + 1 (the next tile's chunk 0 after the last chunk)
-#define OPKW_HALO_NEXT()                                                                      \
-    do {                                                                                      \
-        const bool nt_ = c + 1 >= cpt;                                                        \
-        OPKW_ISSUE2(nt_ ? 0 : c + 1, 0, (gc + c + 1) & 1, 0, nt_, true, false);               \
+        OPKW_ISSUE(c2_, u2_ - 3 * c2_, (gc + (nt_ ? cpt : 0) + c2_) & 1, (u + 2) % 3, nt_);  \
     } while (0)
 #ifdef OPKW_STAMPS
             if (tcount == 0 && u == 3) OPKW_STAMP(8);
@@ -350,7 +332,6 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
             // them) are the only VMEM ops younger than unit 1's DMA -- leave them draining
             constexpr int S1 = MF * (NF / 2 + NF % 2);
             if (DMA_END && u == 0 && gc > 0) vm_wait<S1>();
-            else if (HE && ky == 1) vm_wait_rt(ai);   // the next chunk's halo is younger
             else vm_wait<0>();
 #ifdef OPKW_STAMPS
             if (tcount == 0 && u == 3) OPKW_STAMP(9);
@@ -365,9 +346,7 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
             if (!DMA_END && (OPKW_ABLATE != 4 || u + 2 >= U)) OPKW_DMA_U2();
             OPKW_TAP(ab2, ab2, bb_u, 0, false, 0);
             if (DMA_END && (OPKW_ABLATE != 4 || u + 2 >= U)) OPKW_DMA_U2();
-            if (HE && ky == 0 && (OPKW_ABLATE != 4 || c + 1 >= cpt)) OPKW_HALO_NEXT();
 #undef OPKW_DMA_U2
-#undef OPKW_HALO_NEXT
         }
 
 #ifdef OPKW_STAMPS
@@ -386,7 +365,9 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
         const int chl = wn * WN + 4 * eq;                        // first channel of a lane's fragment
         int prow[MF];   // padded-image positions (< 2^24, launch_conv3 checks)
         bool pok[MF];
-        {
+        if (g.nstrips == 1) {   // (conv3_dev.h Strips::rows1)
+            g.rows1<MF>(p0 + wm * WROWS + er16, a.W, prow, pok);
+        } else {
             const int pbase = p0 + wm * WROWS + er16;
             int f, yy, xx, s;
             prow[0] = (int)g.map(pbase, f, yy, xx, s);
@@ -442,7 +423,7 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
         uint32_t vrow[MF];
 #pragma unroll
         for (int i = 0; i < MF; ++i)
-            vrow[i] = BST && pok[i] && !OPKW_SINK_ONLY ? (uint32_t)prow[i] * (uint32_t)(cs0 * 2) : kBufOOB;
+            vrow[i] = BST && pok[i] && !OPKW_SINK_ONLY ? __umul24((uint32_t)prow[i], (uint32_t)(cs0 * 2)) : kBufOOB;
 #define OPKW_STORE(T_, sink_, ch_, i_, val_)                                                  \
     do {                                                                                      \
         if constexpr (BST) {                                                                  \
@@ -507,7 +488,6 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
 #undef OPKW_ABASE
 #undef OPKW_BBASE
 #undef OPKW_ISSUE
-#undef OPKW_ISSUE2
 #undef OPKW_AROW
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     OPKW_STAMP(6);
@@ -534,7 +514,6 @@ void launch_conv3w(const ConvArgs& a, hipStream_t stream)
     const unsigned G = (unsigned)std::min<long>(a.cus, ntm);
     OPK_CHECK_ARG(G <= 1024, "persistent grid exceeds the sink");
     const bool dma_end = dev_switch("CONV3W", 1) != 2;   // 2: DMA right after the barrier (A/B)
-    const bool he = dev_switch("CONV3W_HE", 0) != 0;
     // buffer-resource epilogue stores (BUFST=0: pointer stores, A/B): one destination whose
     // positions x channel stride fit the 31-bit offsets of the raw buffer range check
     ConvArgs b = a;
@@ -544,11 +523,8 @@ void launch_conv3w(const ConvArgs& a, hipStream_t stream)
     // (the DMA-after-barrier A/B variant only with the select activation)
 #define OPKW_LAUNCH(BN_, DE_, MX_)                                                                 \
     do {                                                                                          \
-        note_launch("conv3w_kernel<%d,%d,%d,%d%s>", BN_, (int)DE_, (int)MX_, b.bufst,            \
-                    DE_ && b.bufst && he ? ",HE" : "");                                           \
-        if (DE_ && b.bufst && he)                                                                 \
-            hipLaunchKernelGGL((conv3w_kernel<BN_, DE_, MX_, true, DE_>), dim3(G), dim3(64 * kW_NW), 0, stream, b); \
-        else if (b.bufst)                                                                         \
+        note_launch("conv3w_kernel<%d,%d,%d,%d>", BN_, (int)DE_, (int)MX_, b.bufst);              \
+        if (b.bufst)                                                                              \
             hipLaunchKernelGGL((conv3w_kernel<BN_, DE_, MX_, true>), dim3(G), dim3(64 * kW_NW), 0, stream, b); \
         else                                                                                      \
             hipLaunchKernelGGL((conv3w_kernel<BN_, DE_, MX_, false>), dim3(G), dim3(64 * kW_NW), 0, stream, b); \

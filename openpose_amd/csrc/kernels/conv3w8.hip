@@ -60,9 +60,7 @@ typedef unsigned int opk8_u4 __attribute__((ext_vector_type(4)));
 #define OPK_FAULT_POOL 0
 #endif
 
-// HE: conv3w.hip's halo-early schedule (a chunk's halo DMA one K unit earlier; dev switch
-// CONV3W8_HE, A/B)
-template <int BN, int NB, bool POOL, bool MX, bool BST, bool HE = false>
+template <int BN, int NB, bool POOL, bool MX, bool BST>
 __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a)
 {
     constexpr int NW = k8_NW, BM = k8_BM, HR = k8_HR;
@@ -119,8 +117,6 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     const int U = 3 * cpt;
     const int ublk = nblk * U;   // the n-block's first K unit in the packed weights
     const int bi = (BPI - wave + NW - 1) / NW;
-    const int ai = (API - wave + NW - 1) / NW;   // halo DMA instructions of this wave
-    (void)ai;
     // weight piece of B DMA instruction j (recomputed at each issue: registers)
 #define OPK8_BOFF(j_)                                                                         \
     ({                                                                                        \
@@ -142,10 +138,9 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     do {                                                                                      \
         _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_) dst_[i_] = OPK8_AROW1(mt_, i_);     \
     } while (0)
-#define OPK8_ISSUE(c_, ky_, aslot_, bslot_, nt_) OPK8_ISSUE2(c_, ky_, aslot_, bslot_, nt_, (ky_) == 0, true)
-#define OPK8_ISSUE2(c_, ky_, aslot_, bslot_, nt_, HALO_, WTS_)                                \
+#define OPK8_ISSUE(c_, ky_, aslot_, bslot_, nt_)                                              \
     do {                                                                                      \
-        if ((HALO_) && (OPK8_ABLATE != 7 || !dma_ab)) {                                       \
+        if ((ky_) == 0 && (OPK8_ABLATE != 7 || !dma_ab)) {                                    \
             const int as_ = (aslot_) * ASLOT;                                                 \
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
                 if (API % NW == 0 || i_ * NW + wave < API)                                    \
@@ -158,7 +153,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         const int bs_ = 2 * ASLOT + (bslot_) * BSLOT;                                         \
         const uint16_t* ub_ = a.w + (size_t)(ublk + (c_) * 3 + (ky_)) * BROWS * 32;                  \
         _Pragma("unroll") for (int j_ = 0; j_ < BIW; ++j_)                                    \
-            if ((WTS_) && (BPI % NW == 0 || j_ * NW + wave < BPI) && (OPK8_ABLATE != 8 || !dma_ab)) { \
+            if ((BPI % NW == 0 || j_ * NW + wave < BPI) && (OPK8_ABLATE != 8 || !dma_ab)) {   \
                 const int bo_ = OPK8_BOFF(j_);                                                \
                 __builtin_amdgcn_global_load_lds(                                             \
                     (const void*)(ub_ + bo_),                                                 \
@@ -305,25 +300,16 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         const bool nt_ = u + 2 >= U;                                                          \
         const int u2_ = nt_ ? u + 2 - U : u + 2;                                              \
         const int c2_ = u2_ / 3;                                                              \
-        OPK8_ISSUE2(c2_, u2_ - 3 * c2_, (gc + (nt_ ? cpt : 0) + c2_) & 1, (u + 2) % 3, nt_,   \
-                    !HE && u2_ - 3 * c2_ == 0, true);                                         \
-    } while (0)
-#define OPK8_HALO_NEXT()                                                                      \
-    do {                                                                                      \
-        const bool nt_ = c + 1 >= cpt;                                                        \
-        OPK8_ISSUE2(nt_ ? 0 : c + 1, 0, (gc + c + 1) & 1, 0, nt_, true, false);               \
+        OPK8_ISSUE(c2_, u2_ - 3 * c2_, (gc + (nt_ ? cpt : 0) + c2_) & 1, (u + 2) % 3, nt_);  \
     } while (0)
             OPK8_TAP(0, ab0, ab1, bb_u, BN * 64, fbE, fbO);
             OPK8_TAP(1, ab1, ab2, bb_u, 2 * BN * 64, fbO, fbE);
             if (u == 0 && gc > 0) vm_wait<S1>();
-            else if (HE && ky == 1) vm_wait_rt(ai);   // the next chunk's halo is younger
             else vm_wait<0>();
             if (OPK8_ABLATE != 1) __builtin_amdgcn_s_barrier();
             OPK8_TAP(2, ab2, nab, nbb, 0, fbE, fbO);
             if (OPK8_ABLATE != 4 || u + 2 >= U) OPK8_DMA_U2();
-            if (HE && ky == 0 && (OPK8_ABLATE != 4 || c + 1 >= cpt)) OPK8_HALO_NEXT();
 #undef OPK8_DMA_U2
-#undef OPK8_HALO_NEXT
         }
 
         // ---- epilogue: bias + activation + fp16 pack, 16-byte stores (border lanes to the sink)
@@ -335,7 +321,9 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         const int cw = 16 * (eq & 1) + 8 * (eq >> 1);   // channel of a lane's 16-byte store
         int prow[MF];
         bool pok[MF];
-        {
+        if (g.nstrips == 1 && !POOL) {   // (conv3_dev.h Strips::rows1)
+            g.rows1<MF>(OPK8_P0(m) + wave * WROWS + er16, a.W, prow, pok);
+        } else {
             const int pbase = OPK8_P0(m) + wave * WROWS + er16;
             int f, yy, xx, s;
             prow[0] = (int)g.map(pbase, f, yy, xx, s);
@@ -492,7 +480,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                 const uint4 val = make_uint4(sl[0], sh[0], sl[1], sh[1]);
                 const int ch = cw + j * 16;
                 if constexpr (BST) {
-                    const uint32_t off = pok[i] ? ((uint32_t)prow[i] * (uint32_t)cs0 + ch) * 2 : kBufOOB;
+                    const uint32_t off = pok[i] ? (__umul24((uint32_t)prow[i], (uint32_t)cs0) + ch) * 2 : kBufOOB;
                     __builtin_amdgcn_raw_buffer_store_b128((opk8_u4){val.x, val.y, val.z, val.w}, rs0,
                                                            (int)off, 0, 0);
                 } else if (nd == 1) {
@@ -525,7 +513,6 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
 #undef OPK8_ABASE
 #undef OPK8_BBASE
 #undef OPK8_ISSUE
-#undef OPK8_ISSUE2
 #undef OPK8_AROW
 #undef OPK8_AROW1
 #undef OPK8_P0
@@ -576,14 +563,10 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
                         a.dst_cs[0] * 2;
     const long pextent = ((long)a.frames * (a.H / 2 + 2) * (a.W / 2 + 2) + kConvGuardTail) * a.dst_cs[0] * 2;
     b.bufst = a.ndst == 1 && (pool ? pextent : extent) < (1L << 31) - 4096 && dev_switch("BUFST", 1) != 0;
-    const bool he = dev_switch("CONV3W8_HE", 0) != 0;
 #define OPK8_LAUNCH2(BN_, NB_, P_, MX_)                                                          \
     do {                                                                                        \
-        note_launch("conv3w8_kernel<%d,%d,%d,%d,%d%s>", BN_, NB_, (int)P_, (int)MX_, b.bufst,    \
-                    b.bufst && he ? ",HE" : "");                                                 \
-        if (b.bufst && he)                                                                      \
-            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, MX_, true, true>), dim3(G), dim3(64 * k8_NW), 0, stream, b); \
-        else if (b.bufst)                                                                       \
+        note_launch("conv3w8_kernel<%d,%d,%d,%d,%d>", BN_, NB_, (int)P_, (int)MX_, b.bufst);      \
+        if (b.bufst)                                                                            \
             hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, MX_, true>), dim3(G), dim3(64 * k8_NW), 0, stream, b); \
         else                                                                                    \
             hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, MX_, false>), dim3(G), dim3(64 * k8_NW), 0, stream, b); \

@@ -4,8 +4,9 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -Iinclude -o tools/conv3w_probe_bin tools/conv3w_probe.hip
 //   conv3w_probe [frames H W cin cout iters dma_end zero_operands variant]
 //   variant 1 (NOSTAMPS builds): conv3w8, checked bit for bit against conv3w
-//   variant 3 (NOSTAMPS builds): conv3w8 with the halo-early schedule, checked against conv3w
-//   variant 2: conv3w with the halo-early DMA schedule (CONV3W_HE), checked bit for bit against conv3w
+//   (round 4 also had variant 2 / 3: conv3w / conv3w8 with the rejected E2 and halo-early
+//   schedules -- profiles/round4/stage_skeleton/)
+//   OPK_<SWITCH>=<value> in the environment sets a dev switch
 #ifndef NOSTAMPS
 #define OPKW_STAMPS
 #endif
@@ -22,12 +23,11 @@
 
 using namespace opk;
 
-static int g_dma_end = 0, g_e2 = 0;
+static int g_dma_end = 0;
 void opk::note_launch(const char*, ...) {}
 int opk::dev_switch(const char* key, int dflt)
 {
     if (std::string(key) == "CONV3W") return g_dma_end ? 1 : 2;
-    if ((std::string(key) == "CONV3W_HE" || std::string(key) == "CONV3W8_HE") && g_e2) return 1;
     const char* e = std::getenv((std::string("OPK_") + key).c_str());
     return e ? std::atoi(e) : dflt;
 }
@@ -122,16 +122,9 @@ int main(int argc, char** argv)
     CK(hipEventCreate(&e1));
     auto launch = [&](const ConvArgs& x) {
 #ifdef NOSTAMPS
-        if (variant == 1 || variant == 3) {
-            g_e2 = variant == 3;
-            launch_conv3w8(x, 0);
-            g_e2 = 0;
-            return;
-        }
+        if (variant == 1) { launch_conv3w8(x, 0); return; }
 #endif
-        g_e2 = variant == 2;
         launch_conv3w(x, 0);
-        g_e2 = 0;
     };
     CK(hipMemset(dout, 0, out_elems * 2));
     for (int i = 0; i < 5; ++i) launch(a);
@@ -144,7 +137,7 @@ int main(int argc, char** argv)
     CK(hipEventElapsedTime(&ms, e0, e1));
     const double us = ms * 1e3 / iters;
     const double flops = 2.0 * frames * H * W * (double)cout * cin * 9;
-    if (variant >= 1) {   // bit-identity against conv3w
+    if (variant == 1) {   // bit-identity against conv3w
         uint16_t* dref;
         CK(hipMalloc(&dref, out_elems * 2));
         CK(hipMemset(dref, 0, out_elems * 2));

@@ -1,6 +1,7 @@
 #!/bin/bash
 # round-4 GPU call: new parity tests (+ the fault-injected variant, expected to fail), the GPU
-# suite, smoke, bench.  OUT_TAG=<dir>  STEPS=<env,new,fault,tests,smoke,bench,multi,b135,prof>
+# suite, smoke, bench.  OUT_TAG=<dir>  STEPS=<env,new,fault,tests,smoke,bench,multi,b135,prof,pmc>
+# (pmc: PMC_COMMIT=<sha of the tree> -- the box has no .git)
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
 OUT=gpurun_out/${OUT_TAG:-r4}
 STEPS=${STEPS:-env,new,fault,tests,smoke,bench}
@@ -81,4 +82,8 @@ if run msab; then   # multi-scale (config 4, 4 sources) NMS walk A/B
       timeout -k 10 200 python -u bench.py --config multiscale --steps 15 --no-cpu-baseline --dev NMS_WALK=$v > $OUT/msab_w${v}_$i.log 2>&1 || exit 1
     done
   done
+fi
+if run pmc; then   # counter passes at this tree (config 2 at the bench batch, config 5 at 64 frames)
+  PMC_COMMIT=$PMC_COMMIT bash tools/pmc_round.sh ${OUT_TAG:-r4}/pmc || exit 1
+  PMC_COMMIT=$PMC_COMMIT bash tools/pmc_round.sh ${OUT_TAG:-r4}/pmc_body135 --config body135 --batch 64 || exit 1
 fi
