@@ -297,8 +297,8 @@ def post_roofline(batch, post_ms, pmc_path=POST_PMC, ref_bytes_frame=POST_BYTES_
     out.update({"valu_frac": round(vf, 4), "hbm_frac": round(hf, 4),
                 "pmc_per_step": {"valu_wave_insts": pmc["valu_insts"], "hbm_bytes": pmc["hbm_bytes"]},
                 "pmc_source": pmc_provenance(pmc_path),
-                "note": "neither bound is near its peak: NMS detect (~70 % of the time) waits on "
-                        "dependent loads of its rolling window (latency)"})
+                "note": "neither bound is near its peak: the NMS walk (the largest post kernel) is "
+                        "bound by its scalar instruction stream (row tables, taps), DESIGN.md 4.8"})
     return out
 
 
