@@ -81,6 +81,60 @@ __device__ __forceinline__ float score_ab(const float* a, const float* b, const 
     return ((double)dist < near_dist) ? reject_score : 0.f;
 }
 
+// The same score with one candidate line per 32-lane half of a wave and one sample per lane
+// (valid: the half has a line; s: the lane's sample index).  Neighbouring samples of a line read
+// neighbouring source pixels, so a lane group's LDS reads are near-broadcasts instead of 32 random
+// gathers (the per-lane-line form spent 60 % of its LDS cycles on bank conflicts, config 5 PMC).
+// Bit-identical to score_ab: every lane evaluates its sample with score_ab's expressions; the
+// count is the half's ballot; the sum is taken in sample order through readlane, the samples at
+// or below the threshold (and the lanes past n) adding +0.0f -- exact, as the running sum starts
+// at +0 and is never -0.  The return value is valid in every lane of the half.
+template <bool LDS>
+__device__ __forceinline__ float score_ab_spl(const float* a, const float* b, const HeatMap& M,
+                                              int plane_x, int plane_y, float inter_th,
+                                              float inter_min_above, float reject_score,
+                                              double near_dist, const float* lx, const float* ly,
+                                              const int* loff, bool valid, int s, int half)
+{
+    const int W = M.w, H = M.h;
+    float vx = 0.f, vy = 0.f, w = 0.f;
+    int n = 5;
+    bool degenerate = true, pass = false;
+    if (valid) {
+        vx = b[0] - a[0];
+        vy = b[1] - a[1];
+        const float vmax = fmaxf(fabsf(vx), fabsf(vy));
+        n = max(5, min(25, round_pos(sqrtf(5 * vmax))));
+        const float norm = sqrtf(vx * vx + vy * vy);
+        degenerate = !((double)norm > 1e-6);
+        if (!degenerate && s < n) {
+            const float ux = vx / norm, uy = vy / norm;
+            const float stepx = vx / (float)n, stepy = vy / (float)n;
+            const int px = max(0, min(W - 1, round_pos(a[0] + (float)s * stepx)));
+            const int py = max(0, min(H - 1, round_pos(a[1] + (float)s * stepy)));
+            const float hx = LDS ? heat_at_lds(M, lx, loff, px, py) : heat_at(M, plane_x, px, py);
+            const float hy = LDS ? heat_at_lds(M, ly, loff, px, py) : heat_at(M, plane_y, px, py);
+            const float v = ux * hx + uy * hy;
+            pass = v > inter_th;
+            w = pass ? v : 0.f;
+        }
+    }
+    const uint64_t bal = __builtin_amdgcn_ballot_w64(pass);
+    const unsigned count = (unsigned)__builtin_popcountll(half ? bal >> 32 : bal & 0xffffffffull);
+    float sum0 = 0.f, sum1 = 0.f;
+    const int wi = __builtin_bit_cast(int, w);
+#pragma unroll
+    for (int k = 0; k < 25; ++k) {   // n <= 25
+        sum0 = sum0 + __builtin_bit_cast(float, __builtin_amdgcn_readlane(wi, k));
+        sum1 = sum1 + __builtin_bit_cast(float, __builtin_amdgcn_readlane(wi, 32 + k));
+    }
+    const float sum = half ? sum1 : sum0;
+    if (degenerate) return 0.f;
+    if ((float)count / (float)n > inter_min_above) return sum / (float)count;
+    const float dist = sqrtf(vx * vx + vy * vy);
+    return ((double)dist < near_dist) ? reject_score : 0.f;
+}
+
 struct PafArgs {
     HeatMap heat;
     const float* peaks;
@@ -136,7 +190,9 @@ __device__ __forceinline__ void stage_planes(const PafArgs& A, int plx, int ply,
     __syncthreads();
 }
 
-template <bool LDS>
+// SPL: pairs with few candidate lines take one line per half-wave, one sample per lane
+// (score_ab_spl); otherwise one line per lane
+template <bool LDS, bool SPL>
 __global__ __launch_bounds__(256) void paf_dense_kernel(float* __restrict__ scores, PafArgs A)
 {
     const int q = blockIdx.x, b = blockIdx.y;
@@ -148,6 +204,23 @@ __global__ __launch_bounds__(256) void paf_dense_kernel(float* __restrict__ scor
     const bool use = LDS && na * nb >= kPafLdsMinLines;
     if (use) stage_planes<LDS>(A, plx, ply, loff, lx, ly);
     float* out = scores + ((size_t)b * A.npairs + q) * A.max_peaks * A.max_peaks;
+    // one sample per lane only for pairs with few candidate lines (< kPafLdsMinLines, never staged):
+    // with many lines the half-waves' idle lanes and the in-order sums cost more than the
+    // per-lane walks' LDS bank conflicts (config 5, 20 people: 0.82 -> 1.56 ms per step)
+    if (SPL && na * nb < kPafLdsMinLines) {
+        const int lane = threadIdx.x & 63, half = lane >> 5, s = lane & 31;
+        const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+        for (int t0 = 2 * wv; t0 < na * nb; t0 += 2 * nw) {   // wave-uniform
+            const int t = t0 + half;
+            const bool valid = t < na * nb;
+            const int i = valid ? t / nb : 0, j = valid ? t - (t / nb) * nb : 0;
+            const float sc = score_ab_spl<false>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply,
+                                                 A.inter_th, A.inter_min_above, A.reject_score,
+                                                 A.near_dist, lx, ly, loff, valid, s, half);
+            if (valid && s == 0) out[(size_t)i * A.max_peaks + j] = sc;
+        }
+        return;
+    }
     for (int t = threadIdx.x; t < na * nb; t += blockDim.x) {
         const int i = t / nb, j = t - (t / nb) * nb;
         out[(size_t)i * A.max_peaks + j] =
@@ -160,7 +233,7 @@ __global__ __launch_bounds__(256) void paf_dense_kernel(float* __restrict__ scor
 
 // compact records: offset of pair q = sum over earlier pairs of nA*nB (recomputed per block from
 // the 2*q peak counts it needs -- 26 pairs, cheaper than a separate scan launch).
-template <bool LDS>
+template <bool LDS, bool SPL>
 __global__ __launch_bounds__(256) void paf_compact_kernel(float* __restrict__ records,
                                                           int rec_floats, PafArgs A)
 {
@@ -187,6 +260,23 @@ __global__ __launch_bounds__(256) void paf_compact_kernel(float* __restrict__ re
     const bool use = LDS && na * nb >= kPafLdsMinLines;
     if (use) stage_planes<LDS>(A, plx, ply, loff, lx, ly);
     float* out = rec + 1 + offset;
+    // one sample per lane only for pairs with few candidate lines (< kPafLdsMinLines, never staged):
+    // with many lines the half-waves' idle lanes and the in-order sums cost more than the
+    // per-lane walks' LDS bank conflicts (config 5, 20 people: 0.82 -> 1.56 ms per step)
+    if (SPL && na * nb < kPafLdsMinLines) {
+        const int lane = threadIdx.x & 63, half = lane >> 5, s = lane & 31;
+        const int wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+        for (int t0 = 2 * wv; t0 < na * nb; t0 += 2 * nw) {   // wave-uniform
+            const int t = t0 + half;
+            const bool valid = t < na * nb;
+            const int i = valid ? t / nb : 0, j = valid ? t - (t / nb) * nb : 0;
+            const float sc = score_ab_spl<false>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply,
+                                                 A.inter_th, A.inter_min_above, A.reject_score,
+                                                 A.near_dist, lx, ly, loff, valid, s, half);
+            if (valid && s == 0) out[t] = sc;
+        }
+        return;
+    }
     for (int t = threadIdx.x; t < na * nb; t += blockDim.x) {
         const int i = t / nb, j = t - (t / nb) * nb;
         out[t] = use ? score_ab<true>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
@@ -240,8 +330,11 @@ void launch_paf_scores(float* scores, const HeatMap& heat, const float* peaks, i
     PafArgs a = make_args(heat, peaks, max_peaks, t, inter_th, inter_min_above, reject_score,
                           near_dist);
     const size_t lds = paf_lds_bytes(heat);
-    if (lds) hipLaunchKernelGGL(paf_dense_kernel<true>, dim3(t.npairs, frames), dim3(256), lds, stream, scores, a);
-    else hipLaunchKernelGGL(paf_dense_kernel<false>, dim3(t.npairs, frames), dim3(256), 0, stream, scores, a);
+    const bool spl = dev_switch("PAF_SPL", 1) != 0;
+    if (lds && spl) hipLaunchKernelGGL((paf_dense_kernel<true, true>), dim3(t.npairs, frames), dim3(256), lds, stream, scores, a);
+    else if (lds) hipLaunchKernelGGL((paf_dense_kernel<true, false>), dim3(t.npairs, frames), dim3(256), lds, stream, scores, a);
+    else if (spl) hipLaunchKernelGGL((paf_dense_kernel<false, true>), dim3(t.npairs, frames), dim3(256), 0, stream, scores, a);
+    else hipLaunchKernelGGL((paf_dense_kernel<false, false>), dim3(t.npairs, frames), dim3(256), 0, stream, scores, a);
     OPK_LAUNCH_CHECK();
 }
 
@@ -254,11 +347,19 @@ void launch_paf_scores_compact(float* records, int rec_floats, const HeatMap& he
     PafArgs a = make_args(heat, peaks, max_peaks, t, inter_th, inter_min_above, reject_score,
                           near_dist);
     const size_t lds = paf_lds_bytes(heat);
-    if (lds)
-        hipLaunchKernelGGL(paf_compact_kernel<true>, dim3(t.npairs, frames), dim3(256), lds, stream,
+    // PAF_SPL (dev A/B): 0 = one candidate line per lane
+    const bool spl = dev_switch("PAF_SPL", 1) != 0;
+    if (lds && spl)
+        hipLaunchKernelGGL((paf_compact_kernel<true, true>), dim3(t.npairs, frames), dim3(256), lds, stream,
+                           records, rec_floats, a);
+    else if (lds)
+        hipLaunchKernelGGL((paf_compact_kernel<true, false>), dim3(t.npairs, frames), dim3(256), lds, stream,
+                           records, rec_floats, a);
+    else if (spl)
+        hipLaunchKernelGGL((paf_compact_kernel<false, true>), dim3(t.npairs, frames), dim3(256), 0, stream,
                            records, rec_floats, a);
     else
-        hipLaunchKernelGGL(paf_compact_kernel<false>, dim3(t.npairs, frames), dim3(256), 0, stream,
+        hipLaunchKernelGGL((paf_compact_kernel<false, false>), dim3(t.npairs, frames), dim3(256), 0, stream,
                            records, rec_floats, a);
     OPK_LAUNCH_CHECK();
 }

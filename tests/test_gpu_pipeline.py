@@ -17,7 +17,7 @@ import torch
 import oracle
 from oracle import body25
 from openpose_amd import synth
-from openpose_amd.api import Net, PoseExtractor
+from openpose_amd.api import Net, PoseExtractor, dev_switches
 from openpose_amd.pose_tables import BODY_135, CONNECT_GPU
 from tests.golden.make_golden import connector_field
 
@@ -257,13 +257,20 @@ def test_gpu_connector_gpu_semantics_matches_reference_fixture(ctx, path):
     np.testing.assert_array_equal(ks, g["scores"])
 
 
+@pytest.mark.parametrize("spl", [1, 0])
 @pytest.mark.parametrize("model,people", [(BODY_135, 20), (0, 5), (0, 20)])
-def test_pose_injection_gpu_semantics(ctx, model, people):
+def test_pose_injection_gpu_semantics(ctx, model, people, spl):
     """BODY_135 through the poseNetOutput injection path -- 439 x 46 x 82
     net output, 20 synthetic people, GPU-path connector -- bit-exact against the oracle chain
     (resize -> NMS -> getScoreAB table -> global-sort assembly); BODY_25 with the same semantics.
     5 people: every pair's line integrals read the sources through L2; 20 people (>= 64 candidate
-    lines per pair): through the planes staged in LDS (paf.hip)."""
+    lines per pair): through the planes staged in LDS (paf.hip).  spl: the line integrals with one
+    sample per lane (the default) and with one line per lane (PAF_SPL=0)."""
+    with dev_switches(PAF_SPL=spl):
+        _pose_injection_gpu_semantics(ctx, model, people)
+
+
+def _pose_injection_gpu_semantics(ctx, model, people):
     t = oracle.pose_tables()[model]
     C = t["parts"] + int(t["bkg"]) + len(t["map_idx"])
     fields = np.stack([synth.overlay(people, 46, 82, seed=1500 + k, table=t) +

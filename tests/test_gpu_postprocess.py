@@ -8,6 +8,7 @@ import torch
 
 import oracle
 from openpose_amd import pose_tables as pt
+from openpose_amd.api import dev_switches
 from tests.fields import noise_field, people_field, smooth_noise_field
 
 pytestmark = pytest.mark.gpu
@@ -76,7 +77,15 @@ def test_nms_tiny_maps(ctx):
         _peaks_equal(peaks.cpu().numpy()[0], oracle.nms(f, 0.05, 128))
 
 
-def test_paf_scores_bitexact(ctx):
+@pytest.mark.parametrize("spl", [1, 0])
+def test_paf_scores_bitexact(ctx, spl):
+    """Dense pair scores (materialised map: the sources read through L2) against the oracle's
+    getScoreAB table, one sample per lane (default) and one line per lane (PAF_SPL=0)."""
+    with dev_switches(PAF_SPL=spl):
+        _paf_scores_bitexact(ctx)
+
+
+def _paf_scores_bitexact(ctx):
     f = people_field(6, 368, 656, seed=7)
     pk = oracle.nms(f, 0.05, 128, (0.25, 0.25))
     scores = torch.zeros((1, 26, 127, 127), device="cuda")
