@@ -368,14 +368,33 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                     qrow[i] = qok[i] ? (f * OHp + ((yy - 1) >> 1) + 1) * OWp + ((s * g.sw + xx - 1) >> 1) + 1 : 0;
                 }
             }
-            // (BST) byte offsets of the window's first / second-row lanes, the other lanes out of range
-            uint32_t qo1[MF], qo2[MF];
+            // (BST) byte offsets of the window's second-row lanes (which store the pooled value), the
+            // other lanes out of range
+            uint32_t qo2[MF];
+#pragma unroll
+            for (int i = 0; i < MF; ++i)
+                qo2[i] = qok[i] && !first[i] ? ((uint32_t)qrow[i] * (uint32_t)cs0 + cw) * 2 : kBufOOB;
+            // The window's two rows meet in LDS: the halo slot of the tile's last chunk is free once
+            // every wave has passed its last reads of it (the barrier below), and the next write into
+            // it is the next tile's chunk-1 DMA, issued after that tile's mid-unit-1 barrier.  First-
+            // row lanes leave their column-pair max there, second-row lanes read it back -- instead
+            // of a store to the pooled image, vmcnt(0), a barrier and a load of the same bytes.
+            // Window slot = (local row / 2) x (VW / 2) + (column - 1) / 2 of the tile's 6 x VW
+            // positions (< 3 x 43 slots of 256 bytes), the 16 16-byte pieces of a slot rotated by the
+            // slot so that neighbouring windows' pieces fall on different banks.
+            __builtin_amdgcn_s_barrier();
+            // (the slot bases are 256-byte aligned, so fragment pair j's piece is the lane's piece
+            // for j = 0 with bits 6-7 flipped by 32 j: one XOR per access, four address registers)
+            char* const xch = reinterpret_cast<char*>(lds + ((gc + cpt - 1) & 1) * ASLOT);
+            uint32_t xoff[MF];
 #pragma unroll
             for (int i = 0; i < MF; ++i) {
-                const uint32_t o = ((uint32_t)qrow[i] * (uint32_t)cs0 + cw) * 2;
-                qo1[i] = qok[i] && first[i] ? o : kBufOOB;
-                qo2[i] = qok[i] && !first[i] ? o : kBufOOB;
+                const int k1 = wave * WROWS + i * 16 + er16 + 1;   // tile-local position + 1
+                const int lr = fdiv(k1, g.VW, g.rv), xx = k1 - lr * g.VW;
+                const int slot = (lr >> 1) * (g.VW >> 1) + ((xx - 1) >> 1);
+                xoff[i] = qok[i] ? (uint32_t)(slot * 256 + (((cw >> 3) ^ slot) & 15) * 16) : 0u;
             }
+#define OPK8_XCH(i_, j_) reinterpret_cast<uint4*>(xch + (xoff[i_] ^ (uint32_t)((j_) * 2)))
             uint4 keep[MF][NF / 2];
 #pragma unroll
             for (int j = 0; j < NF; j += 2) {
@@ -411,32 +430,17 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                     const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
                     const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
                     keep[i][j / 2] = make_uint4(sl[0], sh[0], sl[1], sh[1]);
-                    if constexpr (BST) {
-                        const uint4 k4 = keep[i][j / 2];
-                        __builtin_amdgcn_raw_buffer_store_b128((opk8_u4){k4.x, k4.y, k4.z, k4.w}, rs0,
-                                                               (int)(qo1[i] + j * 32), 0, 0);
-                    } else {
-                        uint4* p = reinterpret_cast<uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
-                        *(qok[i] && first[i] ? p : sink4) = keep[i][j / 2];
-                    }
+                    if (qok[i] && first[i]) *OPK8_XCH(i, j * 16) = keep[i][j / 2];
                 }
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __builtin_amdgcn_s_barrier();
+            __syncthreads();   // (lgkmcnt(0) + barrier: the first rows are in LDS)
             uint4 got[MF][NF / 2];
 #pragma unroll
             for (int j = 0; j < NF; j += 2)
 #pragma unroll
-                for (int i = 0; i < MF; ++i) {
-                    if constexpr (BST) {
-                        const opk8_u4 g4 = __builtin_amdgcn_raw_buffer_load_b128(rs0, (int)(qo2[i] + j * 32), 0, 0);
-                        got[i][j / 2] = make_uint4(g4.x, g4.y, g4.z, g4.w);
-                    } else {
-                        const uint4* p = reinterpret_cast<const uint4*>(d0 + cw + j * 16 + (size_t)qrow[i] * cs0);
-                        got[i][j / 2] = *(qok[i] && !first[i] ? p : sink4);
-                    }
-                }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                for (int i = 0; i < MF; ++i)
+                    got[i][j / 2] = *OPK8_XCH(i, j * 16);   // (used by the second-row lanes only)
+#undef OPK8_XCH
 #pragma unroll
             for (int j = 0; j < NF; j += 2)
 #pragma unroll
