@@ -262,8 +262,13 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     const float* lb = lbias + wn * 128 + 4 * q;
     const float* lm = lmul + wn * 128 + 4 * q;
     // (read per tile, not hoisted out of the persistent loop into registers it has not got)
-    const uint16_t* w7 = a.w7;
-    asm volatile("" : "+s"(w7));
+    const uint16_t* w7o = a.w7;
+    asm volatile("" : "+s"(w7o));
+    // (global address space again: through the opaque copy the loads would be flat_load, which
+    // also count in lgkmcnt -- every wait for them drained the LDS reads as well)
+    typedef const __attribute__((address_space(1))) half8_t* gh8p;
+    const __attribute__((address_space(1))) uint16_t* w7 =
+        (const __attribute__((address_space(1))) uint16_t*)w7o;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
         half8_t a7[NF2];
@@ -274,7 +279,7 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
                 const int sl = (KS + r / N1) % 3;
                 a7[f] = __builtin_bit_cast(half8_t, lds[3 * ASLOT + sl * BSLOT + swz64(r % N1, q)]);
             } else {
-                a7[f] = *reinterpret_cast<const half8_t*>(w7 + (size_t)(f * 16 + r16) * N1 + wn * 128 +
+                a7[f] = *reinterpret_cast<gh8p>(w7 + (size_t)(f * 16 + r16) * N1 + wn * 128 +
                                                           kb * 32 + q * 8);
             }
         }
