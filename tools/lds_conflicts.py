@@ -1,7 +1,9 @@
 """LDS bank-conflict model (dev tool): per-instruction lane groups of MI355X_MICROARCH.md §LDS, one
 LDS cycle per group, extra cycles = (most distinct dwords on one bank of a group) - 1.  Models the
-LDS access patterns of conv1_fused_kernel (before / after the round-4 layouts); the model's
-extra-cycle fraction for the round-3 kernel is 0.195 against the PMC's 0.194.
+LDS access patterns of conv1_fused_kernel (round-3 layouts, round-4 layouts, and round-4 with the
+2x2 pool in registers: fragment rows = 2 halo rows x 8 columns, halo swizzle with a row-parity
+term, no epilogue tile); the model's extra-cycle fraction for the round-3 kernel is 0.195 against
+the PMC's 0.194.
 
     python tools/lds_conflicts.py
 """
@@ -38,9 +40,13 @@ HROWS = (TR + 2) * VW + 8
 PR = TR + 4
 
 
-def conv1(new):
+def conv1(ver):
+    new = ver >= 4
     PC, PS, PD = (67, 683, 2072) if new else (66, 660, 0)
-    hswz = (lambda r: (r >> 1) & 3) if new else (lambda r: ((r >> 2) & 1) << 1)
+    if ver == 5:
+        hswz = lambda r: ((r >> 1) & 3) ^ ((r >> 6) & 1)
+    else:
+        hswz = (lambda r: (r >> 1) & 3) if new else (lambda r: ((r >> 2) & 1) << 1)
     tot = {}
 
     def add(name, kind, addrs):
@@ -80,7 +86,11 @@ def conv1(new):
             for i in range(3):
                 a = []
                 for l in range(64):
-                    row = wave * 48 + i * 16 + (l & 15) + (tap // 3) * VW + tap % 3
+                    if ver == 5:
+                        r16 = l & 15
+                        row = (2 * i + (r16 & 1) + tap // 3) * VW + 8 * wave + (r16 >> 1) + tap % 3
+                    else:
+                        row = wave * 48 + i * 16 + (l & 15) + (tap // 3) * VW + tap % 3
                     a.append((c * HROWS * 4 + row * 4 + ((l >> 4) ^ hswz(row))) * 16)
                 add("A fragment ds_read_b128", "r128", a)
         for st in range(18):   # conv1_2 B fragments (weights, conv3 swizzle) -- unchanged
@@ -89,7 +99,7 @@ def conv1(new):
                 a = [((c * 9 + tap) * 256 + (j * 16 + (l & 15)) * 4 + ((l >> 4) ^ ((((j * 16 + (l & 15)) >> 2) & 1) << 1))) * 16
                      for l in range(64)]
                 add("B fragment ds_read_b128", "r128", a)
-        for i in range(3):     # epilogue tile writes (row stride 72 halves) -- unchanged
+        for i in range(3 if ver < 5 else 0):   # epilogue tile writes (row stride 72 halves)
             for j in (0, 2):
                 a = []
                 for l in range(64):
@@ -97,7 +107,7 @@ def conv1(new):
                     q = l >> 4
                     a.append((m * 72 + j * 16 + 16 * (q & 1) + 8 * (q >> 1)) * 2)
                 add("T ds_write_b128", "w128", a)
-    for rnd in range(2):
+    for rnd in range(2 if ver < 5 else 0):
         for wave in range(8):
             for which in range(4):
                 a = []
@@ -121,9 +131,9 @@ def conv1(new):
 
 
 if __name__ == "__main__":
-    for new in (False, True):
-        tot = conv1(new)
-        print("conv1_fused, %s layouts:" % ("round-4" if new else "round-3"))
+    for ver in (3, 4, 5):
+        tot = conv1(ver)
+        print("conv1_fused, %s layouts:" % {3: "round-3", 4: "round-4", 5: "round-4 register pool"}[ver])
         for k, (b, e) in tot.items():
             print("  %-26s base %5d  extra %5d" % (k, b, e))
         B = sum(b for b, _ in tot.values())
