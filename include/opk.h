@@ -72,6 +72,15 @@ int opk_free(opk_ctx* ctx, void* dev);
 int opk_memset(opk_ctx* ctx, void* dev, int value, size_t bytes);
 int opk_memcpy_h2d(opk_ctx* ctx, void* dev_dst, const void* host_src, size_t bytes);
 int opk_memcpy_d2h(opk_ctx* ctx, void* host_dst, const void* dev_src, size_t bytes); /* syncs */
+/* element type conversion on the device, on the context stream: OPK_F32 <-> OPK_F64 (double -> float
+ * rounds to nearest).  The plugin functions' double instantiations (resizeAndMergeBase.cu:575-581,
+ * nmsBase.cu:353-358, bodyPartConnectorBase.cu:252-266, which compute in double) run the float
+ * kernels between two conversions here (integration/openpose_hip_shim.cpp): the results are the
+ * float instantiation's, widened. */
+#define OPK_F32 0
+#define OPK_F64 1
+int opk_convert(opk_ctx* ctx, void* dst_dev, int dst_type, const void* src_dev, int src_type,
+                size_t count);
 
 /* ---- resizeAndMerge: replaces op::resizeAndMergeGpu<float>
  *      (include/openpose/net/resizeAndMergeBase.hpp:17-20) with resizeAndMergeCpu numerics

@@ -22,7 +22,8 @@
 // resizeAndMergeGpu / nmsGpu compute what the CUDA objects they replace compute (OPK_MAPS_CUDA:
 // Catmull-Rom x8 resize, strict-interior NMS; include/opk.h) unless the shim is built with
 // -DOPK_SHIM_MAPS=OPK_MAPS_CPU, which gives the CPU path's numerics (resizeAndMergeCpu / nmsCpu);
-// everything else follows the CPU path.  Errors come back through op::error, the
+// everything else follows the CPU path.  The double instantiations run the float
+// kernels between device conversions (AsFloat below).  Errors come back through op::error, the
 // reference's convention (errorAndLog.cpp:158-233).  See INTEGRATION.md for the build lines.
 #include <map>
 #include <memory>
@@ -98,12 +99,51 @@ namespace op
                 error(std::string{"libopk_hip: "} + opk_last_error(), line, function, __FILE__);
         }
 
+        // The double instantiations (resizeAndMergeBase.cu:575-581, nmsBase.cu:353-358,
+        // bodyPartConnectorBase.cu:252-266) run the float kernels: a device array of T seen as
+        // float -- the caller's pointer for float, a converted copy for double (opk_convert)
         template <typename T>
-        void requireFloat(const char* what)
+        class AsFloat
         {
-            if (!std::is_same<T, float>::value)
-                error(std::string{what} + ": the MI355X path computes in float only.", __LINE__,
-                      __FUNCTION__, __FILE__);
+        public:
+            AsFloat(const T* src, const size_t count, const bool load) : mCount{count}
+            {
+                if (std::is_same<T, float>::value)
+                {
+                    mPtr = (float*)src;
+                    return;
+                }
+                check(opk_malloc(threadContext(), (void**)&mPtr, count * sizeof(float)), __LINE__,
+                      __FUNCTION__);
+                mOwned = true;
+                if (load)
+                    check(opk_convert(threadContext(), mPtr, OPK_F32, src, OPK_F64, count), __LINE__,
+                          __FUNCTION__);
+            }
+            ~AsFloat()
+            {
+                if (mOwned)
+                    opk_free(threadContext(), mPtr);
+            }
+            AsFloat(const AsFloat&) = delete;
+            AsFloat& operator=(const AsFloat&) = delete;
+            float* get() const { return mPtr; }
+            // the float results back into the caller's T array (double: widened)
+            void store(T* dst) const
+            {
+                if (mOwned)
+                    check(opk_convert(threadContext(), dst, OPK_F64, mPtr, OPK_F32, mCount), __LINE__,
+                          __FUNCTION__);
+            }
+        private:
+            float* mPtr = nullptr;
+            size_t mCount;
+            bool mOwned = false;
+        };
+
+        size_t volume(const std::array<int, 4>& s)
+        {
+            return (size_t)s[0] * s[1] * s[2] * s[3];
         }
     }
 
@@ -114,16 +154,24 @@ namespace op
     {
         try
         {
-            requireFloat<T>("resizeAndMergeGpu");
             std::vector<int> sizes;
             for (const auto& s : sourceSizes)
                 sizes.insert(sizes.end(), s.begin(), s.end());
             std::vector<float> ratios(scaleInputToNetInputs.begin(), scaleInputToNetInputs.end());
-            check(opk_resize_and_merge_semantics(threadContext(), (float*)targetPtr,
-                                                 (const float* const*)sourcePtrs.data(),
-                                                 (int)sourcePtrs.size(), targetSize.data(),
+            std::vector<std::unique_ptr<AsFloat<T>>> sources;
+            std::vector<const float*> sourceFloats;
+            for (auto i = 0u; i < sourcePtrs.size(); i++)
+            {
+                sources.emplace_back(new AsFloat<T>{
+                    sourcePtrs[i], i < sourceSizes.size() ? volume(sourceSizes[i]) : 0, true});
+                sourceFloats.emplace_back(sources.back()->get());
+            }
+            const AsFloat<T> target{targetPtr, volume(targetSize), false};
+            check(opk_resize_and_merge_semantics(threadContext(), target.get(), sourceFloats.data(),
+                                                 (int)sourceFloats.size(), targetSize.data(),
                                                  sizes.data(), ratios.data(), OPK_SHIM_MAPS),
                   __LINE__, __FUNCTION__);
+            target.store(targetPtr);
             check(opk_sync(threadContext()), __LINE__, __FUNCTION__);
         }
         catch (const std::exception& e)
@@ -139,12 +187,13 @@ namespace op
     {
         try
         {
-            requireFloat<T>("nmsGpu");
-            check(opk_nms_semantics(threadContext(), (float*)targetPtr, kernelPtr,
-                                    (const float*)sourcePtr, (float)threshold, targetSize.data(),
-                                    sourceSize.data(), (float)offset.x, (float)offset.y,
-                                    OPK_SHIM_MAPS),
+            const AsFloat<T> source{sourcePtr, volume(sourceSize), true};
+            const AsFloat<T> target{targetPtr, volume(targetSize), false};
+            check(opk_nms_semantics(threadContext(), target.get(), kernelPtr, source.get(),
+                                    (float)threshold, targetSize.data(), sourceSize.data(),
+                                    (float)offset.x, (float)offset.y, OPK_SHIM_MAPS),
                   __LINE__, __FUNCTION__);
+            target.store(targetPtr);
             check(opk_sync(threadContext()), __LINE__, __FUNCTION__);
         }
         catch (const std::exception& e)
@@ -164,12 +213,13 @@ namespace op
     {
         try
         {
-            requireFloat<T>("connectBodyPartsGpu");
             (void)peaksPtr; (void)pairScoresCpu; (void)pairScoresGpuPtr;   // owned by libopk_hip
             (void)bodyPartPairsGpuPtr; (void)mapIdxGpuPtr;
             const auto numberBodyParts = (int)getPoseNumberBodyParts(poseModel);
             const auto channels = numberBodyParts + (addBkgChannel(poseModel) ? 1 : 0)
                                 + (int)getPoseMapIndex(poseModel).size();
+            const AsFloat<T> heat{heatMapGpuPtr, (size_t)channels * heatMapSize.x * heatMapSize.y, true};
+            const AsFloat<T> peaks{peaksGpuPtr, (size_t)numberBodyParts * (maxPeaks + 1) * 3, true};
             // the CPU path's assembly (the parity target) where the reference's CPU connector
             // exists; connectBodyPartsGpu's own global-sort assembly for the other models (BODY_135...)
             const bool cpuModel = numberBodyParts == 25 || numberBodyParts == 18 || numberBodyParts == 15;
@@ -182,7 +232,7 @@ namespace op
                 scores.resize(capacity);
                 check(opk_connect_body_parts_semantics(
                           threadContext(), keypoints.data(), scores.data(), capacity, &people,
-                          (const float*)heatMapGpuPtr, (const float*)peaksGpuPtr, (int)poseModel, channels,
+                          heat.get(), peaks.get(), (int)poseModel, channels,
                           heatMapSize.y, heatMapSize.x, maxPeaks, (float)interMinAboveThreshold,
                           (float)interThreshold, minSubsetCnt, (float)minSubsetScore,
                           (float)defaultNmsThreshold, (float)scaleFactor, maximizePositives ? 1 : 0, semantics),

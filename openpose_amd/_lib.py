@@ -32,6 +32,7 @@ _SIGS = {
     "opk_malloc": (_i, [_p, _c.POINTER(_p), _c.c_size_t]),
     "opk_free": (_i, [_p, _p]),
     "opk_memset": (_i, [_p, _p, _i, _c.c_size_t]),
+    "opk_convert": (_i, [_p, _p, _i, _p, _i, _c.c_size_t]),
     "opk_memcpy_h2d": (_i, [_p, _p, _p, _c.c_size_t]),
     "opk_memcpy_d2h": (_i, [_p, _p, _p, _c.c_size_t]),
     "opk_probe_peaks": (_i, [_p, _c.POINTER(_d), _c.POINTER(_d), _c.POINTER(_d)]),

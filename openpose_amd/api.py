@@ -106,6 +106,14 @@ class Context:
         return self
 
     # ---- operators ---------------------------------------------------------------------------
+    def convert(self, dst, src):
+        """dst <- src element-wise on the device (float32 <-> float64, opk_convert), same count."""
+        kinds = {torch.float32: 0, torch.float64: 1}
+        assert dst.numel() == src.numel() and dst.dtype in kinds and src.dtype in kinds
+        assert dst.is_contiguous() and src.is_contiguous()
+        check(self.L.opk_convert(self.h, _ptr(dst), kinds[dst.dtype], _ptr(src), kinds[src.dtype],
+                                 src.numel()))
+
     def resize_and_merge(self, target, sources, semantics=MAPS_CPU, scale_ratios=None):
         """target [N,C,H,W] fp32 CUDA; sources list of [N,C,h,w] (resizeAndMergeGpu).  semantics
         MAPS_CPU: resizeAndMergeCpu's arithmetic; MAPS_CUDA: the CUDA build's (scale_ratios =

@@ -125,6 +125,27 @@ int opk_free(opk_ctx* ctx, void* p)
     });
 }
 
+int opk_convert(opk_ctx* ctx, void* dst, int dst_type, const void* src, int src_type, size_t count)
+{
+    return guarded([&] {
+        OPK_CHECK_ARG(ctx && (count == 0 || (dst && src)), "NULL argument");
+        OPK_CHECK_ARG((dst_type == OPK_F32 || dst_type == OPK_F64) &&
+                          (src_type == OPK_F32 || src_type == OPK_F64),
+                      "unknown element type");
+        ctx->bind();
+        if (dst_type == src_type) {
+            OPK_HIP(hipMemcpyAsync(dst, src, count * (dst_type == OPK_F64 ? 8 : 4),
+                                   hipMemcpyDeviceToDevice, ctx->stream));
+        } else if (dst_type == OPK_F32) {
+            opk::launch_f64_to_f32(static_cast<float*>(dst), static_cast<const double*>(src), count,
+                                   ctx->stream);
+        } else {
+            opk::launch_f32_to_f64(static_cast<double*>(dst), static_cast<const float*>(src), count,
+                                   ctx->stream);
+        }
+    });
+}
+
 int opk_memset(opk_ctx* ctx, void* p, int v, size_t bytes)
 {
     return guarded([&] {

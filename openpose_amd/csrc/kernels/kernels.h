@@ -143,6 +143,8 @@ void launch_hbm_read(const void* buf, size_t bytes, float* out, int blocks, hipS
 
 // ---- elementwise helpers (misc.hip) -----------------------------------------------------------
 void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stream);
+void launch_f64_to_f32(float* dst, const double* src, size_t n, hipStream_t stream);
+void launch_f32_to_f64(double* dst, const float* src, size_t n, hipStream_t stream);
 // getHeatMapsCopy: dst [frames][nsel][hw] from heat [frames][channels][hw]; sel_dev = nsel source
 // channels then nsel kinds (0 part/background, 1 PAF); scale_mode = op::ScaleMode value
 void launch_heat_copy(float* dst, const float* heat, const int* sel_dev, int nsel, int frames,

@@ -19,6 +19,15 @@ __global__ __launch_bounds__(256) void add_inplace_kernel(float* __restrict__ ds
     for (size_t i = n4 * 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
         dst[i] += src[i];
 }
+// element type conversion for the plugin functions' double instantiations (opk_convert): one
+// rounding per element (double -> float round to nearest even, float -> double exact)
+template <typename D, typename S>
+__global__ __launch_bounds__(256) void convert_kernel(D* __restrict__ dst, const S* __restrict__ src, size_t n)
+{
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        dst[i] = (D)src[i];
+}
 // getHeatMapsCopy's scaling (poseExtractorNet.cpp:106-244); ScaleMode values of
 // include/openpose/core/enumClasses.hpp:6-17
 constexpr int kZeroToOne = 3, kZeroToOneFixed = 4, kPlusMinusOne = 5, kPlusMinusOneFixed = 6,
@@ -78,6 +87,25 @@ void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stre
     const size_t blocks = std::min<size_t>((n / 4 + 255) / 256 + 1, 4096);
     hipLaunchKernelGGL(add_inplace_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, dst, src, n);
     OPK_LAUNCH_CHECK();
+}
+
+template <typename D, typename S>
+static void launch_convert(D* dst, const S* src, size_t n, hipStream_t stream)
+{
+    if (n == 0) return;
+    const size_t blocks = std::min<size_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL((convert_kernel<D, S>), dim3((unsigned)blocks), dim3(256), 0, stream, dst, src, n);
+    OPK_LAUNCH_CHECK();
+}
+
+void launch_f64_to_f32(float* dst, const double* src, size_t n, hipStream_t stream)
+{
+    launch_convert(dst, src, n, stream);
+}
+
+void launch_f32_to_f64(double* dst, const float* src, size_t n, hipStream_t stream)
+{
+    launch_convert(dst, src, n, stream);
 }
 
 }  // namespace opk

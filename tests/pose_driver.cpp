@@ -13,7 +13,8 @@
 //   3. the poseNetOutput injection path (enableNet = false, poseExtractorCaffe.cpp:249-262);
 //   4. makeNetHip in addCaffeNetOnThread's order (poseExtractorCaffe.cpp:82-95): the output blob is
 //      taken before the first forward and read after two forwards of different shapes;
-//   5. resizeAndMergeGpu -> nmsGpu -> connectBodyPartsGpu with the reference signatures;
+//   5. resizeAndMergeGpu -> nmsGpu -> connectBodyPartsGpu with the reference signatures, float and
+//      double instantiations;
 //   6. two worker threads, each with its own PoseExtractorHip (the --num_gpu N Wrapper threads, all
 //      on device 0 here), forwarding concurrently.
 #include <cstdio>
@@ -255,6 +256,39 @@ int main(int argc, char** argv)
                 save("fns_kp.f32", kp.getConstPtr(), kp.getVolume());
                 save("fns_sc.f32", sc.getConstPtr(), sc.getVolume());
             }
+            // 5b: the double instantiations on the same data (float kernels between conversions)
+            const std::vector<double> netOut64(netOut.begin(), netOut.end());
+            void *src64 = nullptr, *heat64 = nullptr, *peaks64 = nullptr;
+            if (opk_malloc(ctx, &src64, netOut64.size() * 8) || opk_malloc(ctx, &heat64, (size_t)78 * H * W * 8) ||
+                opk_malloc(ctx, &peaks64, (size_t)25 * 128 * 3 * 8) ||
+                opk_memcpy_h2d(ctx, src64, netOut64.data(), netOut64.size() * 8))
+                throw std::runtime_error(opk_last_error());
+            op::resizeAndMergeGpu((double*)heat64, std::vector<const double*>{(const double*)src64},
+                                  std::array<int, 4>{1, 78, H, W}, {std::array<int, 4>{1, 78, oh, ow}},
+                                  std::vector<double>{1.});
+            std::vector<double> heatHost64((size_t)78 * H * W);
+            opk_memcpy_d2h(ctx, heatHost64.data(), heat64, heatHost64.size() * 8);
+            save("fns64_heat.f64", heatHost64.data(), heatHost64.size());
+            op::nmsGpu((double*)peaks64, (int*)kern, (const double*)heat64, 0.05, std::array<int, 4>{1, 25, 128, 3},
+                       std::array<int, 4>{1, 78, H, W}, op::Point<double>{(double)off, (double)off});
+            std::vector<double> peaksHost64((size_t)25 * 128 * 3);
+            opk_memcpy_d2h(ctx, peaksHost64.data(), peaks64, peaksHost64.size() * 8);
+            save("fns64_peaks.f64", peaksHost64.data(), peaksHost64.size());
+            op::Array<double> kp64, sc64;
+            op::connectBodyPartsGpu<double>(kp64, sc64, (const double*)heat64, peaksHost64.data(),
+                                     op::PoseModel::BODY_25, op::Point<int>{W, H}, 127, 0.95, 0.05, 3, 0.4,
+                                     0.05, (double)load<float>("fns_scale.f32")[0], false, op::Array<double>{},
+                                     nullptr, nullptr, nullptr, (const double*)peaks64);
+            const double people64 = kp64.empty() ? 0. : (double)kp64.getSize(0);
+            save("fns64_meta.f64", &people64, 1);
+            if (!kp64.empty())
+            {
+                save("fns64_kp.f64", kp64.getConstPtr(), kp64.getVolume());
+                save("fns64_sc.f64", sc64.getConstPtr(), sc64.getVolume());
+            }
+            opk_free(ctx, src64);
+            opk_free(ctx, heat64);
+            opk_free(ctx, peaks64);
             opk_free(ctx, src);
             opk_free(ctx, heat);
             opk_free(ctx, peaks);

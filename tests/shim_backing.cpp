@@ -43,6 +43,7 @@ namespace op
     template <typename T> Point<T>& Point<T>::operator=(Point<T>&& p) { x = p.x; y = p.y; return *this; }
     template struct Point<int>;
     template struct Point<float>;
+    template struct Point<double>;
 
     // ---- Array: a shared buffer; copies share it (array.hpp "fast copy") ------------------------
     template <typename T> void Array<T>::resetAuxiliary(const std::vector<int>& sizes, T* const dataPtr)

@@ -8,7 +8,7 @@ by tests/shim_backing.cpp), against the C-ABI pipeline (openpose_amd.api) on the
 * makeNetHip in addCaffeNetOnThread's order (output blob taken before the first forward, read
   after forwards of two shapes);
 * resizeAndMergeGpu -> nmsGpu -> connectBodyPartsGpu with the reference signatures (the CUDA
-  build's map semantics, the shim's default);
+  build's map semantics, the shim's default), float and double instantiations;
 * two worker threads with one extractor each, forwarding concurrently: same keypoints as one.
 
 The driver is built here where /root/reference is present (__graft_entry__.build() does it too) and
@@ -182,6 +182,16 @@ def test_pose_shim_matches_abi(ctx):
         assert n == len(kp) and n >= 1
         np.testing.assert_array_equal(_read(d, "fns_kp.f32").reshape(n, 25, 3), kp)
         np.testing.assert_array_equal(_read(d, "fns_sc.f32"), sc)
+        # 5b. the double instantiations (the reference instantiates all three for double): the float
+        # kernels between device conversions, so exactly the float results, widened
+        np.testing.assert_array_equal(_read(d, "fns64_heat.f64", np.float64).reshape(78, H, W),
+                                      heat.cpu().numpy()[0].astype(np.float64))
+        np.testing.assert_array_equal(_read(d, "fns64_peaks.f64", np.float64).reshape(25, 128, 3),
+                                      peaks.cpu().numpy()[0].astype(np.float64))
+        assert int(_read(d, "fns64_meta.f64", np.float64)[0]) == n
+        np.testing.assert_array_equal(_read(d, "fns64_kp.f64", np.float64).reshape(n, 25, 3),
+                                      kp.astype(np.float64))
+        np.testing.assert_array_equal(_read(d, "fns64_sc.f64", np.float64), sc.astype(np.float64))
 
         # 6. two concurrent Wrapper threads: every repetition equals the single-thread result
         gk, gs, _ = _result(d, "single")
