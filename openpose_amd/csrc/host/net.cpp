@@ -550,6 +550,21 @@ void NetHip::forward(const float* input, int n, int h, int w)
     forward_on(input, n, h, w, ctx_->stream, true);
 }
 
+float* NetHip::select_output(int n, int h, int w, bool alternate)
+{
+    OPK_CHECK_ARG(n > 0 && h > 0 && w > 0, "empty input");
+    ctx_->bind();
+    ShapePlan& S = *shape_plan(n, h, w, ctx_->stream);
+    if (alternate) {
+        if (!S.out32_alt) {
+            const size_t bytes = (size_t)n * out_c_ * S.lh[out_level_] * S.lw[out_level_] * 4;
+            S.out32_alt = static_cast<float*>(S.out_mem_alt.get(bytes));
+        }
+        S.alt = !S.alt;
+    }
+    return S.out();
+}
+
 void NetHip::prepare(int n, int h, int w)
 {
     OPK_CHECK_ARG(n > 0 && h > 0 && w > 0, "empty input");
@@ -589,7 +604,7 @@ void NetHip::blob(const std::string& name, int f0, int nf, float* host, int shap
         OPK_CHECK_ARG(L.level == out_level_, name + ": not at the output resolution");
         for (int f = 0; f < nf; ++f)
             OPK_HIP(hipMemcpy(host + (size_t)f * L.ch * hw,
-                              S.out32 + ((size_t)(f0 + f) * out_c_ + L.coff) * hw,
+                              S.out() + ((size_t)(f0 + f) * out_c_ + L.coff) * hw,
                               (size_t)L.ch * hw * 4, hipMemcpyDeviceToHost));
         return;
     }
@@ -626,6 +641,7 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
 void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w, hipStream_t st)
 {
     LaunchLog* log = launch_log();
+    float* const out32 = S.out();   // this forward's output buffer (select_output)
     const std::vector<uint16_t*>& ptr = S.base;
     const std::vector<int>& lh_ = S.lh;
     const std::vector<int>& lw_ = S.lw;
@@ -689,7 +705,7 @@ void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w
                     h.dst_cs[d] = b.dst_cs[d];
                     h.dst_coff[d] = b.dst_coff[d];
                 }
-                h.out32 = b.out32;
+                h.out32 = b.out32 ? out32 : nullptr;
                 h.out32_c = b.out32_c;
                 h.out32_coff = b.out32_coff;
                 // persistent grid (HEAD_PERSIST=0: one workgroup per tile, dev A/B)
@@ -701,10 +717,13 @@ void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w
             }
             if (log) log->layer = c.info.name + (a.pool ? "+pool" : "");
             if (c.from_image) {
-                launch_conv_image(a, input, st);
+                ConvArgs ai = a;
+                if (ai.out32) ai.out32 = out32;
+                launch_conv_image(ai, input, st);
             } else {
                 ConvArgs a3 = a;
                 a3.actmax = a.actmax && c.slope01;
+                if (a3.out32) a3.out32 = out32;
                 launch_conv3(a3, st);
             }
         } else {

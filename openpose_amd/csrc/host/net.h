@@ -39,8 +39,13 @@ public:
     void time_begin(hipStream_t s) { timer_.begin(s); }
     void time_end(hipStream_t s) { timer_.end(s); }
     // net output of the last forward ([n][out_channels][out_h][out_w] fp32, stays valid until
-    // set_conv or until more than kMaxShapes other shapes have been planned)
-    float* output() const { return cur_ ? cur_->out32 : nullptr; }
+    // set_conv or until more than kMaxShapes other shapes have been planned; a shape forwarded by
+    // the pose pipeline alternates between two output buffers, select_output)
+    float* output() const { return cur_ ? cur_->out() : nullptr; }
+    // plans the shape and returns the output buffer its next forward writes; alternate: switch to
+    // the shape's other buffer first (PoseHip: batch i+1's nets need not wait for the
+    // post-processing of batch i, which reads the first)
+    float* select_output(int n, int h, int w, bool alternate);
     int out_channels() const { return out_c_; }
     int out_h() const { return cur_ ? cur_->lh[out_level_] : 0; }
     int out_w() const { return cur_ ? cur_->lw[out_level_] : 0; }
@@ -92,8 +97,11 @@ private:
         std::vector<int> lh, lw;
         std::vector<std::unique_ptr<DevBuf>> mem;
         std::vector<uint16_t*> base;   // first position of each buffer (past its head guard)
-        DevBuf out_mem;
+        DevBuf out_mem, out_mem_alt;
         float* out32 = nullptr;
+        float* out32_alt = nullptr;    // the second output buffer (select_output)
+        bool alt = false;              // forwards write out32_alt
+        float* out() const { return alt ? out32_alt : out32; }
         bool fused1 = false;           // conv1_fused_kernel runs for this shape
         bool fusedh = false;           // conv_head_kernel runs the fused head pairs
         std::vector<char> poolfused;   // per pool: run inside its conv's epilogue (conv3w8 POOL)

@@ -63,7 +63,7 @@ PoseHip::~PoseHip()
         (void)hipStreamSynchronize(post_);
         (void)hipStreamDestroy(post_);
         (void)hipEventDestroy(nets_done_);
-        (void)hipEventDestroy(post_done_);
+        for (auto& e : post_done_) (void)hipEventDestroy(e);
     }
     for (auto& s : slots_)
         if (s.done) (void)hipEventDestroy(s.done);
@@ -207,7 +207,7 @@ void PoseHip::submit(const float* frames, int n, int net_h, int net_w, int prod_
     OPK_CHECK_ARG(net_ != nullptr, "no network: use forward_net_output (poseNetOutput path)");
     OPK_CHECK_ARG(count_ < 2, "two batches already in flight: collect first");
     ctx_->bind();
-    wait_post(ctx_->stream);   // the net overwrites the output the last post-processing reads
+    next_output(n, net_h, net_w, true);   // (waits for the posts reading that buffer)
     net_->forward(frames, n, net_h, net_w);
     const NetOutput o{net_->output(), net_->out_h(), net_->out_w()};
     submit_outputs(&o, 1, n, net_h, net_w, prod_w, prod_h, true);
@@ -222,7 +222,7 @@ hipStream_t PoseHip::post_stream(bool own_net)
     if (!post_) {
         OPK_HIP(hipStreamCreateWithFlags(&post_, hipStreamNonBlocking));
         OPK_HIP(hipEventCreateWithFlags(&nets_done_, hipEventDisableTiming));
-        OPK_HIP(hipEventCreateWithFlags(&post_done_, hipEventDisableTiming));
+        for (auto& e : post_done_) OPK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     }
     // everything on the context stream so far: the caller's work and this batch's nets
     OPK_HIP(hipEventRecord(nets_done_, ctx_->stream));
@@ -232,7 +232,23 @@ hipStream_t PoseHip::post_stream(bool own_net)
 
 void PoseHip::wait_post(hipStream_t s)
 {
-    if (post_recorded_) OPK_HIP(hipStreamWaitEvent(s, post_done_, 0));
+    if (post_count_ > 0) OPK_HIP(hipStreamWaitEvent(s, post_done_[(post_count_ - 1) & 1], 0));
+}
+
+void PoseHip::wait_readers(hipStream_t s, const float* out)
+{
+    for (int back = 1; back <= 2 && back <= post_count_; ++back) {
+        const int k = (post_count_ - back) & 1;
+        bool reads = false;
+        for (int i = 0; i < post_nreads_[k]; ++i) reads = reads || post_reads_[k][i] == out;
+        if (reads) OPK_HIP(hipStreamWaitEvent(s, post_done_[k], 0));
+    }
+}
+
+void PoseHip::next_output(int n, int h, int w, bool alternate)
+{
+    const bool alt = alternate && post_ != nullptr && dev_switch("NET_OUT_ALT", 1) != 0;
+    wait_readers(ctx_->stream, net_->select_output(n, h, w, alt));
 }
 
 void PoseHip::set_input(int net_w, int net_h, float dyn, int scale_number, double scale_gap)
@@ -313,7 +329,6 @@ void PoseHip::submit_multi(const float* const* frames, const int* net_hw, int ns
     std::vector<NetOutput> outs(nscales);
     for (int i = 0; i < nscales; ++i) OPK_CHECK_ARG(frames[i] != nullptr, "NULL scale input");
     ctx_->bind();
-    wait_post(ctx_->stream);   // the nets overwrite the outputs the last post-processing reads
     // the scales' nets are independent until the merge: scales 1.. run on streams of their own
     // beside scale 0 (small nets leave most CUs idle on their own), each shape with its own plan
     // and buffers; the context stream waits for all of them before the merge.  Shapes that repeat
@@ -322,6 +337,9 @@ void PoseHip::submit_multi(const float* const* frames, const int* net_hw, int ns
     for (int i = 0; i < nscales && distinct; ++i)
         for (int j = 0; j < i; ++j)
             distinct = distinct && !(net_hw[2 * i] == net_hw[2 * j] && net_hw[2 * i + 1] == net_hw[2 * j + 1]);
+    // each output buffer the nets write: after the post-processings that read it (a repeated
+    // shape shares one plan and buffer, and keeps it)
+    for (int i = 0; i < nscales; ++i) next_output(n, net_hw[2 * i], net_hw[2 * i + 1], nscales == 1 || distinct);
     if (nscales == 1 || !distinct) {
         for (int i = 0; i < nscales; ++i) {
             net_->forward(frames[i], n, net_hw[2 * i], net_hw[2 * i + 1]);
@@ -452,8 +470,11 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
     timer_.end(s);
     OPK_HIP(hipEventRecord(sl.done, s));
     if (post_ && s == post_) {   // (the context stream may be the null stream)
-        OPK_HIP(hipEventRecord(post_done_, post_));
-        post_recorded_ = true;
+        const int k = post_count_ & 1;
+        OPK_HIP(hipEventRecord(post_done_[k], post_));
+        post_nreads_[k] = nscales;
+        for (int i = 0; i < nscales; ++i) post_reads_[k][i] = outs[i].ptr;
+        ++post_count_;
     }
     sl.n = n;
     sl.H = H;

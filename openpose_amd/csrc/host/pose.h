@@ -126,15 +126,23 @@ private:
     // post-processing of a batch (overlay, NMS, PAF integrals) runs on post_, ordered after the
     // batch's nets on the context stream.  Everything the caller enqueues on the context stream
     // -- frame uploads included -- stays ordered before the next batch's warp and nets, and the
-    // next batch's warp overlaps this batch's post-processing; the next nets (which overwrite
-    // the net output post_ reads) wait for post_done_.  POST_STREAM=0: all on the context stream.
+    // next batch's warp overlaps this batch's post-processing.  The nets alternate between two
+    // output buffers per input shape (NetHip::select_output; NET_OUT_ALT=0: one), and before a
+    // forward the context stream waits for those of the last two recorded post-processings that
+    // read the buffer it is about to write (wait_readers) -- so batch i+1's nets start while batch
+    // i's post-processing still runs.  POST_STREAM=0: all on the context stream.
     // The injection path (submit_net_output: a caller-owned net output) stays on the context
     // stream, so a caller may rewrite that buffer on its stream after submit.
     hipStream_t post_ = nullptr;
-    hipEvent_t nets_done_ = nullptr, post_done_ = nullptr;
-    bool post_recorded_ = false;
+    hipEvent_t nets_done_ = nullptr, post_done_[2] = {};
+    int post_count_ = 0;                     // post-processings recorded on post_
+    const float* post_reads_[2][kMaxResizeSources] = {};   // net outputs they read, by parity
+    int post_nreads_[2] = {};
     hipStream_t post_stream(bool own_net);   // the stream a batch's post-processing runs on
     void wait_post(hipStream_t s);           // s after the last recorded post-processing
+    void wait_readers(hipStream_t s, const float* out);   // s after recorded posts reading out
+    // the output buffer the next forward of this shape writes, after the waits it needs
+    void next_output(int n, int h, int w, bool alternate);
     DevBuf cand_;                            // NMS candidate counters (zeroed once, self-resetting)
     // multi-scale: the nets of scales 1.. run on their own streams beside scale 0's
     hipStream_t scale_streams_[kMaxResizeSources - 1] = {};

@@ -54,3 +54,26 @@ def test_sharded_bench_two_ranks(config, tmp_path):
     np.testing.assert_array_equal(a["keypoints"], b["keypoints"])
     np.testing.assert_array_equal(a["scores"], b["scores"])
     assert a["counts"].sum() >= batch   # people were found
+
+
+@pytest.mark.gpu
+def test_alternating_net_outputs_same_records(tmp_path):
+    """Batch i+1's nets write the other of two net-output buffers while batch i's post-processing
+    still reads the first (PoseHip::next_output, NET_OUT_ALT): every frame's records equal those of
+    the single-buffer pipeline, whose nets wait for the previous post-processing.  The frame
+    contents change every step, so a net overwriting an output before its reader ran would show."""
+    def run(alt, dump):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+        r = subprocess.run([sys.executable, "bench.py", "--steps", "6", "--warmup", "1", "--batch", "32",
+                            "--no-cpu-baseline", "--dev", "NET_OUT_ALT=%d" % alt, "--dump-records", dump],
+                           cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+    d0, d1 = str(tmp_path / "alt0.npz"), str(tmp_path / "alt1.npz")
+    run(0, d0)
+    run(1, d1)
+    a, b = np.load(d0), np.load(d1)
+    assert len(a["counts"]) == 6 * 32
+    np.testing.assert_array_equal(a["counts"], b["counts"])
+    np.testing.assert_array_equal(a["keypoints"], b["keypoints"])
+    np.testing.assert_array_equal(a["scores"], b["scores"])
+    assert a["counts"].sum() >= 32
