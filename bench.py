@@ -69,6 +69,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=15.0, help="target CPU-baseline sample")
     ap.add_argument("--dump-records", default=None, metavar="NPZ",
                     help="rank 0: write the gathered per-frame records of the timed steps (tests)")
+    ap.add_argument("--collective-gather", action="store_true",
+                    help="test: at --gpus 1, create the RCCL process group anyway and move the "
+                         "records through the collective gather an N-GPU run uses")
     ap.add_argument("--dev", action="append", default=[], metavar="KEY=VAL",
                     help="kernel-variant switch for A/B runs (opk_dev_set; include/opk.h)")
     return ap.parse_args()
@@ -203,13 +206,106 @@ def cpu_baseline(args, params, frames_np, overlays_np):
                                        "speed.md:21), other hardware"}
 
 
-def host_breakdown(host, steps):
+PARITY_FRAMES = 3
+
+
+def gpu_parity_run(net, pose, convs, frames_u8):
+    """GPU half of the parity block (outside every timed region, after the bench): the bench's
+    first PARITY_FRAMES frames at the bench geometry through the pipeline with FULL-strength heads
+    (out_scale 1: the random net drives the maps, no overlay), so fp16-vs-fp32 CNN differences are
+    what the post-processing sees.  Returns what the CPU leg compares against."""
+    from openpose_amd import synth
+    params = synth.he_weights(convs, seed=0, out_scale=1.0)
+    net.set_params(params)
+    pose.set_overlay(None)
+    pose.forward_frames(frames_u8[:PARITY_FRAMES])
+    return {"params": params, "net_input": pose.net_input_numpy(), "net_output": net.output_numpy(),
+            "peaks": pose.peaks_numpy(), "keypoints": [pose.keypoints(f)[0] for f in range(PARITY_FRAMES)],
+            "scale": pose.scale_net_to_output()}
+
+
+def cpu_parity(g, threads):
+    """CPU half (the cpu_baseline leg: the fp32 reference path on the same frames, oracle/ +
+    oracle/parity.py as the checker): net rel-L2, NMS peak indices identical / within 1 px, the
+    largest refined-peak and keypoint shifts, people counts.  North star: keypoints within 1e-3
+    of the CPU reference with peak indices bit-exact; this measures it on a CNN-driven field."""
+    import oracle
+    from oracle import body25, parity
+    graph = body25.layers()
+    s = g["scale"]
+    off = float(np.float32(0.5 / np.float64(s)))
+    t0 = time.perf_counter()
+    out = {"frames": PARITY_FRAMES, "workload": "BODY_25 656x368 net input from 1280x720 uint8 "
+           "frames, He-init weights with full-strength heads (out_scale 1), no overlay",
+           "per_frame": []}
+    tot_peaks = tot_same = tot_near = 0
+    worst_peak = worst_kp = 0.0
+    num = den = 0.0
+    for f in range(PARITY_FRAMES):
+        ref = body25.forward(g["net_input"][f:f + 1], g["params"], graph=graph, nthreads=threads)[0]
+        got = g["net_output"][f]
+        num += float(np.sum((got.astype(np.float64) - ref) ** 2))
+        den += float(np.sum(ref.astype(np.float64) ** 2))
+        heat_r = oracle.resize_merge([ref], NET_H, NET_W)
+        heat_g = oracle.resize_merge([got], NET_H, NET_W)   # = the GPU's lazy maps (bit-exact)
+        total, same, near = parity.compare_peaks(parity.peak_mask(heat_r, 0.05, PARTS),
+                                                 parity.peak_mask(heat_g, 0.05, PARTS))
+        peaks_r = oracle.nms(heat_r, 0.05, 128, (off, off))
+        rk, _ = oracle.connect(heat_r, peaks_r, scale=s)
+        shift = parity.refined_shift(peaks_r, g["peaks"][f])
+        kshift, matched = parity.keypoint_shift(rk, g["keypoints"][f])
+        tot_peaks += total
+        tot_same += same * total
+        tot_near += near * total
+        worst_peak = max(worst_peak, shift)
+        worst_kp = max(worst_kp, kshift)
+        out["per_frame"].append({
+            "net_rel_l2": round(float(np.linalg.norm(got - ref) / np.linalg.norm(ref)), 6),
+            "fp32_peaks": total, "peak_index_identical": round(same, 5),
+            "peaks_within_1px": round(near, 5), "people_gpu": len(g["keypoints"][f]),
+            "people_fp32": len(rk), "people_matched": matched,
+            "max_keypoint_shift_px": round(kshift, 4)})
+    out.update({
+        "net_rel_l2": round((num / den) ** 0.5, 6),
+        "fp32_peaks": tot_peaks,
+        "peak_index_identical": round(tot_same / max(tot_peaks, 1), 5),
+        "peaks_within_1px": round(tot_near / max(tot_peaks, 1), 5),
+        "max_refined_peak_shift_heatmap_px": round(worst_peak, 4),
+        "max_keypoint_shift_px": round(worst_kp, 4),
+        "people_delta": sum(p["people_gpu"] - p["people_fp32"] for p in out["per_frame"]),
+        "cpu_seconds": round(time.perf_counter() - t0, 1),
+        "note": "integer peak sets by nmsCpu's test on each side's own x8 maps; shifts over peaks "
+                "(people) matched within 1 px (greedily); keypoints in frame pixels"})
+    return out
+
+
+def host_breakdown(host, steps, collect_times=None):
     """Rank 0's host time in the timed region: per step, the submit call (enqueue), collect (wait
     for the batch + people assembly) and records (pack + gather push); finish (the ordered gather's
-    unpack on rank 0) once for the whole run."""
+    unpack on rank 0) once for the whole run.  collect_times (PoseExtractor.read_collect_times):
+    collect split into the wait for the batch's device results and the people assembly, and the
+    assembly threads / CPUs this rank had."""
     out = {k: round(v / steps * 1e3, 3) for k, v in host.items() if k != "finish"}
     out["finish_total"] = round(host.get("finish", 0.0) * 1e3, 3)
+    if collect_times:
+        n = max(collect_times["collects"], 1)
+        out["collect_device_wait"] = round(collect_times["wait_ms"] / n, 3)
+        out["collect_assembly"] = round(collect_times["assembly_ms"] / n, 3)
+        out["assembly_workers"] = collect_times["workers"]
+        out["cpus"] = parallel.cpu_ranges(os.sched_getaffinity(0))
     return out
+
+
+def rank_host_info(dist, host_ms):
+    """Every rank's assembly threads and CPU set (rank 0 prints them: disjoint per rank)."""
+    mine = {"assembly_workers": host_ms.get("assembly_workers"), "cpus": host_ms.get("cpus"),
+            "collect_device_wait": host_ms.get("collect_device_wait"),
+            "collect_assembly": host_ms.get("collect_assembly")}
+    if dist is None:
+        return [mine]
+    allr = [None] * dist.get_world_size()
+    dist.all_gather_object(allr, mine)
+    return allr
 
 
 def _first(*rel):
@@ -303,26 +399,32 @@ def post_roofline(batch, post_ms, pmc_path=POST_PMC, ref_bytes_frame=POST_BYTES_
     return out
 
 
-def dist_setup(world, local):
+def dist_setup(world, local, collective=False):
     """Device and process group of this rank: its own GPU and RCCL.  OPK_BENCH_REHEARSE=1 (dev, a
     1-GPU box): every rank on GPU 0 with gloo, to run the N-rank launcher, the ordered gather in
     the timed loop and the max-over-ranks timing on real hardware (the ranks share the GPU, so the
-    throughput of such a run means nothing)."""
+    throughput of such a run means nothing).  collective (--collective-gather, tests): an RCCL
+    group of one rank, so a 1-GPU box runs the N-GPU transport (device gather, all-gather)."""
     rehearse = os.environ.get("OPK_BENCH_REHEARSE") == "1"
     dev = 0 if rehearse else local
     torch.cuda.set_device(dev)
     dist = None
-    if world > 1:
+    if world == 1 and collective:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(parallel.free_port()))
+        dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", dev))
+    elif world > 1:
         import torch.distributed as dist
         if rehearse:
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    return dev, dist, "cpu" if rehearse else "cuda"
+    return dev, dist, "cpu" if rehearse and world > 1 else "cuda"
 
 
 def rank_main(args, rank, world, local):
-    local, dist, comm_dev = dist_setup(world, local)
+    local, dist, comm_dev = dist_setup(world, local, args.collective_gather)
 
     from openpose_amd import synth
     from openpose_amd.api import Context, Net, PoseExtractor, dev_switches, scale_and_size
@@ -354,13 +456,17 @@ def rank_main(args, rank, world, local):
     # net-output statistics before any overlay (the overlay is added in place into it)
     pose.forward_frames(frames[first_content])
     out_std = float(net.output_numpy()[:2].std()) if nscales == 1 else None
-    ov_np = np.stack([synth.overlay(args.people, NET_H // 8, NET_W // 8, seed=f) for f in range(B)])
-    overlay = torch.from_numpy(ov_np).cuda()
-    pose.set_overlay(overlay)
+    # the people field of a frame depends on its global frame id, like its pixels: frame id
+    # k * B + f of global batch k (content c = k % CONTENTS) gets overlay seed c * B + f (= the
+    # frame id modulo the contents' period), so every step's post-processing sees new fields
+    ov_np = {c: np.stack([synth.overlay(args.people, NET_H // 8, NET_W // 8, seed=c * B + f)
+                          for f in range(B)]) for c in frames}
+    overlays = {c: torch.from_numpy(v).cuda() for c, v in ov_np.items()}
 
     # per-step ordered gather of the per-frame records (capacity: 4x the synthetic people + 8)
     cap = B * (1 + (4 * args.people + 8) * (PARTS * 3 + 1))
-    gather = parallel.RecordGather(world, rank, cap, args.steps, comm_dev)
+    gather = parallel.RecordGather(world, rank, cap, args.steps, comm_dev,
+                                    collective=dist is not None)
 
     # Two-stage pipeline (opk_pose_submit / opk_pose_collect): the device work of batch i+1 is
     # enqueued before the host assembly of batch i, which then overlaps it.
@@ -381,8 +487,10 @@ def rank_main(args, rank, world, local):
             host["records"] += time.perf_counter() - c1
 
     def step(i, timed):
+        c = (i * world + rank) % CONTENTS
         s0 = time.perf_counter()
-        pose.submit_frames(frames[(i * world + rank) % CONTENTS])
+        pose.set_overlay(overlays[c])   # (read at submit; the buffers are never rewritten)
+        pose.submit_frames(frames[c])
         if timed:
             host["submit"] += time.perf_counter() - s0
         if pose.pending() > 1:
@@ -402,6 +510,7 @@ def rank_main(args, rank, world, local):
     # every forward / every batch's post-processing, on the context stream the kernels run on
     net.set_timing(True)
     pose.set_timing(True)
+    pose.read_collect_times()   # (reset)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -409,6 +518,7 @@ def rank_main(args, rank, world, local):
     for i in range(args.steps):
         step(i, True)
     drain(True)
+    collect_times = pose.read_collect_times()
     f0 = time.perf_counter()
     ordered = gather.finish(PARTS)        # rank 0: every frame's record, in frame order
     host["finish"] = time.perf_counter() - f0
@@ -454,6 +564,8 @@ def rank_main(args, rank, world, local):
     # reaches from registers on random operands is the attainable MFMA roof under this clock
     peaks = ctx.probe_peaks()
 
+    host_ms = host_breakdown(host, args.steps, collect_times)
+    rank_hosts = rank_host_info(dist, host_ms)
     total_frames = world * B * args.steps
     if rank == 0:
         assert len(ordered) == total_frames, (len(ordered), total_frames)
@@ -517,11 +629,16 @@ def rank_main(args, rank, world, local):
         },
         "post_roofline": (dict(post_roofline(B, post_ms), overlapped_event_span_ms=round(post_overlap_ms, 3))
                           if nscales == 1 else None),
-        "host_ms": host_breakdown(host, args.steps),
+        "host_ms": host_ms,
+        "per_rank_host": rank_hosts,
     }
     if rank == 0 and world == 1 and nscales == 1 and not args.no_cpu_baseline:
         frames_np = frames[first_content][:2].cpu().numpy()   # uint8 [2][720][1280][3]
-        result["cpu_baseline"] = cpu_baseline(args, params, frames_np, ov_np[:2])
+        result["cpu_baseline"] = cpu_baseline(args, params, frames_np, ov_np[first_content][:2])
+        # keypoint parity at full strength on the same frames (after every measurement: this
+        # replaces the net's weights)
+        result["parity"] = cpu_parity(gpu_parity_run(net, pose, convs, frames[first_content]),
+                                      args.cpu_threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
@@ -531,7 +648,7 @@ def rank_main(args, rank, world, local):
 def rank_main_body135(args, rank, world, local):
     """BASELINE configs[4]: post-processing stress through the injection path (no CNN: the
     reference has no BODY_135 network); frames/s and the post-processing HBM roofline."""
-    local, dist, comm_dev = dist_setup(world, local)
+    local, dist, comm_dev = dist_setup(world, local, args.collective_gather)
     from openpose_amd import synth
     from openpose_amd.api import Context, PoseExtractor, dev_switches, pose_model_info
     from openpose_amd.pose_tables import BODY_135, CONNECT_GPU
@@ -554,7 +671,8 @@ def rank_main_body135(args, rank, world, local):
     pose = PoseExtractor(ctx, None, pose_model=BODY_135, semantics=CONNECT_GPU)
     parts = t["parts"]
     cap = B * (1 + (4 * people + 8) * (parts * 3 + 1))
-    gather = parallel.RecordGather(world, rank, cap, args.steps, comm_dev)
+    gather = parallel.RecordGather(world, rank, cap, args.steps, comm_dev,
+                                    collective=dist is not None)
     rec_buf = np.empty(cap, np.float32)
     collected = [0]
 
@@ -589,6 +707,7 @@ def rank_main_body135(args, rank, world, local):
     torch.cuda.synchronize()
     found = [pose.num_people(f) for f in range(min(B, 4))]
     pose.set_timing(True)
+    pose.read_collect_times()   # (reset)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -596,6 +715,7 @@ def rank_main_body135(args, rank, world, local):
     for i in range(args.steps):
         step(i, True)
     drain(True)
+    collect_times = pose.read_collect_times()
     f0 = time.perf_counter()
     ordered = gather.finish(parts)
     host["finish"] = time.perf_counter() - f0
@@ -612,6 +732,8 @@ def rank_main_body135(args, rank, world, local):
         tt = torch.tensor([elapsed, post_ms], device=comm_dev, dtype=torch.float64)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed, post_ms = float(tt[0]), float(tt[1])
+    host_ms = host_breakdown(host, args.steps, collect_times)
+    rank_hosts = rank_host_info(dist, host_ms)
     total_frames = world * B * args.steps
     if rank == 0:
         assert len(ordered) == total_frames, (len(ordered), total_frames)
@@ -646,7 +768,8 @@ def rank_main_body135(args, rank, world, local):
             "frames_gathered_in_order": total_frames,
         },
         "roofline": dict(post_roofline(B, post_ms, POST_PMC_B135, post_bytes), traffic=None),
-        "host_ms": host_breakdown(host, args.steps),
+        "host_ms": host_ms,
+        "per_rank_host": rank_hosts,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle   # the CPU baseline leg only
@@ -687,6 +810,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit("bench.py: --gpus %d but WORLD_SIZE=%d" % (args.gpus, world))
+    # several ranks on this node: each keeps to its GPU-local share of the host CPUs (before any
+    # thread or GPU call), so the ranks' people-assembly threads never share cores
+    parallel.pin_rank_cpus(local, int(os.environ.get("LOCAL_WORLD_SIZE", world)))
     if args.config == "body135":
         rank_main_body135(args, rank, world, local)
     else:

@@ -66,6 +66,8 @@ int opk_ctx_create(int device, void* hip_stream /* used as given; NULL = the nul
 int opk_ctx_create_private_stream(int device, opk_ctx** out);
 int opk_ctx_destroy(opk_ctx* ctx);
 int opk_ctx_stream(opk_ctx* ctx, void** hip_stream);
+/* waits for the context stream and for the side streams of the context's objects (a pose
+ * pipeline's post-processing stream) */
 int opk_sync(opk_ctx* ctx);
 int opk_malloc(opk_ctx* ctx, void** dev, size_t bytes);
 int opk_free(opk_ctx* ctx, void* dev);
@@ -281,8 +283,12 @@ int opk_net_read_timing(opk_net* net, int* forwards, double* total_ms);
 /* device pointer + NCHW shape of the last forward's net_output blob.  Valid right after
  * opk_net_create, as NetCaffe::getOutputBlobArray is (poseExtractorCaffe.cpp:94-95 takes it once,
  * before any forward, and keeps it): before the first forward *output_dev is NULL and shape is
- * {0, out_channels, 0, 0}.  The buffer of one input shape is stable across forwards of that
- * shape (the values are the latest forward's). */
+ * {0, out_channels, 0, 0}.  The buffer of one input shape is stable across direct forwards of
+ * that shape (the values are the latest forward's).  A net driven by an opk_pose pipeline
+ * alternates between two output buffers per input shape (batch i+1's nets write the one batch i's
+ * post-processing does not read), so re-query the pointer after each forward.  A forward that
+ * writes a buffer a pipeline's post-processing still reads -- including a direct opk_net_forward
+ * between opk_pose_submit and opk_pose_collect -- waits for that post-processing first. */
 int opk_net_output(opk_net* net, float** output_dev, int shape[4]);
 /* Inspection (caffe::Net::blob_by_name, which NetCaffe does not expose; used by the per-layer
  * parity tests): frames [frame0, frame0 + nframes) of the named top of the last forward -- a
@@ -343,7 +349,13 @@ int opk_pose_forward_net_output(opk_pose* pose, const float* net_output_dev, int
  * for the OLDEST submitted batch, assembles its people on the host and makes it the batch the
  * result accessors below refer to.  At most two batches in flight: submit(i+1) then collect(i)
  * overlaps the host assembly of batch i with the device work of batch i+1.  opk_pose_forward* =
- * submit + collect.  *frames (may be NULL) receives the collected batch's frame count. */
+ * submit + collect.  *frames (may be NULL) receives the collected batch's frame count.
+ * Streams: the frames / net inputs / injected net output are read after the work queued on the
+ * context stream before the submit.  When the pipeline runs its own net, a batch's
+ * post-processing (overlay add, NMS, PAF scores) runs on a side stream after the batch's nets, so
+ * work queued on the context stream after the submit is NOT ordered before it: keep the overlay
+ * unchanged until collect (or opk_sync); forwards of the same net are ordered after it by the
+ * net (opk_net_output).  The injection path stays on the context stream. */
 int opk_pose_submit(opk_pose* pose, const float* frames_dev, int n, int net_h, int net_w,
                     int producer_w, int producer_h);
 int opk_pose_submit_net_output(opk_pose* pose, const float* net_output_dev, int n, int out_h,
@@ -374,7 +386,9 @@ int opk_pose_net_input(opk_pose* pose, int scale, const float** input_dev, int* 
                        int* net_h);
 int opk_pose_pending(opk_pose* pose);   /* batches in flight, -1 for NULL */
 /* optional additive overlay on the net output before resize (synthetic-people workloads):
- * [n][78][out_h][out_w] device fp32, NULL to disable */
+ * [n][78][out_h][out_w] device fp32, NULL to disable.  With a pipeline that runs its own net the
+ * overlay is read by the post-processing stream after the batch's nets: rewrite it only after the
+ * batch is collected (or after opk_sync). */
 int opk_pose_set_overlay(opk_pose* pose, const float* overlay_dev);
 int opk_pose_num_people(opk_pose* pose, int frame);
 /* keypoints_host [max_people][parts][3], scores_host [max_people] of one collected frame */
@@ -382,10 +396,19 @@ int opk_pose_keypoints(opk_pose* pose, int frame, float* keypoints_host, float* 
                        int max_people);
 /* Post-processing timing (measurement hook, no reference counterpart): while enabled the device
  * work of every submitted batch after its net forward (overlay add, NMS, PAF integrals) is
- * bracketed by HIP events on the context stream; read waits for them and returns the number of
- * batches since the last read and their summed device time in milliseconds. */
+ * bracketed by HIP events on the stream it runs on -- the pipeline's post-processing stream when
+ * it runs its own net (batch i's post-processing then shares the GPU with batch i+1's nets, so
+ * the span includes that time-sharing), the context stream on the injection path; read waits for
+ * them and returns the number of batches since the last read and their summed device time in
+ * milliseconds. */
 int opk_pose_set_timing(opk_pose* pose, int enable);
 int opk_pose_read_timing(opk_pose* pose, int* batches, double* total_ms);
+/* Host-side collect timing (measurement hook, no reference counterpart): for the collects since
+ * the last read, their number and the summed milliseconds spent waiting for the batches' device
+ * results and assembling their people; *workers = the assembly threads (at most 16 and at most
+ * the CPUs of the process's affinity mask).  Any pointer may be NULL. */
+int opk_pose_read_collect_times(opk_pose* pose, int* collects, double* wait_ms, double* assembly_ms,
+                                int* workers);
 /* Every frame of the last collected batch as one packed host record (the result the reference's
  * WQueueOrderer re-sequences, wQueueOrderer.hpp:62-141): for each frame f in order,
  *   [people_f, keypoints_f (people_f x parts x 3), scores_f (people_f)]  (all float).

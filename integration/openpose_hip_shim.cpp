@@ -99,9 +99,59 @@ namespace op
                 error(std::string{"libopk_hip: "} + opk_last_error(), line, function, __FILE__);
         }
 
+        // Conversion buffers of the double instantiations, kept per thread and reused in stream
+        // order on the thread's context (an opk_malloc / opk_free per call would synchronise the
+        // device at every hipFree).  The pool holds its context, so it is freed safely at thread
+        // exit; a thread whose context moved to another device starts a new pool.
+        struct ConvPool
+        {
+            OpkContext ctx;
+            std::vector<std::pair<float*, size_t>> free;
+            void flush()
+            {
+                for (const auto& b : free)
+                    opk_free(ctx.get(), b.first);
+                free.clear();
+            }
+            ~ConvPool() { flush(); }
+        };
+        thread_local ConvPool tConvPool;
+
+        float* convAcquire(const size_t count, size_t& capacity)
+        {
+            auto& pool = tConvPool;
+            const auto ctx = opkShimThreadContext();
+            if (pool.ctx != ctx)
+            {
+                pool.flush();
+                pool.ctx = ctx;
+            }
+            for (size_t i = 0; i < pool.free.size(); ++i)
+                if (pool.free[i].second >= count)
+                {
+                    float* const b = pool.free[i].first;
+                    capacity = pool.free[i].second;
+                    pool.free.erase(pool.free.begin() + (long)i);
+                    return b;
+                }
+            float* b = nullptr;
+            check(opk_malloc(ctx.get(), (void**)&b, count * sizeof(float)), __LINE__, __FUNCTION__);
+            capacity = count;
+            return b;
+        }
+
+        void convRelease(float* b, const size_t capacity)
+        {
+            if (tConvPool.ctx.get() == threadContext())
+                tConvPool.free.emplace_back(b, capacity);
+            else
+                opk_free(threadContext(), b);
+        }
+
         // The double instantiations (resizeAndMergeBase.cu:575-581, nmsBase.cu:353-358,
         // bodyPartConnectorBase.cu:252-266) run the float kernels: a device array of T seen as
-        // float -- the caller's pointer for float, a converted copy for double (opk_convert)
+        // float -- the caller's pointer for float, a converted copy for double (opk_convert), so
+        // a double caller gets the float kernels' results widened (float precision)
         template <typename T>
         class AsFloat
         {
@@ -113,8 +163,7 @@ namespace op
                     mPtr = (float*)src;
                     return;
                 }
-                check(opk_malloc(threadContext(), (void**)&mPtr, count * sizeof(float)), __LINE__,
-                      __FUNCTION__);
+                mPtr = convAcquire(count, mCapacity);
                 mOwned = true;
                 if (load)
                     check(opk_convert(threadContext(), mPtr, OPK_F32, src, OPK_F64, count), __LINE__,
@@ -123,7 +172,7 @@ namespace op
             ~AsFloat()
             {
                 if (mOwned)
-                    opk_free(threadContext(), mPtr);
+                    convRelease(mPtr, mCapacity);
             }
             AsFloat(const AsFloat&) = delete;
             AsFloat& operator=(const AsFloat&) = delete;
@@ -137,7 +186,7 @@ namespace op
             }
         private:
             float* mPtr = nullptr;
-            size_t mCount;
+            size_t mCount, mCapacity = 0;
             bool mOwned = false;
         };
 

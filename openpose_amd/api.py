@@ -638,6 +638,14 @@ class PoseExtractor:
         check(self.L.opk_pose_read_timing(self.h, ctypes.byref(n), ctypes.byref(ms)))
         return n.value, ms.value
 
+    def read_collect_times(self):
+        """{collects, wait_ms, assembly_ms, workers} of the collects since the last read (host
+        time waiting for the device results vs assembling people; opk_pose_read_collect_times)."""
+        n, w, a, k = ctypes.c_int(0), ctypes.c_double(0), ctypes.c_double(0), ctypes.c_int(0)
+        check(self.L.opk_pose_read_collect_times(self.h, ctypes.byref(n), ctypes.byref(w),
+                                                 ctypes.byref(a), ctypes.byref(k)))
+        return {"collects": n.value, "wait_ms": w.value, "assembly_ms": a.value, "workers": k.value}
+
     def records(self, out=None):
         """Packed results of every frame of the last collected batch (opk_pose_records):
         per frame [people, keypoints (people x parts x 3), scores (people)], float32.  With `out`

@@ -104,6 +104,7 @@ int opk_sync(opk_ctx* ctx)
         OPK_CHECK_ARG(ctx, "NULL ctx");
         ctx->bind();
         OPK_HIP(hipStreamSynchronize(ctx->stream));
+        for (hipStream_t s : ctx->side_streams) OPK_HIP(hipStreamSynchronize(s));
     });
 }
 

@@ -306,6 +306,16 @@ int opk_pose_read_timing(opk_pose* p, int* batches, double* total_ms)
     });
 }
 
+int opk_pose_read_collect_times(opk_pose* p, int* collects, double* wait_ms, double* assembly_ms,
+                                int* workers)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(p, "NULL pose");
+        p->pose->read_collect_times(collects, wait_ms, assembly_ms);
+        if (workers) *workers = p->pose->assembly_workers();
+    });
+}
+
 int opk_pose_records(opk_pose* p, float* rec, size_t capacity, size_t* used)
 {
     return guarded_net([&] {

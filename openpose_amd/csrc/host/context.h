@@ -53,6 +53,19 @@ struct Context {
     int* nms_candidates(int frames, int parts);
     HostBuf host_peaks, host_scores;
 
+    // streams other objects of this context run device work on besides `stream` (PoseHip's
+    // post-processing stream, its multi-scale net streams): opk_sync waits for them too
+    std::vector<hipStream_t> side_streams;
+    void add_side_stream(hipStream_t s) { side_streams.push_back(s); }
+    void remove_side_stream(hipStream_t s)
+    {
+        for (size_t i = 0; i < side_streams.size(); ++i)
+            if (side_streams[i] == s) {
+                side_streams.erase(side_streams.begin() + (long)i);
+                return;
+            }
+    }
+
     // device < 0: host-only context (graph planning / host assembly; no device calls)
     void bind() const
     {

@@ -565,6 +565,26 @@ float* NetHip::select_output(int n, int h, int w, bool alternate)
     return S.out();
 }
 
+void NetHip::note_reader(const float* out, hipEvent_t ev)
+{
+    for (auto& r : readers_)
+        if (r.first == out) {
+            r.second = ev;
+            return;
+        }
+    readers_.emplace_back(out, ev);
+}
+
+void NetHip::forget_reader_events(const hipEvent_t* evs, int n)
+{
+    for (size_t i = readers_.size(); i-- > 0;)
+        for (int k = 0; k < n; ++k)
+            if (readers_[i].second == evs[k]) {
+                readers_.erase(readers_.begin() + (long)i);
+                break;
+            }
+}
+
 void NetHip::prepare(int n, int h, int w)
 {
     OPK_CHECK_ARG(n > 0 && h > 0 && w > 0, "empty input");
@@ -579,6 +599,8 @@ void NetHip::forward_on(const float* input, int n, int h, int w, hipStream_t st,
     ctx_->bind();
     ShapePlan& S = *shape_plan(n, h, w, st);
     cur_ = &S;
+    for (const auto& r : readers_)   // post-processings still reading this output buffer
+        if (r.first == S.out()) OPK_HIP(hipStreamWaitEvent(st, r.second, 0));
     if (timed) timer_.begin(st);
     forward_launches(S, input, n, h, w, st);
     if (timed) timer_.end(st);

@@ -46,6 +46,13 @@ public:
     // the shape's other buffer first (PoseHip: batch i+1's nets need not wait for the
     // post-processing of batch i, which reads the first)
     float* select_output(int n, int h, int w, bool alternate);
+    // Readers of an output buffer outside the forward's stream order (PoseHip's post-processing
+    // stream): ev was recorded after the last such read of out.  Every later forward that writes
+    // out -- through PoseHip or a direct opk_net_forward -- first makes its stream wait for ev, so
+    // the forward never overwrites values a post-processing still reads.  One event per buffer
+    // (the readers run in order on one stream, so the latest covers the earlier ones).
+    void note_reader(const float* out, hipEvent_t ev);
+    void forget_reader_events(const hipEvent_t* evs, int n);   // (the owner destroys them)
     int out_channels() const { return out_c_; }
     int out_h() const { return cur_ ? cur_->lh[out_level_] : 0; }
     int out_w() const { return cur_ ? cur_->lw[out_level_] : 0; }
@@ -142,6 +149,7 @@ private:
 
     std::vector<std::unique_ptr<ShapePlan>> shapes_;   // oldest first
     ShapePlan* cur_ = nullptr;    // shape of the last forward
+    std::vector<std::pair<const float*, hipEvent_t>> readers_;   // note_reader
     DevBuf sink_;                 // persistent conv3: target of masked-off stores
     EventTimer timer_;            // forwards bracketed by HIP events (set_timing)
 };

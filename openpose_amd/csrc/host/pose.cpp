@@ -12,7 +12,10 @@
 // may already run the next batch.
 #include "pose.h"
 
+#include <sched.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstring>
 #include <exception>
@@ -61,6 +64,8 @@ PoseHip::~PoseHip()
     }
     if (post_) {
         (void)hipStreamSynchronize(post_);
+        if (net_) net_->forget_reader_events(post_done_, 2);
+        ctx_->remove_side_stream(post_);
         (void)hipStreamDestroy(post_);
         (void)hipEventDestroy(nets_done_);
         for (auto& e : post_done_) (void)hipEventDestroy(e);
@@ -207,7 +212,7 @@ void PoseHip::submit(const float* frames, int n, int net_h, int net_w, int prod_
     OPK_CHECK_ARG(net_ != nullptr, "no network: use forward_net_output (poseNetOutput path)");
     OPK_CHECK_ARG(count_ < 2, "two batches already in flight: collect first");
     ctx_->bind();
-    next_output(n, net_h, net_w, true);   // (waits for the posts reading that buffer)
+    next_output(n, net_h, net_w, true);
     net_->forward(frames, n, net_h, net_w);
     const NetOutput o{net_->output(), net_->out_h(), net_->out_w()};
     submit_outputs(&o, 1, n, net_h, net_w, prod_w, prod_h, true);
@@ -223,6 +228,7 @@ hipStream_t PoseHip::post_stream(bool own_net)
         OPK_HIP(hipStreamCreateWithFlags(&post_, hipStreamNonBlocking));
         OPK_HIP(hipEventCreateWithFlags(&nets_done_, hipEventDisableTiming));
         for (auto& e : post_done_) OPK_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx_->add_side_stream(post_);   // opk_sync covers the post-processing
     }
     // everything on the context stream so far: the caller's work and this batch's nets
     OPK_HIP(hipEventRecord(nets_done_, ctx_->stream));
@@ -235,20 +241,12 @@ void PoseHip::wait_post(hipStream_t s)
     if (post_count_ > 0) OPK_HIP(hipStreamWaitEvent(s, post_done_[(post_count_ - 1) & 1], 0));
 }
 
-void PoseHip::wait_readers(hipStream_t s, const float* out)
-{
-    for (int back = 1; back <= 2 && back <= post_count_; ++back) {
-        const int k = (post_count_ - back) & 1;
-        bool reads = false;
-        for (int i = 0; i < post_nreads_[k]; ++i) reads = reads || post_reads_[k][i] == out;
-        if (reads) OPK_HIP(hipStreamWaitEvent(s, post_done_[k], 0));
-    }
-}
-
 void PoseHip::next_output(int n, int h, int w, bool alternate)
 {
+    // (the forward that writes the buffer waits for the post-processings reading it:
+    // NetHip::note_reader)
     const bool alt = alternate && post_ != nullptr && dev_switch("NET_OUT_ALT", 1) != 0;
-    wait_readers(ctx_->stream, net_->select_output(n, h, w, alt));
+    (void)net_->select_output(n, h, w, alt);
 }
 
 void PoseHip::set_input(int net_w, int net_h, float dyn, int scale_number, double scale_gap)
@@ -391,6 +389,8 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
     ctx_->bind();
     Slot& sl = slots_[(head_ + count_) & 1];
     const hipStream_t s = post_stream(own_net);
+    // dev hook: a slow post-processing, so a missing stream wait corrupts results every time
+    if (const int d = dev_switch("POST_DELAY_US", 0)) launch_delay(d, s);
     timer_.begin(s);
     if (overlay_) {   // synthetic people on the first scale's output
         const size_t out_elems = (size_t)n * C * outs[0].h * outs[0].w;
@@ -472,8 +472,9 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
     if (post_ && s == post_) {   // (the context stream may be the null stream)
         const int k = post_count_ & 1;
         OPK_HIP(hipEventRecord(post_done_[k], post_));
-        post_nreads_[k] = nscales;
-        for (int i = 0; i < nscales; ++i) post_reads_[k][i] = outs[i].ptr;
+        // every later forward writing one of these outputs (ours or a direct opk_net_forward)
+        // waits for this post-processing first
+        for (int i = 0; i < nscales; ++i) net_->note_reader(outs[i].ptr, post_done_[k]);
         ++post_count_;
     }
     sl.n = n;
@@ -482,6 +483,26 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
     sl.scale = scale;
     sl.heat = heat;
     ++count_;
+}
+
+int PoseHip::assembly_threads()
+{
+    // the CPUs this process may run on (its affinity mask: a rank pinned to its GPU-local cores
+    // by openpose_amd.parallel.pin_rank_cpus gets only those), not the machine's count
+    int cpus = 0;
+    cpu_set_t set;
+    if (sched_getaffinity(0, sizeof set, &set) == 0) cpus = CPU_COUNT(&set);
+    if (cpus <= 0) cpus = (int)std::max(1u, std::thread::hardware_concurrency());
+    return std::max(1, std::min(kAssemblyThreads, cpus));
+}
+
+void PoseHip::read_collect_times(int* count, double* wait_ms, double* assembly_ms)
+{
+    if (count) *count = collect_count_;
+    if (wait_ms) *wait_ms = collect_wait_ms_;
+    if (assembly_ms) *assembly_ms = collect_assembly_ms_;
+    collect_count_ = 0;
+    collect_wait_ms_ = collect_assembly_ms_ = 0.;
 }
 
 int PoseHip::collect()
@@ -502,7 +523,9 @@ int PoseHip::collect()
                            copy_));
     OPK_HIP(hipMemcpy2DAsync(hr, K * 4, sl.records.ptr, rf * 4, K * 4, n, hipMemcpyDeviceToHost,
                              copy_));
+    const auto tw0 = std::chrono::steady_clock::now();
     OPK_HIP(hipStreamSynchronize(copy_));
+    const auto tw1 = std::chrono::steady_clock::now();
 
     ConnectParams cp{(int)props_[OPK_PROP_MIN_SUBSET_CNT], (float)props_[OPK_PROP_MIN_SUBSET_SCORE],
                      sl.scale, maximize_positives_, semantics_};
@@ -547,10 +570,7 @@ int PoseHip::collect()
     }
     // people assembly: frames are independent (connectBodyParts* per frame), so they run on the
     // pool's kAssemblyThreads host threads; every frame's result is the single-threaded one
-    if (!pool_ && n > 1) {
-        const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-        pool_ = std::make_unique<WorkerPool>((int)std::min<unsigned>(kAssemblyThreads, hw));
-    }
+    if (!pool_ && n > 1) pool_ = std::make_unique<WorkerPool>(assembly_threads());
     const int workers = pool_ ? pool_->workers() : 1;
     if ((int)scratch_.size() < workers) scratch_.resize(workers);
     const float* ho = static_cast<const float*>(overflow_.ptr);
@@ -565,6 +585,10 @@ int PoseHip::collect()
     if (pool_) pool_->run(n, frame);
     else
         for (int f = 0; f < n; ++f) frame(f, 0);
+    const auto tw2 = std::chrono::steady_clock::now();
+    collect_wait_ms_ += std::chrono::duration<double, std::milli>(tw1 - tw0).count();
+    collect_assembly_ms_ += std::chrono::duration<double, std::milli>(tw2 - tw1).count();
+    ++collect_count_;
     head_ = (head_ + 1) & 1;
     --count_;
     last_ = si;

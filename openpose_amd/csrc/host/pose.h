@@ -81,11 +81,18 @@ public:
     // integrals: the work after the net forward), HIP events on the context stream
     void set_timing(bool on) { timer_.on = on; }
     void read_timing(int* count, double* total_ms) { timer_.read(count, total_ms); }
+    // host time of the collects since the last read: waiting for the batch's device results
+    // (D2H copies behind its post-processing) and assembling its people on the pool's threads
+    void read_collect_times(int* count, double* wait_ms, double* assembly_ms);
+    int assembly_workers() const { return pool_ ? pool_->workers() : assembly_threads(); }
     int model() const { return model_; }
 
     static constexpr int kMaxPeaks = kPoseMaxPeople;   // peaks blob [parts][128][3]
     static constexpr int kRecordHead = 16384;          // record floats copied eagerly per frame
-    static constexpr int kAssemblyThreads = 16;        // host threads assembling a batch's people
+    // host threads assembling a batch's people: at most this many, and at most the CPUs of the
+    // process's affinity mask (assembly_threads)
+    static constexpr int kAssemblyThreads = 16;
+    static int assembly_threads();
 
 private:
     struct Slot {
@@ -129,19 +136,18 @@ private:
     // next batch's warp overlaps this batch's post-processing.  The nets alternate between two
     // output buffers per input shape (NetHip::select_output; NET_OUT_ALT=0: one), and before a
     // forward the context stream waits for those of the last two recorded post-processings that
-    // read the buffer it is about to write (wait_readers) -- so batch i+1's nets start while batch
-    // i's post-processing still runs.  POST_STREAM=0: all on the context stream.
+    // read the buffer it is about to write (NetHip::note_reader, which also orders a direct
+    // opk_net_forward of the same net after them) -- so batch i+1's nets start while batch i's
+    // post-processing still runs.  post_ is a side stream of the context (opk_sync waits for it).
+    // POST_STREAM=0: all on the context stream.
     // The injection path (submit_net_output: a caller-owned net output) stays on the context
     // stream, so a caller may rewrite that buffer on its stream after submit.
     hipStream_t post_ = nullptr;
     hipEvent_t nets_done_ = nullptr, post_done_[2] = {};
     int post_count_ = 0;                     // post-processings recorded on post_
-    const float* post_reads_[2][kMaxResizeSources] = {};   // net outputs they read, by parity
-    int post_nreads_[2] = {};
     hipStream_t post_stream(bool own_net);   // the stream a batch's post-processing runs on
     void wait_post(hipStream_t s);           // s after the last recorded post-processing
-    void wait_readers(hipStream_t s, const float* out);   // s after recorded posts reading out
-    // the output buffer the next forward of this shape writes, after the waits it needs
+    // switch the shape's output buffer for its next forward (alternate) and plan the shape
     void next_output(int n, int h, int w, bool alternate);
     DevBuf cand_;                            // NMS candidate counters (zeroed once, self-resetting)
     // multi-scale: the nets of scales 1.. run on their own streams beside scale 0's
@@ -155,6 +161,8 @@ private:
     // people assembly: worker threads (started by the first multi-frame collect) and one
     // scratch per worker
     std::unique_ptr<WorkerPool> pool_;
+    int collect_count_ = 0;
+    double collect_wait_ms_ = 0., collect_assembly_ms_ = 0.;
     std::vector<AssemblyScratch> scratch_;
 
     float scale_net_to_output_ = 1.f;

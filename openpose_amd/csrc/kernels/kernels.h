@@ -143,6 +143,7 @@ void launch_hbm_read(const void* buf, size_t bytes, float* out, int blocks, hipS
 
 // ---- elementwise helpers (misc.hip) -----------------------------------------------------------
 void launch_add_inplace(float* dst, const float* src, size_t n, hipStream_t stream);
+void launch_delay(int microseconds, hipStream_t stream);   // dev hook: hold a stream
 void launch_f64_to_f32(float* dst, const double* src, size_t n, hipStream_t stream);
 void launch_f32_to_f64(double* dst, const float* src, size_t n, hipStream_t stream);
 // getHeatMapsCopy: dst [frames][nsel][hw] from heat [frames][channels][hw]; sel_dev = nsel source

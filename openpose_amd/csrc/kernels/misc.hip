@@ -19,6 +19,14 @@ __global__ __launch_bounds__(256) void add_inplace_kernel(float* __restrict__ ds
     for (size_t i = n4 * 4 + (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
         dst[i] += src[i];
 }
+// dev hook (POST_DELAY_US): one wave that holds its stream for `ticks` of the 100 MHz constant
+// clock, so stream-ordering tests see a slow post-processing every time (bounded: the loop ends
+// when the clock has advanced that far)
+__global__ __launch_bounds__(64) void delay_kernel(unsigned long long ticks)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(32);
+}
 // element type conversion for the plugin functions' double instantiations (opk_convert): one
 // rounding per element (double -> float round to nearest even, float -> double exact)
 template <typename D, typename S>
@@ -78,6 +86,13 @@ void launch_heat_copy(float* dst, const float* heat, const int* sel_dev, int nse
     const unsigned bx = (unsigned)std::min<size_t>((hw + 255) / 256, 64);
     hipLaunchKernelGGL(heat_copy_kernel, dim3(bx, nsel, frames), dim3(256), 0, stream, dst, heat,
                        sel_dev, nsel, channels, hw, scale_mode);
+    OPK_LAUNCH_CHECK();
+}
+
+void launch_delay(int microseconds, hipStream_t stream)
+{
+    OPK_CHECK_ARG(microseconds >= 0 && microseconds <= 1000000, "delay: 0 .. 1 s");
+    hipLaunchKernelGGL(delay_kernel, dim3(1), dim3(64), 0, stream, (unsigned long long)microseconds * 100ull);
     OPK_LAUNCH_CHECK();
 }
 

@@ -653,8 +653,11 @@ __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ 
     // which lanes test a column, by the row's kind in nmsCpu's rules (testable: not the window's
     // halo columns, inside the map): an inner row tests inner and edge columns, an edge row (1,
     // h-2) every in-map column, an outer row (0, h-1) the edge columns only -- as wave masks.
-    // Out-of-map COLUMNS need no value: no tested pixel has one as a neighbour (x = 0 and w-1 are
-    // never tested); out-of-map ROWS hold th (the border rule's outside value).
+    // Out-of-map ROWS hold th (the border rule's outside value).  Out-of-map COLUMNS (neighbours
+    // of x = 0 and x = w-1, tested on the edge rows 1 and h-2) read 0 from zero coefficients
+    // where nmsCpu compares with th: the same outcome, since a tested value is > th >= 0 (both
+    // comparisons hold) -- a negative threshold is rejected as nmsCpu rejects it
+    // ("threshold value invalid.", nmsBase.cpp:121-122; api.cpp opk_nms, pose.cpp).
     uint64_t Min[CPL], Mok[CPL], Mout[CPL];
     bool cinner[CPL];
 #pragma unroll

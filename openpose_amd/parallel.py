@@ -58,6 +58,113 @@ def run_sharded(process_batch, n_frames, batch, rank, world):
     return out
 
 
+# ---- per-rank host CPUs ---------------------------------------------------------------------------
+def _cpulist(text):
+    out = []
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def gpu_numa_nodes(root="/sys/class/kfd/kfd/topology/nodes"):
+    """NUMA node of every GPU in KFD topology order (the HIP device order when no *_VISIBLE_DEVICES
+    remaps it): a GPU node (simd_count > 0) links to its CPU node through io_links.  [] when the
+    topology is not readable."""
+    try:
+        nodes = sorted(int(n) for n in os.listdir(root) if n.isdigit())
+    except OSError:
+        return []
+    props = {}
+    for n in nodes:
+        try:
+            with open(os.path.join(root, str(n), "properties")) as f:
+                props[n] = dict(l.split()[:2] for l in f if len(l.split()) >= 2)
+        except OSError:
+            return []
+    cpu_nodes = [n for n in nodes if int(props[n].get("cpu_cores_count", 0)) > 0]
+    out = []
+    for n in nodes:
+        if int(props[n].get("simd_count", 0)) == 0:
+            continue
+        numa = None
+        links = os.path.join(root, str(n), "io_links")
+        for l in sorted(os.listdir(links)) if os.path.isdir(links) else []:
+            try:
+                with open(os.path.join(links, l, "properties")) as f:
+                    to = dict(x.split()[:2] for x in f if len(x.split()) >= 2).get("node_to")
+            except OSError:
+                continue
+            if to is not None and int(to) in cpu_nodes:
+                numa = cpu_nodes.index(int(to))
+                break
+        out.append(numa)
+    return out
+
+
+def rank_cpus(local_rank, local_world, affinity=None, gpu_numa=None, node_cpus=None):
+    """Host CPUs for rank `local_rank` of `local_world` ranks on one node (one GPU each): the CPUs of
+    its GPU's NUMA node within the process's affinity mask, split into disjoint contiguous shares
+    among the ranks on that node -- the reference's per-GPU worker threads
+    (wrapperAuxiliary.hpp:328-337, 1050-1067) each with host cores of their own for the people
+    assembly.  Without NUMA information (or a node with none of the allowed CPUs) the affinity
+    mask is split into local_world contiguous shares.  None: leave the mask alone (one rank)."""
+    if local_world <= 1:
+        return None
+    aff = sorted(affinity if affinity is not None else os.sched_getaffinity(0))
+    if gpu_numa is None:
+        visible = any(os.environ.get(k) for k in ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+                                                  "ROCR_VISIBLE_DEVICES"))
+        gpu_numa = [] if visible else gpu_numa_nodes()
+    gpu = local_rank if os.environ.get("OPK_BENCH_REHEARSE") != "1" else 0
+    group, pool = list(range(local_world)), aff
+    if gpu_numa and all(g is not None for g in gpu_numa) and len(gpu_numa) >= local_world:
+        def numa_of(r):
+            return gpu_numa[r if os.environ.get("OPK_BENCH_REHEARSE") != "1" else 0]
+        node = gpu_numa[gpu]
+        if node_cpus is None:
+            try:
+                with open("/sys/devices/system/node/node%d/cpulist" % node) as f:
+                    cpus = set(_cpulist(f.read()))
+            except OSError:
+                cpus = set()
+        else:
+            cpus = set(node_cpus[node])
+        local = [c for c in aff if c in cpus]
+        if local:
+            group = [r for r in range(local_world) if numa_of(r) == node]
+            pool = local
+    k, i = len(group), group.index(local_rank)
+    share = len(pool) // k
+    if share == 0:
+        return [pool[i % len(pool)]]
+    return pool[i * share:(i + 1) * share]
+
+
+def pin_rank_cpus(local_rank, local_world):
+    """Restrict this process (before it starts any thread or touches a GPU) to rank_cpus(); returns
+    the CPU list applied, or None."""
+    cpus = rank_cpus(local_rank, local_world)
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+    return cpus
+
+
+def cpu_ranges(cpus):
+    """[0, 1, 2, 5] -> '0-2,5'."""
+    out, cpus = [], sorted(cpus)
+    i = 0
+    while i < len(cpus):
+        j = i
+        while j + 1 < len(cpus) and cpus[j + 1] == cpus[j] + 1:
+            j += 1
+        out.append("%d" % cpus[i] if i == j else "%d-%d" % (cpus[i], cpus[j]))
+        i = j + 1
+    return ",".join(out)
+
+
 # ---- launcher: one process per GPU --------------------------------------------------------------
 def free_port():
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
@@ -112,13 +219,17 @@ class RecordGather:
     packs its slice's records (PoseExtractor.records(): per frame [people, keypoints, scores]),
     and one gather per step (RCCL over xGMI on the GPU box, gloo on CPU) moves them to rank 0.
     `finish()` on rank 0 returns the records of every frame in frame order and raises if a frame
-    is missing or duplicated.  `capacity` = floats per rank and step (records beyond it raise)."""
+    is missing or duplicated.  `capacity` = floats per rank and step (records beyond it raise).
+    `collective`: move the records through the collective even at world size 1 (a process group
+    must exist) -- the 1-GPU box's test of the transport an N-GPU run uses (pinned staging,
+    events, dist.gather of device tensors, the device-side unpack)."""
 
-    def __init__(self, world, rank, capacity, steps, device, group=None):
+    def __init__(self, world, rank, capacity, steps, device, group=None, collective=False):
         self.world, self.rank, self.steps, self.group = world, rank, steps, group
         self.device = torch.device(device)
         self.cap = int(capacity)
-        if world == 1:
+        self.local = world == 1 and not collective
+        if self.local:
             # nothing to move: the records stay on the host, one block per step (pages touched
             # here, outside any timed region)
             self.blocks = np.zeros((steps, HEAD + self.cap), np.float32)
@@ -145,7 +256,7 @@ class RecordGather:
         if n > self.cap:
             raise RuntimeError("rank %d step %d: %d record floats exceed the gather capacity %d"
                                % (self.rank, step, n, self.cap))
-        if self.world == 1:
+        if self.local:
             blk = self.blocks[step]
             blk[:HEAD] = (self.rank, step, first_frame, n_frames, n)
             blk[HEAD:HEAD + n] = records
@@ -178,7 +289,7 @@ class RecordGather:
         """Rank 0: [(keypoints [people, parts, 3], scores [people]), ...] for frames 0..F-1."""
         if self.rank != 0:
             return None
-        if self.world == 1:   # headers and bodies in place (never-pushed steps: header -1)
+        if self.local:   # headers and bodies in place (never-pushed steps: header -1)
             heads = self.blocks[:, None, :HEAD]
             starts = (np.arange(self.steps) * (HEAD + self.cap) + HEAD)[:, None]
             body_all = self.blocks.reshape(-1)

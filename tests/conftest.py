@@ -20,3 +20,22 @@ def ctx():
     c = Context(0)
     yield c
     c.close()
+
+
+_REPORTED = []
+
+
+def pytest_runtest_logreport(report):
+    """Collect the measured quantities tests publish with record_property("report_...", value)
+    (e.g. the full-strength keypoint parity), so that they are printed at the end of the run."""
+    if report.when == "call":
+        for k, v in report.user_properties:
+            if k.startswith("report_"):
+                _REPORTED.append((report.nodeid, k[len("report_"):], v))
+
+
+def pytest_terminal_summary(terminalreporter):
+    if _REPORTED:
+        terminalreporter.section("measured (record_property report_*)")
+        for nodeid, k, v in _REPORTED:
+            terminalreporter.write_line("%s: %s = %s" % (nodeid.split("::")[-1], k, v))

@@ -129,6 +129,32 @@ def test_record_gather_single_rank_roundtrip():
         g.finish(parts)
 
 
+def test_record_gather_forced_collective_single_rank():
+    """RecordGather(collective=True) at world size 1 (bench.py --collective-gather): the records
+    go through dist.gather and the device-side unpack, here over a one-rank gloo group on CPU;
+    the result equals the host path's."""
+    import torch.distributed as dist
+    from tests.rank_stub import frame_result
+    steps, batch, parts = 3, 4, 25
+    results = [frame_result(f, parts) for f in range(steps * batch)]
+    cap = max(parallel.pack_records(results[i * batch:(i + 1) * batch], parts).size
+              for i in range(steps))
+    dist.init_process_group("gloo", init_method="tcp://127.0.0.1:%d" % parallel.free_port(),
+                            rank=0, world_size=1)
+    try:
+        g = parallel.RecordGather(1, 0, cap, steps, "cpu", collective=True)
+        assert not g.local
+        for i in range(steps):
+            g.push(i, i * batch, batch, parallel.pack_records(results[i * batch:(i + 1) * batch], parts))
+        got = g.finish(parts)
+    finally:
+        dist.destroy_process_group()
+    assert len(got) == steps * batch
+    for (kp, ks), (rk, rs) in zip(got, results):
+        np.testing.assert_array_equal(kp, np.asarray(rk, np.float32).reshape(-1, parts, 3))
+        np.testing.assert_array_equal(ks, rs)
+
+
 def test_bench_rejects_world_mismatch():
     import subprocess
     env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
@@ -150,3 +176,28 @@ def test_bench_content_depends_on_global_batch_only():
                 k = step * world + rank
                 assert k % bench.CONTENTS in have
             assert have == {(s * world + rank) % bench.CONTENTS for s in range(12)}
+
+
+def test_rank_cpus_disjoint_gpu_local_shares(monkeypatch):
+    """every rank's people-assembly threads get a disjoint share of its GPU's
+    NUMA-local CPUs (parallel.rank_cpus, applied by bench.py before any GPU call); the assembly
+    pool is sized from the affinity mask (PoseHip::assembly_threads)."""
+    monkeypatch.delenv("OPK_BENCH_REHEARSE", raising=False)
+    aff = list(range(256))
+    numa = [0, 0, 0, 0, 1, 1, 1, 1]
+    node_cpus = {0: range(0, 128), 1: range(128, 256)}
+    shares = [parallel.rank_cpus(r, 8, aff, numa, node_cpus) for r in range(8)]
+    seen = set()
+    for r, s in enumerate(shares):
+        assert len(s) == 32 and not seen & set(s)
+        seen |= set(s)
+        assert set(s) <= set(node_cpus[numa[r]])   # GPU-local
+    # the mask restricts the shares; no NUMA information: contiguous split of the mask
+    shares = [parallel.rank_cpus(r, 2, list(range(16, 48)), [], None) for r in range(2)]
+    assert shares == [list(range(16, 32)), list(range(32, 48))]
+    assert parallel.rank_cpus(0, 1, aff, numa, node_cpus) is None   # one rank: mask untouched
+    # rehearsal (every rank on GPU 0): the ranks split GPU 0's node
+    monkeypatch.setenv("OPK_BENCH_REHEARSE", "1")
+    shares = [parallel.rank_cpus(r, 2, aff, numa, node_cpus) for r in range(2)]
+    assert shares == [list(range(0, 64)), list(range(64, 128))]
+    assert parallel.cpu_ranges([0, 1, 2, 5, 7, 8]) == "0-2,5,7-8"

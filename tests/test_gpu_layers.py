@@ -7,7 +7,8 @@ Geometry: the bench's (bench.py): BODY_25 at 656x368 with the tile-aligned batch
 (tile_aligned_batch: 130 frames on a 256-CU MI355X), so every kernel instantiation the bench
 launches -- conv1_fused, conv3w<128/96>, conv3w8<128, 1/2/4> with and without the pooled epilogue,
 conv_head<512/256, 2/4>, the 16-wave conv3 1x1 tiles -- runs here with the bench's grid and tile
-walk.  Frames 0, 64 and the last one are checked (first, middle, last tile rounds).
+walk.  Frames 0, n//2 - 1 (64 at 130 frames) and the last one are checked (first, middle,
+last tile rounds).
 
 Bound per output element (oracle/fp16.py): |gpu - ref| <= 2 ulp16(ref) + C_ACC * S,
 S = sum |w x| + |b|.  C_ACC = 2^-16 (one conv) / 2^-14 (kernels with an fp16 intermediate on

@@ -131,71 +131,87 @@ def test_end_to_end_keypoints_within_tolerance(ctx):
         assert np.abs(ks - rs).max() <= KEYPOINT_TOL
 
 
-def _peak_drift(ref_peaks, got_peaks, radius=1.0):
-    """Fraction of the reference peaks with a peak of the same part within `radius` heat-map
-    pixels, and the largest such displacement."""
-    matched, total, worst = 0, 0, 0.0
-    for c in range(ref_peaks.shape[0]):
-        r = ref_peaks[c, 1:int(ref_peaks[c, 0, 0]) + 1, :2]
-        g = got_peaks[c, 1:int(got_peaks[c, 0, 0]) + 1, :2]
-        total += len(r)
-        if len(r) == 0 or len(g) == 0:
-            continue
-        d = np.sqrt(((r[:, None, :] - g[None, :, :]) ** 2).sum(-1)).min(1)
-        ok = d <= radius
-        matched += int(ok.sum())
-        if ok.any():
-            worst = max(worst, float(d[ok].max()))
-    return (matched / total if total else 1.0), worst, total
+# Stated parity bounds at full strength (random He weights, out_scale 1, no overlay: every peak
+# comes from the CNN, ~2,400 peaks per frame, many of them near-ties of neighbouring pixels).
+# fp16 storage of ~100 layers' activations moves the net output by rel-L2 ~2e-3, which flips the
+# order of pixels whose fp32 values differ by less than that: those peaks move by one pixel.
+UNSCALED_REL_L2 = 5e-3
+UNSCALED_PEAKS_IDENTICAL = 0.80   # fraction of fp32 peaks detected at the identical pixel
+UNSCALED_PEAKS_WITHIN_1PX = 0.95
+UNSCALED_PEOPLE_DELTA = 0.03      # |people - fp32 people| / fp32 people
 
 
 def test_end_to_end_unscaled_heads(ctx, record_property):
-    """Full-strength heads (out_scale 1, no overlay) at 656x368, one frame.
+    """Full-strength heads (out_scale 1, no overlay) at 656x368, two frames.
 
     (1) post-processing isolated: the oracle's resize -> NMS -> connector run on the GPU's OWN net
         output must give the GPU pipeline's peaks and keypoints bit for bit;
-    (2) fp16-vs-fp32 CNN drift, measured: the same chain on the fp32 oracle net output; the
-        fraction of fp32 peaks reproduced within 1 heat-map pixel and the largest displacement
-        are recorded (record_property) and bounded loosely.
+    (2) fp16-vs-fp32 CNN drift, measured and bounded: the same chain on the fp32 oracle net
+        output; the fraction of fp32 NMS peaks (nmsCpu's integer pixels, oracle/parity.py) the GPU
+        finds at the identical pixel and within 1 heat-map pixel, the largest refined-peak and
+        keypoint shifts and the people counts are printed at the end of the run (conftest:
+        report_*) and checked against the UNSCALED_* bounds above.
     poseExtractorCaffe.cpp:246-333 is the chain both sides follow."""
+    from oracle import parity
     graph = body25.layers()
     params = synth.he_weights(graph, seed=31, out_scale=1.0)
-    x = np.random.default_rng(32).uniform(-0.5, 0.5, (1, 3, 368, 656)).astype(np.float32)
+    x = np.random.default_rng(32).uniform(-0.5, 0.5, (2, 3, 368, 656)).astype(np.float32)
     net = Net(ctx, "builtin:BODY_25")
     net.set_params(params)
     pose = PoseExtractor(ctx, net)
     pose.forward(_dev(x), (1280, 720))
     s = pose.scale_net_to_output()
     off = float(np.float32(0.5 / np.float64(s)))
-    gpu_out = net.output_numpy()[0]
-    gpu_peaks = pose.peaks_numpy()[0]
-    kp, ks = pose.keypoints(0)
+    gpu_outs = net.output_numpy()
+    stats = {"fp32_peaks": 0, "same": 0.0, "near": 0.0, "shift": 0.0, "kshift": 0.0,
+             "people": 0, "people32": 0, "num": 0.0, "den": 0.0}
+    for k in range(2):
+        gpu_out = gpu_outs[k]
+        gpu_peaks = pose.peaks_numpy()[k]
+        kp, ks = pose.keypoints(k)
 
-    heat = oracle.resize_merge([gpu_out], 368, 656)
-    peaks = oracle.nms(heat, 0.05, 128, (off, off))
-    rk, rs = oracle.connect(heat, peaks, scale=s)
-    for c in range(25):
-        n = int(peaks[c, 0, 0])
-        assert int(gpu_peaks[c, 0, 0]) == n
-        np.testing.assert_array_equal(gpu_peaks[c, 1:n + 1], peaks[c, 1:n + 1])
-    np.testing.assert_array_equal(kp, rk)
-    np.testing.assert_array_equal(ks, rs)
+        heat = oracle.resize_merge([gpu_out], 368, 656)
+        peaks = oracle.nms(heat, 0.05, 128, (off, off))
+        rk, rs = oracle.connect(heat, peaks, scale=s)
+        for c in range(25):
+            n = int(peaks[c, 0, 0])
+            assert int(gpu_peaks[c, 0, 0]) == n
+            np.testing.assert_array_equal(gpu_peaks[c, 1:n + 1], peaks[c, 1:n + 1])
+        np.testing.assert_array_equal(kp, rk)
+        np.testing.assert_array_equal(ks, rs)
 
-    ref_out = body25.forward(x, params, graph=graph)[0]
-    err = float(np.linalg.norm(gpu_out - ref_out) / np.linalg.norm(ref_out))
-    heat32 = oracle.resize_merge([ref_out], 368, 656)
-    peaks32 = oracle.nms(heat32, 0.05, 128, (off, off))
-    frac, worst, total = _peak_drift(peaks32, gpu_peaks)
-    rk32, _ = oracle.connect(heat32, peaks32, scale=s)
-    record_property("net_rel_l2", err)
-    record_property("fp32_peaks", total)
-    record_property("peaks_within_1px", frac)
-    record_property("max_peak_shift_px", worst)
-    record_property("people_fp16_fp32", (len(kp), len(rk32)))
-    print("unscaled heads: rel-L2 %.2e, %d fp32 peaks, %.4f within 1 px (max shift %.3f px), "
-          "people %d vs %d" % (err, total, frac, worst, len(kp), len(rk32)))
-    assert err < 5e-3
-    assert total > 0 and frac >= 0.9
+        ref_out = body25.forward(x[k:k + 1], params, graph=graph)[0]
+        stats["num"] += float(np.sum((gpu_out.astype(np.float64) - ref_out) ** 2))
+        stats["den"] += float(np.sum(ref_out.astype(np.float64) ** 2))
+        heat32 = oracle.resize_merge([ref_out], 368, 656)
+        total, same, near = parity.compare_peaks(parity.peak_mask(heat32, 0.05, 25),
+                                                 parity.peak_mask(heat, 0.05, 25))
+        peaks32 = oracle.nms(heat32, 0.05, 128, (off, off))
+        rk32, _ = oracle.connect(heat32, peaks32, scale=s)
+        kshift, _ = parity.keypoint_shift(rk32, kp)
+        stats["fp32_peaks"] += total
+        stats["same"] += same * total
+        stats["near"] += near * total
+        stats["shift"] = max(stats["shift"], parity.refined_shift(peaks32, gpu_peaks))
+        stats["kshift"] = max(stats["kshift"], kshift)
+        stats["people"] += len(kp)
+        stats["people32"] += len(rk32)
+    err = (stats["num"] / stats["den"]) ** 0.5
+    total = stats["fp32_peaks"]
+    same, near = stats["same"] / total, stats["near"] / total
+    delta = abs(stats["people"] - stats["people32"]) / max(stats["people32"], 1)
+    for k, v in (("net_rel_l2", round(err, 6)), ("fp32_peaks", total),
+                 ("peak_index_identical", round(same, 5)), ("peaks_within_1px", round(near, 5)),
+                 ("max_refined_peak_shift_px", round(stats["shift"], 4)),
+                 ("max_keypoint_shift_px", round(stats["kshift"], 4)),
+                 ("people_gpu_fp32", (stats["people"], stats["people32"]))):
+        record_property("report_" + k, v)
+    print("unscaled heads: rel-L2 %.2e, %d fp32 peaks, %.4f identical, %.4f within 1 px (max "
+          "shift %.3f px), people %d vs %d" % (err, total, same, near, stats["shift"],
+                                               stats["people"], stats["people32"]))
+    assert err < UNSCALED_REL_L2
+    assert total > 0 and same >= UNSCALED_PEAKS_IDENTICAL and near >= UNSCALED_PEAKS_WITHIN_1PX
+    assert delta <= UNSCALED_PEOPLE_DELTA
 
 
 def test_pose_submit_collect_pipeline(ctx):

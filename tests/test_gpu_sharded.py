@@ -77,3 +77,36 @@ def test_alternating_net_outputs_same_records(tmp_path):
     np.testing.assert_array_equal(a["keypoints"], b["keypoints"])
     np.testing.assert_array_equal(a["scores"], b["scores"])
     assert a["counts"].sum() >= 32
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config", ["body25", "body135"])
+def test_rccl_gather_one_rank(config, tmp_path):
+    """The RCCL transport of an N-GPU run, executed on the 1-GPU box: bench.py
+    --collective-gather creates an nccl process group of one rank and forces RecordGather through
+    its collective branch -- pinned host staging, events, dist.gather of CUDA tensors, the
+    device-side unpack (_unpack_device) -- and the max-over-ranks all-gather on the device.  The
+    gathered records must equal the host path's (world size 1, no process group) bit for bit."""
+    batch, steps = 8, 3
+
+    def run(extra, dump):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "OPK_BENCH_REHEARSE"):
+            env.pop(k, None)
+        r = subprocess.run([sys.executable, "bench.py", "--gpus", "1", "--steps", str(steps),
+                            "--warmup", "1", "--batch", str(batch), "--no-cpu-baseline",
+                            "--config", config, "--dump-records", dump] + extra,
+                           cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-3000:]
+        return json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    dc, dh = str(tmp_path / "coll.npz"), str(tmp_path / "host.npz")
+    line = run(["--collective-gather"], dc)
+    assert line["n_gpus"] == 1 and "RCCL" in line["config"]["parallelism"]
+    assert line["config"]["frames_gathered_in_order"] == batch * steps
+    run([], dh)
+    a, b = np.load(dc), np.load(dh)
+    assert len(a["counts"]) == batch * steps
+    np.testing.assert_array_equal(a["counts"], b["counts"])
+    np.testing.assert_array_equal(a["keypoints"], b["keypoints"])
+    np.testing.assert_array_equal(a["scores"], b["scores"])
+    assert a["counts"].sum() >= batch

@@ -1,0 +1,41 @@
+"""CPU: the parity checker (oracle/parity.py) against the oracle's nmsCpu restatement -- the numpy
+peak test must accept exactly the pixels orc_nms counts, border rules included."""
+import numpy as np
+
+import oracle
+from oracle import parity
+
+
+def test_peak_mask_matches_oracle_nms():
+    rng = np.random.default_rng(0)
+    for trial in range(6):
+        h, w = (23, 31) if trial % 2 else (40, 17)
+        heat = rng.uniform(0, 1, (25, h, w)).astype(np.float32)
+        if trial >= 2:   # plateaus: ties decide the strict / non-strict rules
+            heat = np.round(heat * 4) / 4
+        if trial >= 4:   # sparse maps: peaks on and next to the border
+            heat *= rng.uniform(0, 1, heat.shape) > 0.7
+        th = 0.05
+        mask = parity.peak_mask(heat, th)
+        peaks = oracle.nms(heat, th, 128, (0.0, 0.0))
+        for c in range(25):
+            n = int(peaks[c, 0, 0])
+            m = int(mask[c].sum())
+            assert n == min(m, 127), (trial, c, n, m)
+            if m <= 127:   # the integer pixel of each refined peak is a mask pixel
+                ys, xs = np.nonzero(mask[c])
+                # raster order, as nmsCpu collects them
+                assert list(zip(ys, xs)) == sorted(zip(ys, xs))
+
+
+def test_compare_peaks_and_keypoint_shift():
+    a = np.zeros((2, 10, 10), bool)
+    b = np.zeros((2, 10, 10), bool)
+    a[0, 3, 3] = a[0, 6, 6] = a[1, 2, 7] = True
+    b[0, 3, 3] = b[0, 6, 7] = b[1, 5, 5] = True
+    total, same, near = parity.compare_peaks(a, b)
+    assert total == 3 and same == 1 / 3 and near == 2 / 3
+    r = np.array([[[1, 1, 1], [2, 2, 1]], [[10, 10, 1], [0, 0, 0]]], np.float32)
+    g = np.array([[[10.5, 10, 1], [0, 0, 0]], [[1, 1.25, 1], [2, 2, 1]]], np.float32)
+    worst, matched = parity.keypoint_shift(r, g)
+    assert matched == 2 and abs(worst - 0.5) < 1e-6

@@ -254,3 +254,80 @@ def test_gpu_pose_frames_rewritten_between_submits(ctx):
         for f in range(n):
             np.testing.assert_array_equal(got[b][f][0], ref[b][f][0])
             np.testing.assert_array_equal(got[b][f][1], ref[b][f][1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("delay_us", [0, 30000])
+def test_gpu_pose_direct_forward_between_submit_and_collect(ctx, delay_us):
+    """a batch's post-processing runs on the pipeline's side stream and reads
+    the net output; a direct forward of the SAME net and shape queued on the context stream after
+    the submit (opk_net_forward) writes that same buffer.  It must wait for the post-processing
+    (NetHip::note_reader).  The dev hook POST_DELAY_US holds the post-processing stream for 30 ms
+    before it reads anything, so a missing wait corrupts the batch deterministically, not by
+    timing luck.  Also: the pipelined submits with the delay (batch i+1's nets on the other output
+    buffer) and opk_sync covering the side stream."""
+    import torch
+    from oracle import body25
+    from openpose_amd import synth
+    from openpose_amd.api import Net, PoseExtractor, dev_switches
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(synth.he_weights(body25.layers(), seed=5, out_scale=0.02))
+    size, n = (256, 144), 2
+    _, [(w, h)] = api.scale_and_size(size, (-1, 128))
+    ov = torch.from_numpy(np.stack([synth.overlay(3, h // 8, w // 8, seed=60 + f)
+                                    for f in range(n)])).cuda()
+    frames = [_frames(n, size[1], size[0], 200 + b).cuda() for b in range(3)]
+
+    def people(pose):
+        return [pose.keypoints(f) for f in range(n)]
+
+    with dev_switches(POST_STREAM=0):   # reference: everything on the context stream
+        pose = PoseExtractor(ctx, net)
+        pose.set_input((-1, 128))
+        pose.set_overlay(ov)
+        ref = []
+        for b in range(3):
+            pose.forward_frames(frames[b])
+            ref.append(people(pose))
+        pose.close()
+    assert not all(np.array_equal(ref[0][f][1], ref[1][f][1]) for f in range(n))
+
+    with dev_switches(POST_DELAY_US=delay_us):
+        pose = PoseExtractor(ctx, net)
+        pose.set_input((-1, 128))
+        pose.set_overlay(ov)
+        # 1. submit, then a direct forward of the same shape (batch 1's net input), then collect
+        pose.submit_frames(frames[0])
+        x0 = torch.from_numpy(pose.net_input_numpy()).cuda()   # (synchronises the context stream)
+        net.forward(torch.flip(x0, dims=[3]).contiguous())     # another input, same shape
+        pose.collect()
+        got0 = people(pose)
+        for f in range(n):
+            np.testing.assert_array_equal(got0[f][0], ref[0][f][0])
+            np.testing.assert_array_equal(got0[f][1], ref[0][f][1])
+        # 2. pipelined submits (alternating output buffers) under the delay
+        got = []
+        for b in range(3):
+            pose.submit_frames(frames[b])
+            if pose.pending() == 2:
+                pose.collect()
+                got.append(people(pose))
+        while pose.pending():
+            pose.collect()
+            got.append(people(pose))
+        for b in range(3):
+            for f in range(n):
+                np.testing.assert_array_equal(got[b][f][0], ref[b][f][0])
+                np.testing.assert_array_equal(got[b][f][1], ref[b][f][1])
+        # 3. opk_sync waits for the side stream too: with the post-processing held for 30 ms
+        #    after the nets, a sync right after the submit takes at least that long
+        import time
+        pose.submit_frames(frames[2])
+        t0 = time.perf_counter()
+        ctx.sync()
+        if delay_us:
+            assert time.perf_counter() - t0 >= 0.8 * delay_us * 1e-6
+        pose.collect()
+        for f in range(n):
+            np.testing.assert_array_equal(people(pose)[f][1], ref[2][f][1])
+        pose.close()
