@@ -106,6 +106,15 @@ __device__ __forceinline__ void opkw_bst(const uint2& v, __amdgpu_buffer_rsrc_t 
 #ifndef OPKW_ABLATE   // dev probe only (tools/conv3w_probe.hip): 1 no mid-unit barrier, 2 no MFMAs,
 #define OPKW_ABLATE 0  // 3 no fragment reads, 4 no DMA after the prologue (timing only, wrong results)
 #endif
+#ifndef OPKW_HALO_SAME   // dev probe only: every chunk's halo DMA reads chunk 0's bytes (L2-warm
+#define OPKW_HALO_SAME 0  // halo for chunks 1..: is the halo's HBM/MALL traffic the stall? wrong results)
+#endif
+#ifndef OPKW_DESYNC       // dev probe: workgroup group g = (blockIdx.x >> 3) % OPKW_DESYNC_N starts
+#define OPKW_DESYNC 0     // g * OPKW_DESYNC cycles late, so the CUs' halo bursts fall apart in time
+#endif
+#ifndef OPKW_DESYNC_N
+#define OPKW_DESYNC_N 2
+#endif
 #if OPKW_ABLATE == 3
 #define OPKW_DSR(dst_, addr_, off_)                                                           \
     asm volatile("; no read %1" : "=v"(dst_) : "v"(addr_))
@@ -150,6 +159,11 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
     const int tix = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (blockIdx.x >> 3);
     int m = tix;
     if (m >= ntm) return;
+    if (OPKW_DESYNC > 0) {
+        const unsigned long long d = (unsigned long long)(((blockIdx.x >> 3) % OPKW_DESYNC_N) * OPKW_DESYNC);
+        const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+        while (__builtin_amdgcn_s_memtime() - t0 < d) __builtin_amdgcn_s_sleep(2);
+    }
 
     // bias and negative-side multiplier (1 none, 0 ReLU, slope PReLU) for the whole launch:
     // loaded into registers here, stored to LDS once the prologue's DMA wait has covered them
@@ -193,7 +207,7 @@ __global__ __launch_bounds__(64 * kW_NW, 1) void conv3w_kernel(const ConvArgs a)
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
                 if (API % NW == 0 || i_ * NW + wave < API)                                    \
                     __builtin_amdgcn_global_load_lds(                                         \
-                        (const void*)(abase + (c_) * 64 + ((nt_) ? aoffn[i_] : aoff[i_])),    \
+                        (const void*)(abase + (OPKW_HALO_SAME ? 0 : (c_)) * 64 + ((nt_) ? aoffn[i_] : aoff[i_])), \
                         (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * NW + wave) * 64]), \
                         16, 0, OPKW_APOL);                                                            \
         }                                                                                     \

@@ -80,29 +80,52 @@ def refined_shift(ref_peaks, got_peaks, radius=1.0):
     return worst
 
 
-def keypoint_shift(ref_kp, got_kp):
-    """Largest keypoint displacement (pixels of the keypoint coordinates) over people matched
-    greedily by mean distance of the parts both detect, and the number matched.  kp:
-    [people, parts, 3] (x, y, score; score 0 = part absent)."""
+def keypoint_shift(ref_kp, got_kp, radius=2.0):
+    """Largest keypoint displacement over people matched greedily (smallest mean distance first)
+    among pairs that detect the same parts with a mean distance <= radius, and the number matched.
+    kp: [people, parts, 3] (x, y, score; score 0 = part absent), distances in kp units."""
     ref_kp = np.asarray(ref_kp, np.float64)
     got_kp = np.asarray(got_kp, np.float64)
     if len(ref_kp) == 0 or len(got_kp) == 0:
         return 0.0, 0
-    cost = np.full((len(ref_kp), len(got_kp)), np.inf)
-    for i, r in enumerate(ref_kp):
-        for j, g in enumerate(got_kp):
-            both = (r[:, 2] > 0) & (g[:, 2] > 0)
-            if both.any():
-                cost[i, j] = np.sqrt(((r[both, :2] - g[both, :2]) ** 2).sum(-1)).mean()
+    pr = ref_kp[:, :, 2] > 0
+    pg = got_kp[:, :, 2] > 0
+    same_parts = (pr[:, None, :] == pg[None, :, :]).all(-1)
+    d = np.sqrt(((ref_kp[:, None, :, :2] - got_kp[None, :, :, :2]) ** 2).sum(-1))   # [R, G, parts]
+    cnt = np.maximum(pr.sum(-1), 1)[:, None]
+    cost = np.where(same_parts, (d * pr[:, None, :]).sum(-1) / cnt, np.inf)
     worst, matched = 0.0, 0
     used_r, used_g = set(), set()
     for flat in np.argsort(cost, axis=None):
         i, j = divmod(int(flat), cost.shape[1])
-        if not np.isfinite(cost[i, j]) or i in used_r or j in used_g:
+        if not cost[i, j] <= radius:
+            break
+        if i in used_r or j in used_g:
             continue
         used_r.add(i)
         used_g.add(j)
-        both = (ref_kp[i, :, 2] > 0) & (got_kp[j, :, 2] > 0)
-        worst = max(worst, float(np.abs(ref_kp[i, both, :2] - got_kp[j, both, :2]).max()))
+        worst = max(worst, float(np.abs(ref_kp[i, pr[i], :2] - got_kp[j, pr[i], :2]).max()))
         matched += 1
     return worst, matched
+
+
+def people_identical(ref_kp, got_kp, tol):
+    """Number of reference people that some GPU person reproduces exactly: the same parts, every
+    keypoint within tol (kp units), one GPU person per reference person."""
+    ref_kp = np.asarray(ref_kp, np.float64)
+    got_kp = np.asarray(got_kp, np.float64)
+    if len(ref_kp) == 0 or len(got_kp) == 0:
+        return 0
+    pr = ref_kp[:, :, 2] > 0
+    pg = got_kp[:, :, 2] > 0
+    ok = (pr[:, None, :] == pg[None, :, :]).all(-1)
+    diff = np.abs(ref_kp[:, None, :, :2] - got_kp[None, :, :, :2]).max(-1)   # [R, G, parts]
+    ok &= np.where(pr[:, None, :], diff <= tol, True).all(-1)
+    used, n = set(), 0
+    for i in range(len(ref_kp)):
+        for j in np.nonzero(ok[i])[0]:
+            if int(j) not in used:
+                used.add(int(j))
+                n += 1
+                break
+    return n

@@ -135,9 +135,12 @@ def test_end_to_end_keypoints_within_tolerance(ctx):
 # comes from the CNN, ~2,400 peaks per frame, many of them near-ties of neighbouring pixels).
 # fp16 storage of ~100 layers' activations moves the net output by rel-L2 ~2e-3, which flips the
 # order of pixels whose fp32 values differ by less than that: those peaks move by one pixel.
+# Measured (round 5, profiles/round5/): rel-L2 1.5e-3, 90.4 % of 18,658 fp32 peaks at the
+# identical pixel, 97.5 % within 1 px, people 348 vs 346 (the bench's parity block on its own
+# frames: 93.6 % / 98.3 %).
 UNSCALED_REL_L2 = 5e-3
-UNSCALED_PEAKS_IDENTICAL = 0.80   # fraction of fp32 peaks detected at the identical pixel
-UNSCALED_PEAKS_WITHIN_1PX = 0.95
+UNSCALED_PEAKS_IDENTICAL = 0.88   # fraction of fp32 peaks detected at the identical pixel
+UNSCALED_PEAKS_WITHIN_1PX = 0.96
 UNSCALED_PEOPLE_DELTA = 0.03      # |people - fp32 people| / fp32 people
 
 
@@ -164,7 +167,7 @@ def test_end_to_end_unscaled_heads(ctx, record_property):
     off = float(np.float32(0.5 / np.float64(s)))
     gpu_outs = net.output_numpy()
     stats = {"fp32_peaks": 0, "same": 0.0, "near": 0.0, "shift": 0.0, "kshift": 0.0,
-             "people": 0, "people32": 0, "num": 0.0, "den": 0.0}
+             "people": 0, "people32": 0, "num": 0.0, "den": 0.0, "exact": 0}
     for k in range(2):
         gpu_out = gpu_outs[k]
         gpu_peaks = pose.peaks_numpy()[k]
@@ -188,7 +191,8 @@ def test_end_to_end_unscaled_heads(ctx, record_property):
                                                  parity.peak_mask(heat, 0.05, 25))
         peaks32 = oracle.nms(heat32, 0.05, 128, (off, off))
         rk32, _ = oracle.connect(heat32, peaks32, scale=s)
-        kshift, _ = parity.keypoint_shift(rk32, kp)
+        kshift, _ = parity.keypoint_shift(rk32, kp, radius=2.0 * s)
+        stats["exact"] += parity.people_identical(rk32, kp, 1e-3 * s)
         stats["fp32_peaks"] += total
         stats["same"] += same * total
         stats["near"] += near * total
@@ -204,7 +208,8 @@ def test_end_to_end_unscaled_heads(ctx, record_property):
                  ("peak_index_identical", round(same, 5)), ("peaks_within_1px", round(near, 5)),
                  ("max_refined_peak_shift_px", round(stats["shift"], 4)),
                  ("max_keypoint_shift_px", round(stats["kshift"], 4)),
-                 ("people_gpu_fp32", (stats["people"], stats["people32"]))):
+                 ("people_gpu_fp32", (stats["people"], stats["people32"])),
+                 ("people_identical_1e-3", round(stats["exact"] / max(stats["people32"], 1), 4))):
         record_property("report_" + k, v)
     print("unscaled heads: rel-L2 %.2e, %d fp32 peaks, %.4f identical, %.4f within 1 px (max "
           "shift %.3f px), people %d vs %d" % (err, total, same, near, stats["shift"],
@@ -344,7 +349,7 @@ def test_pose_injection_mixed_record_lengths(ctx):
             assert (len(kp) > 0) == (people[src] > 0)
 
 
-def _multiscale_case(ctx, nscales, gap, seed, nms_stream=1, nms_walk=None):
+def _multiscale_case(ctx, nscales, gap, seed, nms_stream=1, nms_walk=None, frames=2):
     """--scale_number nscales --scale_gap gap through opk_pose_forward_multi, sizes from
     ScaleAndSizeExtractor (scaleAndSizeExtractor.cpp:74-88); merged heat maps (resizeAndMergeCpu
     average, resizeAndMergeBase.cpp:55-106), peaks and people bit-identical to the oracle chain fed
@@ -358,14 +363,14 @@ def _multiscale_case(ctx, nscales, gap, seed, nms_stream=1, nms_walk=None):
     net = Net(ctx, "builtin:BODY_25")
     net.set_params(params)
     rng = np.random.default_rng(seed + 1)
-    xs = [rng.uniform(-0.5, 0.5, (2, 3, h, w)).astype(np.float32) for h, w in sizes]
+    xs = [rng.uniform(-0.5, 0.5, (frames, 3, h, w)).astype(np.float32) for h, w in sizes]
     outs = []
     for x in xs:
         net.forward(_dev(x))
         outs.append(net.output_numpy())
     assert [o.shape[2:] for o in outs] == [(h // 8, w // 8) for h, w in sizes]
     # the overlay rides on scale 0 only: scaled so that the average over the scales keeps people
-    ov = np.stack([synth.overlay(4, 46, 82, seed=2300 + k) for k in range(2)]).astype(np.float32)
+    ov = np.stack([synth.overlay(4, 46, 82, seed=2300 + k) for k in range(frames)]).astype(np.float32)
     ov *= np.float32(max(1.0, nscales / 4.0))
     pose = PoseExtractor(ctx, net)
     ovd = _dev(ov)
@@ -380,7 +385,7 @@ def _multiscale_case(ctx, nscales, gap, seed, nms_stream=1, nms_walk=None):
     off = float(np.float32(0.5 / np.float64(s)))
     gpu_heat = pose.heatmaps_numpy()
     gpu_peaks = pose.peaks_numpy()
-    for k in range(2):
+    for k in range(frames):
         heat = oracle.resize_merge([outs[0][k] + ov[k]] + [o[k] for o in outs[1:]], 368, 656)
         np.testing.assert_array_equal(gpu_heat[k], heat)
         peaks = oracle.nms(heat, 0.05, 128, (off, off))
@@ -416,6 +421,11 @@ def test_nms_walk_variants_bitexact(ctx, walk, nscales):
     default) and the one-column ring walk (NMS_WALK=0) -- give the oracle's peaks and people, with
     1 and 4 sources (the other tests run the default)."""
     _multiscale_case(ctx, nscales, 0.25, 90 + nscales, 1, walk)
+
+
+def test_nms_one_frame(ctx):
+    """A batch of one frame (25 planes) through the streaming walk: peaks and people the oracle's."""
+    _multiscale_case(ctx, 1, 0.25, 97, 1, 8, frames=1)
 
 
 def _resize_get_scale_factor(init, target):

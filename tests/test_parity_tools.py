@@ -39,3 +39,7 @@ def test_compare_peaks_and_keypoint_shift():
     g = np.array([[[10.5, 10, 1], [0, 0, 0]], [[1, 1.25, 1], [2, 2, 1]]], np.float32)
     worst, matched = parity.keypoint_shift(r, g)
     assert matched == 2 and abs(worst - 0.5) < 1e-6
+    assert parity.keypoint_shift(r, g, radius=0.3) == (0.25, 1)
+    assert parity.people_identical(r, g, 0.3) == 1 and parity.people_identical(r, g, 0.6) == 2
+    g[0, 1] = [3, 3, 1]   # another part set: never matched
+    assert parity.keypoint_shift(r, g) == (0.25, 1)

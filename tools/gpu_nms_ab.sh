@@ -1,18 +1,14 @@
 #!/bin/bash
-# dev: the whole GPU suite + smoke on the product build, then an interleaved bench A/B of a variant
-# build against it on configs 2 and 5, and a kernel trace of the product build
-#   gpu_nms_ab.sh OUTDIR VARIANT
-cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-out=gpurun_out/$1; var=$2
-mkdir -p $out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $out/pytest_gpu.log 2>&1 || exit 1
-timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $out/smoke.log 2>&1 || exit 1
-V=$GRAFT_REPO_ROOT/openpose_amd/variants/libopk_$var.so
-for rep in 1 2; do
-  OPK_LIB_PATH=$V timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 60 > $out/bench_${var}_$rep.log 2>&1 || exit 1
-  timeout -k 10 200 python -u bench.py --no-cpu-baseline --steps 60 > $out/bench_base_$rep.log 2>&1 || exit 1
-  OPK_LIB_PATH=$V timeout -k 10 200 python -u bench.py --no-cpu-baseline --config body135 > $out/b135_${var}_$rep.log 2>&1 || exit 1
-  timeout -k 10 200 python -u bench.py --no-cpu-baseline --config body135 > $out/b135_base_$rep.log 2>&1 || exit 1
+# dev (round 5): NMS walk, one vs two maps per wave (NMS_MAPS) -- the NMS / pipeline GPU tests,
+# configs 5 and 2 interleaved, kernel statistics of config 5 under both
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && O=gpurun_out/${OUT:-nms_ab} && mkdir -p $O || exit 1
+timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_pipeline.py tests/test_gpu_postprocess.py tests/test_semantics.py > $O/pytest.log 2>&1 || exit 1
+for i in 1 2; do
+  for m in 1 2; do
+    timeout -k 10 200 python -u bench.py --config body135 --steps 30 --no-cpu-baseline --dev NMS_MAPS=$m > $O/b135_m${m}_$i.log 2>&1 || exit 1
+    timeout -k 10 200 python -u bench.py --steps 20 --no-cpu-baseline --dev NMS_MAPS=$m > $O/b25_m${m}_$i.log 2>&1 || exit 1
+  done
 done
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline > $out/prof.log 2>&1 || exit 1
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof135 -o run -- python bench.py --steps 10 --warmup 3 --no-cpu-baseline --config body135 > $out/prof135.log 2>&1 || exit 1
+for m in 1 2; do
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof_b135_m$m -o run -- python bench.py --config body135 --steps 10 --no-cpu-baseline --dev NMS_MAPS=$m > $O/prof_b135_m$m.log 2>&1 || exit 1
+done

@@ -33,10 +33,12 @@ def main():
     f, w = per_kernel(fetch), per_kernel(write)
     cnn = [k for k in f if ("conv" in k and "kernel" in k) or "maxpool" in k]
     forwards = sum(f[k][0] for k in f if "conv1_fused_kernel" in k or "conv_image_kernel" in k)
-    fetch_b = 2.0 * sum(f[k][1] for k in cnn) / forwards
-    write_b = sum(w[k][1] for k in cnn if k in w) / forwards
+    # a pass with no CNN (the BODY_135 injection config: post-processing only) has no forward to
+    # divide by: its CNN fields are None and only the post kernels are summarised
+    fetch_b = 2.0 * sum(f[k][1] for k in cnn) / forwards if forwards else None
+    write_b = sum(w[k][1] for k in cnn if k in w) / forwards if forwards else None
     by_kernel = {}
-    for k in cnn:
+    for k in (cnn if forwards else []):
         by_kernel[short(k)] = {
             "launches_per_forward": f[k][0] / forwards,
             "fetch_bytes_per_forward": 2.0 * f[k][1] / forwards,
@@ -51,7 +53,8 @@ def main():
     res = {"unit": "bytes per CNN forward of %d frames" % frames, "batch": frames,
            "forwards_profiled": forwards,
            "cnn_forward_fetch_bytes": fetch_b, "cnn_forward_write_bytes": write_b,
-           "cnn_forward_hbm_bytes": fetch_b + write_b, "by_kernel": by_kernel, "post": post,
+           "cnn_forward_hbm_bytes": fetch_b + write_b if forwards else None,
+           "by_kernel": by_kernel, "post": post,
            "correction": "FETCH_SIZE x2 (gfx950 wide-read undercount), WRITE_SIZE x1"}
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps({k: v for k, v in res.items() if k != "by_kernel"}, indent=1))
