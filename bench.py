@@ -233,14 +233,16 @@ def cpu_baseline(args, params, frames_np, overlays_np):
 PARITY_FRAMES = 3
 
 
-def gpu_parity_run(net, pose, convs, frames_u8):
+def gpu_parity_run(net, pose, convs, frames_u8, precision=0):
     """GPU half of the parity block (outside every timed region, after the bench): the bench's
     first PARITY_FRAMES frames at the bench geometry through the pipeline with FULL-strength heads
     (out_scale 1: the random net drives the maps, no overlay), so fp16-vs-fp32 CNN differences are
-    what the post-processing sees.  Returns what the CPU leg compares against."""
+    what the post-processing sees.  precision: opk_net_set_precision.  Returns what the CPU leg
+    compares against."""
     from openpose_amd import synth
     params = synth.he_weights(convs, seed=0, out_scale=1.0)
     net.set_params(params)
+    net.set_precision(precision)
     pose.set_overlay(None)
     pose.forward_frames(frames_u8[:PARITY_FRAMES])
     return {"params": params, "net_input": pose.net_input_numpy(), "net_output": net.output_numpy(),
@@ -248,65 +250,94 @@ def gpu_parity_run(net, pose, convs, frames_u8):
             "scale": pose.scale_net_to_output()}
 
 
-def cpu_parity(g, threads):
+def split_precision_cost(net, pose, frames_u8, fp16_ms):
+    """CNN time of one bench batch in split precision (HIP events, 3 forwards after a warm one),
+    against the fp16 forward of the timed steps."""
+    from openpose_amd.api import PRECISION_FP16, PRECISION_SPLIT
+    net.set_precision(PRECISION_SPLIT)
+    pose.forward_frames(frames_u8)
+    torch.cuda.synchronize()
+    net.set_timing(True)
+    for _ in range(3):
+        pose.forward_frames(frames_u8)
+    k, ms = net.read_timing()
+    net.set_timing(False)
+    net.set_precision(PRECISION_FP16)
+    return {"cnn_ms_per_step": round(ms / k, 3), "fp16_cnn_ms_per_step": round(fp16_ms, 3),
+            "relative_cost": round(ms / k / fp16_ms, 3),
+            "note": "split precision (opk_net_set_precision OPK_PRECISION_SPLIT): every weight and "
+                    "activation an fp16 hi/lo pair, three MFMA passes per conv on the generic conv "
+                    "kernel, no fused kernels"}
+
+
+def cpu_parity(gs, threads):
     """CPU half (the cpu_baseline leg: the fp32 reference path on the same frames, oracle/ +
     oracle/parity.py as the checker): net rel-L2, NMS peak indices identical / within 1 px, the
-    largest refined-peak and keypoint shifts, people counts.  North star: keypoints within 1e-3
-    of the CPU reference with peak indices bit-exact; this measures it on a CNN-driven field."""
+    largest refined-peak and keypoint shifts, people counts and people reproduced within 1e-3 --
+    for every GPU run in gs (one per precision; the fp32 reference computed once).  North star:
+    keypoints within 1e-3 of the CPU reference with peak indices bit-exact; this measures it on a
+    CNN-driven field."""
     import oracle
     from oracle import body25, parity
     graph = body25.layers()
-    s = g["scale"]
+    g0 = gs[0]
+    s = g0["scale"]
     off = float(np.float32(0.5 / np.float64(s)))
     t0 = time.perf_counter()
-    out = {"frames": PARITY_FRAMES, "workload": "BODY_25 656x368 net input from 1280x720 uint8 "
-           "frames, He-init weights with full-strength heads (out_scale 1), no overlay",
-           "per_frame": []}
-    tot_peaks = tot_same = tot_near = 0
-    worst_peak = worst_kp = 0.0
-    num = den = 0.0
+    refs = []
     for f in range(PARITY_FRAMES):
-        ref = body25.forward(g["net_input"][f:f + 1], g["params"], graph=graph, nthreads=threads)[0]
-        got = g["net_output"][f]
-        num += float(np.sum((got.astype(np.float64) - ref) ** 2))
-        den += float(np.sum(ref.astype(np.float64) ** 2))
+        ref = body25.forward(g0["net_input"][f:f + 1], g0["params"], graph=graph, nthreads=threads)[0]
         heat_r = oracle.resize_merge([ref], NET_H, NET_W)
-        heat_g = oracle.resize_merge([got], NET_H, NET_W)   # = the GPU's lazy maps (bit-exact)
-        total, same, near = parity.compare_peaks(parity.peak_mask(heat_r, 0.05, PARTS),
-                                                 parity.peak_mask(heat_g, 0.05, PARTS))
         peaks_r = oracle.nms(heat_r, 0.05, 128, (off, off))
         rk, _ = oracle.connect(heat_r, peaks_r, scale=s)
-        shift = parity.refined_shift(peaks_r, g["peaks"][f])
-        kshift, matched = parity.keypoint_shift(rk, g["keypoints"][f], radius=2.0 * s)
-        # north star: keypoints within 1e-3 (net-input pixels; keypoints are in frame pixels)
-        exact = parity.people_identical(rk, g["keypoints"][f], 1e-3 * s)
-        tot_peaks += total
-        tot_same += same * total
-        tot_near += near * total
-        worst_peak = max(worst_peak, shift)
-        worst_kp = max(worst_kp, kshift)
-        out["per_frame"].append({
-            "net_rel_l2": round(float(np.linalg.norm(got - ref) / np.linalg.norm(ref)), 6),
-            "fp32_peaks": total, "peak_index_identical": round(same, 5),
-            "peaks_within_1px": round(near, 5), "people_gpu": len(g["keypoints"][f]),
-            "people_fp32": len(rk), "people_matched_2px": matched,
-            "people_identical_1e-3": exact, "max_keypoint_shift_px": round(kshift, 4)})
-    out.update({
-        "net_rel_l2": round((num / den) ** 0.5, 6),
-        "fp32_peaks": tot_peaks,
-        "peak_index_identical": round(tot_same / max(tot_peaks, 1), 5),
-        "peaks_within_1px": round(tot_near / max(tot_peaks, 1), 5),
-        "max_refined_peak_shift_heatmap_px": round(worst_peak, 4),
-        "max_keypoint_shift_px": round(worst_kp, 4),
-        "people_delta": sum(p["people_gpu"] - p["people_fp32"] for p in out["per_frame"]),
-        "people_identical_1e-3_frac": round(sum(p["people_identical_1e-3"] for p in out["per_frame"]) /
-                                            max(sum(p["people_fp32"] for p in out["per_frame"]), 1), 5),
-        "cpu_seconds": round(time.perf_counter() - t0, 1),
-        "note": "integer peak sets by nmsCpu's test on each side's own x8 maps; refined-peak shift "
-                "over peaks matched within 1 heat-map px; keypoint shift over people with the same "
-                "parts matched greedily within a 2 net-px mean distance (frame pixels); people "
-                "identical = same parts, every keypoint within 1e-3 net-input px"})
-    return out
+        refs.append((ref, parity.peak_mask(heat_r, 0.05, PARTS), peaks_r, rk))
+    outs = []
+    for g in gs:
+        out = {"frames": PARITY_FRAMES, "workload": "BODY_25 656x368 net input from 1280x720 uint8 "
+               "frames, He-init weights with full-strength heads (out_scale 1), no overlay",
+               "per_frame": []}
+        tot_peaks = tot_same = tot_near = 0
+        worst_peak = worst_kp = 0.0
+        num = den = 0.0
+        for f in range(PARITY_FRAMES):
+            ref, mask_r, peaks_r, rk = refs[f]
+            got = g["net_output"][f]
+            num += float(np.sum((got.astype(np.float64) - ref) ** 2))
+            den += float(np.sum(ref.astype(np.float64) ** 2))
+            heat_g = oracle.resize_merge([got], NET_H, NET_W)   # = the GPU's lazy maps (bit-exact)
+            total, same, near = parity.compare_peaks(mask_r, parity.peak_mask(heat_g, 0.05, PARTS))
+            shift = parity.refined_shift(peaks_r, g["peaks"][f])
+            kshift, matched = parity.keypoint_shift(rk, g["keypoints"][f], radius=2.0 * s)
+            # north star: keypoints within 1e-3 (net-input pixels; keypoints are in frame pixels)
+            exact = parity.people_identical(rk, g["keypoints"][f], 1e-3 * s)
+            tot_peaks += total
+            tot_same += same * total
+            tot_near += near * total
+            worst_peak = max(worst_peak, shift)
+            worst_kp = max(worst_kp, kshift)
+            out["per_frame"].append({
+                "net_rel_l2": round(float(np.linalg.norm(got - ref) / np.linalg.norm(ref)), 7),
+                "fp32_peaks": total, "peak_index_identical": round(same, 5),
+                "peaks_within_1px": round(near, 5), "people_gpu": len(g["keypoints"][f]),
+                "people_fp32": len(rk), "people_matched_2px": matched,
+                "people_identical_1e-3": exact, "max_keypoint_shift_px": round(kshift, 4)})
+        out.update({
+            "net_rel_l2": round((num / den) ** 0.5, 7),
+            "fp32_peaks": tot_peaks,
+            "peak_index_identical": round(tot_same / max(tot_peaks, 1), 5),
+            "peaks_within_1px": round(tot_near / max(tot_peaks, 1), 5),
+            "max_refined_peak_shift_heatmap_px": round(worst_peak, 4),
+            "max_keypoint_shift_px": round(worst_kp, 4),
+            "people_delta": sum(p["people_gpu"] - p["people_fp32"] for p in out["per_frame"]),
+            "people_identical_1e-3_frac": round(sum(p["people_identical_1e-3"] for p in out["per_frame"]) /
+                                                max(sum(p["people_fp32"] for p in out["per_frame"]), 1), 5),
+            "note": "integer peak sets by nmsCpu's test on each side's own x8 maps; refined-peak "
+                    "shift over peaks matched within 1 heat-map px; keypoint shift over people with "
+                    "the same parts matched greedily within a 2 net-px mean distance (frame pixels); "
+                    "people identical = same parts, every keypoint within 1e-3 net-input px"})
+        outs.append(out)
+    outs[0]["cpu_seconds"] = round(time.perf_counter() - t0, 1)
+    return outs
 
 
 def host_breakdown(host, steps, collect_times=None):
@@ -665,10 +696,17 @@ def rank_main(args, rank, world, local):
     if rank == 0 and world == 1 and nscales == 1 and not args.no_cpu_baseline:
         frames_np = frames[first_content][:2].cpu().numpy()   # uint8 [2][720][1280][3]
         result["cpu_baseline"] = cpu_baseline(args, params, frames_np, ov_np[first_content][:2])
-        # keypoint parity at full strength on the same frames (after every measurement: this
-        # replaces the net's weights)
-        result["parity"] = cpu_parity(gpu_parity_run(net, pose, convs, frames[first_content]),
-                                      args.cpu_threads)
+        # keypoint parity at full strength on the same frames, fp16 and split precision, and the
+        # cost of split precision (after every measurement: this replaces the net's weights)
+        from openpose_amd.api import PRECISION_FP16, PRECISION_SPLIT
+        g16 = gpu_parity_run(net, pose, convs, frames[first_content], PRECISION_FP16)
+        gsp = gpu_parity_run(net, pose, convs, frames[first_content], PRECISION_SPLIT)
+        net.set_precision(PRECISION_FP16)
+        p16, psp = cpu_parity([g16, gsp], args.cpu_threads)
+        psp["cost"] = split_precision_cost(net, pose, frames[first_content], net_ms)
+        p16["precision"] = "fp16 (the measured product path)"
+        psp["precision"] = "split (opk_net_set_precision OPK_PRECISION_SPLIT)"
+        result["parity"] = dict(p16, split_precision=psp)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:

@@ -275,6 +275,17 @@ int opk_net_set_conv(opk_net* net, const char* name, const float* weights_host,
 int opk_net_forward(opk_net* net, const float* input_dev, int n, int h, int w);
 /* useful (unpadded) convolution FLOPs of one frame of h x w (2 * MACs, all conv layers) */
 int opk_net_flops_per_frame(opk_net* net, int h, int w, double* flops);
+/* Arithmetic of the forward (no reference counterpart: Caffe's forward is fp32).
+ * OPK_PRECISION_FP16 (default): fp16 weights and stored activations, fp32 MFMA accumulation, the
+ *   tuned fused kernels -- net output within rel-L2 ~2.5e-3 of fp32 on random He-initialised
+ *   BODY_25 nets.
+ * OPK_PRECISION_SPLIT: every weight and activation held as an fp16 hi/lo pair (x = hi + lo to
+ *   ~22 bits), three MFMA passes per conv (x_hi w_hi + x_lo w_hi + x_hi w_lo, each product exact in
+ *   fp32): fp32-level results (parity mode) at ~3x the MFMA work and 2x the activation bytes, on
+ *   the generic conv kernel with no fusion.  Re-plans the net's shapes; loaded weights are kept. */
+#define OPK_PRECISION_FP16 0
+#define OPK_PRECISION_SPLIT 1
+int opk_net_set_precision(opk_net* net, int precision);
 /* Forward timing (measurement hook, no reference counterpart): while enabled every forward is
  * bracketed by HIP events on the context stream; read waits for them and returns the number of
  * forwards since the last read and their summed device time in milliseconds. */

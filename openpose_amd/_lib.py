@@ -88,6 +88,7 @@ _SIGS = {
     "opk_pose_set_timing": (_i, [_p, _i]),
     "opk_pose_read_timing": (_i, [_p, _ip, _c.POINTER(_d)]),
     "opk_pose_read_collect_times": (_i, [_p, _ip, _c.POINTER(_d), _c.POINTER(_d), _ip]),
+    "opk_net_set_precision": (_i, [_p, _i]),
     "opk_pose_records": (_i, [_p, _p, _c.c_size_t, _c.POINTER(_c.c_size_t)]),
     "opk_pose_heatmaps": (_i, [_p, _c.POINTER(_p), _ip]),
     "opk_pose_peaks": (_i, [_p, _c.POINTER(_p), _ip]),

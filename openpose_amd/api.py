@@ -19,6 +19,7 @@ from .pose_tables import (BODY_25, CONNECT_CPU, CONNECT_GPU, CONNECT_INTER_MIN_A
 
 # heat-map semantics (include/opk.h OPK_MAPS_*): the reference's CPU build or its CUDA build
 MAPS_CPU, MAPS_CUDA = 0, 1
+PRECISION_FP16, PRECISION_SPLIT = 0, 1      # opk_net_set_precision
 
 
 def _ptr(t):
@@ -442,6 +443,11 @@ class Net:
         n = ctypes.c_int()
         check(self.L.opk_net_load_caffemodel(self.h, path.encode(), ctypes.byref(n)))
         return n.value
+
+    def set_precision(self, precision):
+        """PRECISION_FP16 (default) or PRECISION_SPLIT (fp16 hi/lo pairs, ~fp32 results at ~3x
+        the MFMA work; opk_net_set_precision)."""
+        check(self.L.opk_net_set_precision(self.h, int(precision)))
 
     def set_timing(self, on=True):
         check(self.L.opk_net_set_timing(self.h, int(on)))

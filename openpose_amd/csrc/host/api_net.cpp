@@ -397,6 +397,14 @@ int opk_caffemodel_blob(const char* caffemodel, const char* layer, int index, fl
     });
 }
 
+int opk_net_set_precision(opk_net* net, int precision)
+{
+    return guarded_net([&] {
+        OPK_CHECK_ARG(net, "NULL net");
+        net->net->set_precision(precision);
+    });
+}
+
 int opk_net_set_timing(opk_net* net, int enable)
 {
     return guarded_net([&] {

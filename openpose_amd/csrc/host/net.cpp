@@ -293,6 +293,35 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
     ConvPlan& c = convs_[it->second];
     OPK_CHECK_ARG(w && b, name + ": weights and bias required");
     OPK_CHECK_ARG(c.info.act != 2 || slope, name + ": PReLU slopes required");
+    c.hw.assign(w, w + (size_t)c.info.cout * c.info.cin * c.info.k * c.info.k);
+    c.hb.assign(b, b + c.info.cout);
+    if (slope) c.hs.assign(slope, slope + c.info.cout);
+    else c.hs.clear();
+    pack(c);
+    c.loaded = true;
+    shapes_.clear();   // re-derive launch arguments
+    cur_ = nullptr;
+}
+
+void NetHip::set_precision(int precision)
+{
+    OPK_CHECK_ARG(precision == kPrecisionFp16 || precision == kPrecisionSplit, "unknown precision");
+    if (precision == precision_) return;
+    precision_ = precision;
+    for (auto& c : convs_)
+        if (c.loaded) pack(c);
+    shapes_.clear();
+    cur_ = nullptr;
+}
+
+void NetHip::pack(ConvPlan& c)
+{
+    const std::string& name = c.info.name;
+    (void)name;
+    const float* w = c.hw.data();
+    const float* b = c.hb.data();
+    const float* slope = c.hs.empty() ? nullptr : c.hs.data();
+    const bool split = precision_ == kPrecisionSplit;
     const int K = c.ksteps * kConvBK;
     const int cin = c.info.cin, k = c.info.k;
     const bool need_packed = c.from_image;   // conv_image's layout: [cout_pad][64]
@@ -313,25 +342,33 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
                 dst[t * c.cin_pad + ci] = f2h(w[(((size_t)co * cin + ci) * k + ky) * k + kx]);
         }
     }
-    // conv3.hip layout: [cout_pad/BN][cin_pad/32][ky][kx][n BN][ci 32]
+    // conv3.hip layout: [cout_pad/BN][cin_pad/32][ky][kx][n BN][ci 32]; split precision: three
+    // passes of chunks, [cout_pad/BN][3][cin_pad/32]..., holding w_hi, w_hi, w_lo (ConvArgs::split;
+    // the first conv then runs on conv3 too, over the 32-channel split image)
     std::vector<uint16_t> packed3;
-    if (!c.from_image) {
+    if (!c.from_image || split) {
         const int BN = conv3_shape(1, 1, 1, c.info.cout, k, border_).bn;   // BN depends on cout only
         const int nb = (c.info.cout + BN - 1) / BN, cpt = c.cin_pad / 32, kt = k * k;
-        packed3.assign((size_t)nb * cpt * kt * BN * 32, 0);
+        const int passes = split ? 3 : 1;
+        packed3.assign((size_t)nb * passes * cpt * kt * BN * 32, 0);
         for (int co = 0; co < c.info.cout; ++co)
             for (int ci = 0; ci < cin; ++ci)
                 for (int t = 0; t < kt; ++t) {
-                    const size_t idx =
-                        ((((size_t)(co / BN) * cpt + ci / 32) * kt + t) * BN + co % BN) * 32 + ci % 32;
-                    packed3[idx] = f2h(w[(((size_t)co * cin + ci) * k + t / k) * k + t % k]);
+                    const float wv = w[(((size_t)co * cin + ci) * k + t / k) * k + t % k];
+                    const _Float16 hi = (_Float16)wv;
+                    for (int ps = 0; ps < passes; ++ps) {
+                        const size_t idx = ((((size_t)(co / BN) * passes * cpt + ps * cpt + ci / 32) * kt + t) *
+                                                BN + co % BN) * 32 + ci % 32;
+                        packed3[idx] = ps < 2 ? __builtin_bit_cast(uint16_t, hi)
+                                              : f2h(wv - (float)hi);
+                    }
                 }
     }
     // conv_head.hip layouts: Mconv6 [cin_pad/32][n1][32]; Mconv7 K-permuted [n2 <= 32 ? 32 : 64][n1]
     std::vector<uint16_t> packedh;
     if (c.head >= 0) {
         const FuseHead& fh = heads_[c.head];
-        if (fh.a == it->second) {
+        if (&convs_[fh.a] == &c) {
             const int n1 = c.info.cout, cpt = c.cin_pad / 32;
             packedh.assign((size_t)cpt * n1 * 32, 0);
             for (int co = 0; co < n1; ++co)
@@ -374,9 +411,6 @@ void NetHip::set_conv(const std::string& name, const float* w, const float* b, c
     OPK_HIP(hipMemcpyAsync(db, bias.data(), bias.size() * 4, hipMemcpyHostToDevice, ctx_->stream));
     OPK_HIP(hipMemcpyAsync(ds, sl.data(), sl.size() * 4, hipMemcpyHostToDevice, ctx_->stream));
     OPK_HIP(hipStreamSynchronize(ctx_->stream));
-    c.loaded = true;
-    shapes_.clear();   // re-derive launch arguments
-    cur_ = nullptr;
 }
 
 bool NetHip::ready() const
@@ -433,12 +467,13 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
     std::vector<uint16_t*>& ptr = S.base;
     ptr.assign(bufs_.size(), nullptr);
     // CONV1_FUSED=0 (opk_dev_set, A/B tests): the three separate kernels instead of the fusion
-    S.fused1 = fuse1_.a >= 0 && dev_switch("CONV1_FUSED", 1) != 0 && border_ == 1 &&
+    S.split = precision_ == kPrecisionSplit;   // (split precision: no fused kernel)
+    S.fused1 = !S.split && fuse1_.a >= 0 && dev_switch("CONV1_FUSED", 1) != 0 && border_ == 1 &&
                conv1_fused_supported(h, w, 64, 64);
     // HEAD_FUSE=0 (opk_dev_set, A/B tests): Mconv6 and Mconv7 as two conv3 launches
     // Positions are decoded by float-reciprocal division in conv_head_kernel, exact below 2^24:
     // larger batches run the pairs unfused.
-    S.fusedh = !heads_.empty() && dev_switch("HEAD_FUSE", 1) != 0;
+    S.fusedh = !S.split && !heads_.empty() && dev_switch("HEAD_FUSE", 1) != 0;
     for (const auto& fh : heads_) {
         const int L = convs_[fh.a].level;
         S.fusedh = S.fusedh && (long)n * (lh_[L] + 2) * (lw_[L] + 2) < (1L << 24);
@@ -447,7 +482,7 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
     S.poolfused.assign(pools_.size(), 0);
     for (size_t q = 0; q < pools_.size(); ++q) {
         const int ci = pool_conv_[q];
-        if (ci < 0 || dev_switch("POOL_FUSE", 1) == 0) continue;
+        if (ci < 0 || S.split || dev_switch("POOL_FUSE", 1) == 0) continue;
         const ConvPlan& c = convs_[ci];
         const int H = lh_[c.level], W = lw_[c.level];
         const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, 3, border_);
@@ -455,9 +490,12 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
                          6 * (s3.sw + 2) <= 512 && s3.sw + 2 > 16 &&
                          lh_[c.level + 1] == H / 2 && lw_[c.level + 1] == W / 2;
     }
+    S.base_lo.assign(bufs_.size(), nullptr);
     for (size_t i = 0; i < bufs_.size(); ++i) {
         S.mem.push_back(std::make_unique<DevBuf>());
-        if ((int)i == image_buf_) continue;   // conv_image reads the NCHW input itself
+        S.mem_lo.push_back(std::make_unique<DevBuf>());
+        // conv_image reads the NCHW input itself (split precision: the split image, 32 channels)
+        if ((int)i == image_buf_ && !S.split) continue;
         bool head_buf = false;
         for (const auto& fh : heads_) head_buf = head_buf || fh.buf == (int)i;
         if (S.fusedh && head_buf) continue;   // Mconv6 outputs live only inside conv_head_kernel
@@ -478,6 +516,11 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
         // zeroed on the stream whose kernels read the plan first
         OPK_HIP(hipMemsetAsync(raw, 0, bytes, zero_stream ? zero_stream : ctx_->stream));
         ptr[i] = raw + head * bufs_[i].cs;
+        if (S.split) {   // the lo twin: same layout, zeroed borders and guards
+            uint16_t* rl = static_cast<uint16_t*>(S.mem_lo.back()->get(bytes));
+            OPK_HIP(hipMemsetAsync(rl, 0, bytes, zero_stream ? zero_stream : ctx_->stream));
+            S.base_lo[i] = rl + head * bufs_[i].cs;
+        }
     }
     const size_t out_bytes = (size_t)n * out_c_ * lh_[out_level_] * lw_[out_level_] * 4;
     S.out32 = static_cast<float*>(S.out_mem.get(out_bytes));
@@ -492,14 +535,14 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
         a.in_cs = bufs_[c.in.buf].cs;
         a.in_coff = c.in.coff;
         a.cin_pad = c.cin_pad;
-        a.ntaps = c.ntaps;
-        if (c.ntaps == 9)
+        a.ntaps = c.from_image && S.split ? 9 : c.ntaps;   // (split: the first conv on conv3)
+        if (a.ntaps == 9)
             for (int t = 0; t < 9; ++t) a.tapoff[t] = (t / 3) * Wp + (t % 3);
-        else if (c.ntaps == 1)
+        else if (a.ntaps == 1)
             a.tapoff[0] = Wp + 1;
         a.border = border_;
         a.ksteps = c.ksteps;
-        const bool use3 = !c.from_image;
+        const bool use3 = !c.from_image || S.split;
         S.use3[ci] = use3;
         OPK_CHECK_ARG(use3 || c.w.ptr != nullptr, c.info.name + ": weights not set");
         if (use3) {
@@ -526,7 +569,10 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
             a.dst[d] = ptr[c.outs[d].buf];
             a.dst_cs[d] = bufs_[c.outs[d].buf].cs;
             a.dst_coff[d] = c.outs[d].coff;
+            a.dst_lo[d] = S.base_lo[c.outs[d].buf];
         }
+        a.split = S.split ? 1 : 0;
+        a.in_lo = S.base_lo[c.in.buf];
         for (size_t q = 0; q < pools_.size(); ++q)
             if (S.poolfused[q] && pool_conv_[q] == (int)ci) {   // the pooled image instead
                 a.pool = 1;
@@ -634,15 +680,21 @@ void NetHip::blob(const std::string& name, int f0, int nf, float* host, int shap
                   name + ": kept on chip by a fused kernel (not materialised at this shape)");
     const int B = border_, Wp = W + 2 * B, Hp = H + 2 * B, cs = bufs_[L.buf].cs;
     const size_t frame_elems = (size_t)Hp * Wp * cs;
-    std::vector<uint16_t> raw(frame_elems * nf);
+    std::vector<uint16_t> raw(frame_elems * nf), rlo(S.split ? frame_elems * nf : 0);
     OPK_HIP(hipMemcpy(raw.data(), S.base[L.buf] + (size_t)f0 * frame_elems, raw.size() * 2,
                       hipMemcpyDeviceToHost));
+    if (S.split)   // split precision: the value is hi + lo
+        OPK_HIP(hipMemcpy(rlo.data(), S.base_lo[L.buf] + (size_t)f0 * frame_elems, rlo.size() * 2,
+                          hipMemcpyDeviceToHost));
     for (int f = 0; f < nf; ++f)
         for (int y = 0; y < H; ++y)
             for (int x = 0; x < W; ++x) {
-                const uint16_t* src = raw.data() + f * frame_elems + ((size_t)(y + B) * Wp + x + B) * cs + L.coff;
+                const size_t at = f * frame_elems + ((size_t)(y + B) * Wp + x + B) * cs + L.coff;
+                const uint16_t* src = raw.data() + at;
                 for (int c = 0; c < L.ch; ++c)
-                    host[((size_t)f * L.ch + c) * hw + (size_t)y * W + x] = (float)__builtin_bit_cast(_Float16, src[c]);
+                    host[((size_t)f * L.ch + c) * hw + (size_t)y * W + x] =
+                        (float)__builtin_bit_cast(_Float16, src[c]) +
+                        (S.split ? (float)__builtin_bit_cast(_Float16, rlo[at + c]) : 0.f);
             }
 }
 
@@ -668,6 +720,9 @@ void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w
     const std::vector<int>& lh_ = S.lh;
     const std::vector<int>& lw_ = S.lw;
     size_t first = 0;
+    if (S.split)   // the first conv's input as the split 32-channel image
+        launch_image_split(ptr[image_buf_], S.base_lo[image_buf_], bufs_[image_buf_].cs, input, n, h,
+                           w, border_, st);
     if (S.fused1) {
         const ConvPlan& a = convs_[fuse1_.a];
         const ConvPlan& b = convs_[fuse1_.b];
@@ -738,7 +793,7 @@ void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w
                 continue;
             }
             if (log) log->layer = c.info.name + (a.pool ? "+pool" : "");
-            if (c.from_image) {
+            if (c.from_image && !S.split) {
                 ConvArgs ai = a;
                 if (ai.out32) ai.out32 = out32;
                 launch_conv_image(ai, input, st);
@@ -753,8 +808,13 @@ void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w
             const PoolPlan& p = pools_[s.idx];
             const int L = p.level_in;
             if (log) log->layer = "pool";
-            launch_maxpool2(ptr[p.out_buf], ptr[p.in_buf], n, lh_[L], lw_[L],
-                            bufs_[p.in_buf].cs, lh_[L + 1], lw_[L + 1], st, border_);
+            if (S.split)
+                launch_maxpool2_split(ptr[p.out_buf], S.base_lo[p.out_buf], ptr[p.in_buf],
+                                      S.base_lo[p.in_buf], n, lh_[L], lw_[L], bufs_[p.in_buf].cs,
+                                      lh_[L + 1], lw_[L + 1], st, border_);
+            else
+                launch_maxpool2(ptr[p.out_buf], ptr[p.in_buf], n, lh_[L], lw_[L],
+                                bufs_[p.in_buf].cs, lh_[L + 1], lw_[L + 1], st, border_);
         }
     }
 }

@@ -22,6 +22,14 @@ public:
     };
     const std::vector<ConvInfo>& convs() const { return info_; }
     void set_conv(const std::string& name, const float* w, const float* b, const float* slope);
+    // Arithmetic of the forward: kPrecisionFp16 (default: fp16 weights and stored activations,
+    // fp32 MFMA accumulation, the tuned fused kernels) or kPrecisionSplit (every weight and
+    // activation as an fp16 hi / lo pair, three MFMA passes per conv on conv3_kernel, no fused
+    // kernels: ~fp32 results at ~3x the MFMA work; ConvArgs::split).  Re-plans the shapes and
+    // re-packs the loaded weights.
+    static constexpr int kPrecisionFp16 = 0, kPrecisionSplit = 1;
+    void set_precision(int precision);
+    int precision() const { return precision_; }
     bool ready() const;
     // caffe::Net::CopyTrainedLayersFrom (netCaffe.cpp:165,185): weights, bias and PReLU slopes of
     // every conv named in the file (shapes checked as Caffe does); layers the net does not have
@@ -94,7 +102,9 @@ private:
         int head = -1;        // index into heads_ (as either half), -1 none
         bool loaded = false;
         bool slope01 = true;  // PReLU slopes all in [0, 1] (ConvArgs::actmax)
+        std::vector<float> hw, hb, hs;   // host copies of the weights (re-packed per precision)
     };
+    void pack(ConvPlan& c);   // device layouts of one conv's weights for the current precision
     struct PoolPlan { int in_buf, out_buf, level_in, channels; };
     struct Step { bool conv; int idx; };
 
@@ -104,6 +114,9 @@ private:
         std::vector<int> lh, lw;
         std::vector<std::unique_ptr<DevBuf>> mem;
         std::vector<uint16_t*> base;   // first position of each buffer (past its head guard)
+        bool split = false;            // planned for kPrecisionSplit: every buffer has a lo twin
+        std::vector<std::unique_ptr<DevBuf>> mem_lo;
+        std::vector<uint16_t*> base_lo;
         DevBuf out_mem, out_mem_alt;
         float* out32 = nullptr;
         float* out32_alt = nullptr;    // the second output buffer (select_output)
@@ -141,6 +154,7 @@ private:
     // (and nothing else reads), -1 none; per input shape it runs fused where conv3w8 supports it
     std::vector<int> pool_conv_;
     int cus_ = 256;               // compute units (persistent-kernel grid)
+    int precision_ = kPrecisionFp16;
     int border_ = 1;              // zero border of every padded image (widest conv pad, >= 1)
 
     struct BlobLoc { int buf = -1, coff = 0, ch = 0, level = 0; bool out32 = false; };

@@ -48,6 +48,16 @@ struct ConvArgs {
                           // through a buffer resource (set by launch_conv3w)
     int pool;             // conv3w8: 2x2/2 max pool fused into the epilogue; dst[0] is the pooled
                           // padded image [frames][H/2+2][W/2+2][cs] (conv3w8_pool_supported)
+    // Split precision (NetHip precision OPK_PRECISION_SPLIT; conv3_kernel only): every activation
+    // x is held as two fp16 images, hi = fp16(x) and lo = fp16(x - hi) (in_lo / dst_lo: the lo
+    // twins, same layout and offsets), and every weight w as w_hi = fp16(w), w_lo = fp16(w - w_hi).
+    // The K loop runs three passes over the input channels -- x_hi * w_hi, x_lo * w_hi,
+    // x_hi * w_lo (weights packed [cout_pad/BN][3 * cin_pad/32][ky][kx][BN][32], pass-major) --
+    // each product exact in fp32, so only the fp32 summation and the dropped x_lo * w_lo term
+    // (~2^-22 relative) separate the result from an fp32 convolution.
+    int split;
+    const uint16_t* in_lo;
+    uint16_t* dst_lo[kConvMaxDst];
 };
 
 // conv3.hip: 7x7, 3x3 and 1x1, input halo staged once per 32-channel chunk over a "virtual image" of
@@ -128,6 +138,15 @@ bool conv1_fused_supported(int H, int W, int cout1, int cout2);
 void launch_conv1_fused(const Conv1FusedArgs& a, int workgroups, hipStream_t stream);
 
 // 2x2 stride-2 max pool with Caffe ceil sizing, padded NHWC fp16 -> padded NHWC fp16.
+// split precision: the lo twins of input and output; the pooled pair is the (hi, lo) pair of the
+// largest hi + lo (exact in fp32)
+void launch_maxpool2_split(uint16_t* out, uint16_t* out_lo, const uint16_t* in, const uint16_t* in_lo,
+                           int frames, int H, int W, int C, int OH, int OW, hipStream_t stream,
+                           int border);
+// split precision, the first conv's input: fp32 NCHW [frames][3][H][W] -> padded NHWC fp16 hi / lo
+// images of `cs` channels (3 used, the rest zero; border zero)
+void launch_image_split(uint16_t* hi, uint16_t* lo, int cs, const float* image, int frames, int H,
+                        int W, int border, hipStream_t stream);
 void launch_maxpool2(uint16_t* out, const uint16_t* in, int frames, int H, int W, int C, int OH,
                      int OW, hipStream_t stream, int border = 1);
 

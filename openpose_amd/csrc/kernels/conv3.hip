@@ -64,7 +64,9 @@ __device__ unsigned long long* opk3_stamps;
 // and epilogue stalls).
 // KS: 3 (3x3, pad 1) or 1 (1x1: the "halo" is the tile itself, one tap per chunk).
 // NW: waves per workgroup (8, or 16 for the 512-row tiles of the one-per-CU variant).
-template <int BM, int BN, int HR, int TAPU, int MINB, int KS, int NW = 8>
+// SPLIT: split precision (ConvArgs::split, conv.h) -- a separate instantiation, so the fp16 path
+// is unchanged
+template <int BM, int BN, int HR, int TAPU, int MINB, int KS, int NW = 8, bool SPLIT = false>
 __global__ __launch_bounds__(64 * NW, MINB) __attribute__((amdgpu_waves_per_eu(NW / 4 * MINB)))
 void conv3_kernel(const ConvArgs a)
 {
@@ -106,8 +108,11 @@ void conv3_kernel(const ConvArgs a)
 
     // ---- DMA lane geometry: 16 rows x 4 pieces per wave instruction --------------------------
     const int lrow = lane >> 2, phys = lane & 3;
-    const int cpt = a.cin_pad >> 5;               // 32-channel chunks
-    const int U = UPC * cpt;                      // units (chunk, taps)
+    const int cpt = a.cin_pad >> 5;               // 32-channel chunks of the input
+    // split precision: three passes over the chunks (x_hi w_hi, x_lo w_hi, x_hi w_lo; conv.h)
+    const int cptk = SPLIT ? 3 * cpt : cpt;       // K chunks
+    const int U = UPC * cptk;                     // units (chunk, taps)
+    const ptrdiff_t dlo = SPLIT ? a.in_lo - a.in : 0;   // hi -> lo twin (elements)
     // halo row hr = (i*8 + wave)*16 + lrow holds virtual position p0 - VW - 1 + hr; its image
     // address (chunk 0, swizzled piece) is fixed for the whole tile
     const uint16_t* arow[AIW];
@@ -123,7 +128,7 @@ void conv3_kernel(const ConvArgs a)
     // this wave issues halo instructions i*8 + wave < API and B instructions j*8 + wave < BPI
     const int ai = (API - wave + NW - 1) / NW;
     const int bi = (BPI - wave + NW - 1) / NW;
-    const uint16_t* wbase = a.w + (size_t)nb * cpt * KT * BN * 32;
+    const uint16_t* wbase = a.w + (size_t)nb * cptk * KT * BN * 32;
 
 #define OPK3_ISSUE(u_)                                                                        \
     do {                                                                                      \
@@ -131,10 +136,13 @@ void conv3_kernel(const ConvArgs a)
         /* dev probe only: 6 = no halo DMA, 7 = no weight DMA after the prologue */           \
         if ((u_) - c_ * UPC == 0 && (OPK3_ABLATE != 6 || (u_) < 2)) {                        \
             const int as_ = (c_ % NAS) * ASLOT;                                               \
+            /* split precision: pass 1 reads the lo twin; passes 0 and 2 the hi image */       \
+            const int ps_ = !SPLIT ? 0 : c_ >= 2 * cpt ? 2 : (c_ >= cpt ? 1 : 0);             \
+            const ptrdiff_t ao_ = (ptrdiff_t)(c_ - ps_ * cpt) * 32 + (ps_ == 1 ? dlo : 0);    \
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
                 if (API % NW == 0 || i_ * NW + wave < API)                                    \
                     __builtin_amdgcn_global_load_lds(                                         \
-                        (const void*)(arow[i_] + c_ * 32),                                    \
+                        (const void*)(arow[i_] + ao_),                                        \
                         (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * NW + wave) * 64]), \
                         16, 0, 0);                                                            \
         }                                                                                     \
@@ -277,7 +285,7 @@ void conv3_kernel(const ConvArgs a)
         for (int j = 0; j + 1 < NF; j += 2) {
 #pragma unroll
             for (int i = 0; i < MF; ++i) {
-                uint32_t pk[2][2];
+                uint32_t pk[2][2], pl[2][2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const float4_t t = acc[i][j + h] + bv[j + h];
@@ -285,16 +293,32 @@ void conv3_kernel(const ConvArgs a)
                     float v[4];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
-                    pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
-                    pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+                    const half2_t h01 = __builtin_convertvector((float2_t){v[0], v[1]}, half2_t);
+                    const half2_t h23 = __builtin_convertvector((float2_t){v[2], v[3]}, half2_t);
+                    pk[h][0] = __builtin_bit_cast(uint32_t, h01);
+                    pk[h][1] = __builtin_bit_cast(uint32_t, h23);
+                    // split precision: lo = fp16(v - hi) (v - hi is exact in fp32)
+                    pl[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                        (float2_t){v[0], v[1]} - __builtin_convertvector(h01, float2_t), half2_t));
+                    pl[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                        (float2_t){v[2], v[3]} - __builtin_convertvector(h23, float2_t), half2_t));
                 }
                 // every lane takes part in the swap; masked lanes store nothing afterwards
                 const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
                 const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+                uint4 lval = make_uint4(0, 0, 0, 0);
+                if constexpr (SPLIT) {
+                    const auto ll = __builtin_amdgcn_permlane16_swap(pl[0][0], pl[1][0], false, false);
+                    const auto lh = __builtin_amdgcn_permlane16_swap(pl[0][1], pl[1][1], false, false);
+                    lval = make_uint4(ll[0], lh[0], ll[1], lh[1]);
+                }
                 if (!pok[i] || cw + j * 16 >= a.cout) continue;
                 const uint4 val = make_uint4(sl[0], sh[0], sl[1], sh[1]);
-                for (int d = 0; d < a.ndst; ++d)
-                    *reinterpret_cast<uint4*>(a.dst[d] + a.dst_coff[d] + cw + j * 16 + prow[i] * a.dst_cs[d]) = val;
+                for (int d = 0; d < a.ndst; ++d) {
+                    const size_t o = a.dst_coff[d] + cw + j * 16 + prow[i] * a.dst_cs[d];
+                    *reinterpret_cast<uint4*>(a.dst[d] + o) = val;
+                    if constexpr (SPLIT) *reinterpret_cast<uint4*>(a.dst_lo[d] + o) = lval;
+                }
             }
         }
         OPK3_STAMP(5);
@@ -314,21 +338,33 @@ void conv3_kernel(const ConvArgs a)
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = t[r] > 0.f ? t[r] : tm[r];
             if (!pok[i] || ch >= a.cout) continue;
-            const uint32_t lo = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[0], v[1]}, half2_t));
-            const uint32_t hi = __builtin_bit_cast(uint32_t, __builtin_convertvector((float2_t){v[2], v[3]}, half2_t));
+            const half2_t h01 = __builtin_convertvector((float2_t){v[0], v[1]}, half2_t);
+            const half2_t h23 = __builtin_convertvector((float2_t){v[2], v[3]}, half2_t);
+            const uint32_t lo = __builtin_bit_cast(uint32_t, h01);
+            const uint32_t hi = __builtin_bit_cast(uint32_t, h23);
+            // split precision: the lo halves fp16(v - hi)
+            const uint32_t llo = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                (float2_t){v[0], v[1]} - __builtin_convertvector(h01, float2_t), half2_t));
+            const uint32_t lhi = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                (float2_t){v[2], v[3]} - __builtin_convertvector(h23, float2_t), half2_t));
             for (int d = 0; d < a.ndst; ++d) {
                 const int cs = a.dst_cs[d];
-                uint16_t* p = a.dst[d] + a.dst_coff[d] + ch + prow[i] * cs;
+                const size_t o = a.dst_coff[d] + ch + prow[i] * cs;
+                uint16_t* p = a.dst[d] + o;
                 if (vec && ((a.dst_coff[d] | cs) & 3) == 0) {
 #if OPK3_ABLATE == 5   // dev probe only: no output stores
                     asm volatile("" ::"v"(lo), "v"(hi), "v"(p));
 #else
                     *reinterpret_cast<uint2*>(p) = make_uint2(lo, hi);
+                    if constexpr (SPLIT) *reinterpret_cast<uint2*>(a.dst_lo[d] + o) = make_uint2(llo, lhi);
 #endif
                 } else {
 #pragma unroll
                     for (int e = 0; e < 4; ++e)
-                        if (ch + e < a.cout) p[e] = (uint16_t)((e < 2 ? lo : hi) >> (16 * (e & 1)));
+                        if (ch + e < a.cout) {
+                            p[e] = (uint16_t)((e < 2 ? lo : hi) >> (16 * (e & 1)));
+                            if constexpr (SPLIT) a.dst_lo[d][o + e] = (uint16_t)((e < 2 ? llo : lhi) >> (16 * (e & 1)));
+                        }
                 }
             }
             if (a.out32) {   // fp32 NCHW net output (the activations before fp16)
@@ -764,6 +800,7 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     const int nn = (a.cout + s.bn - 1) / s.bn;
     const long ntiles = ((total + s.bm - 1) / s.bm) * nn;
     dim3 grid((unsigned)ntiles);
+    OPK_CHECK_ARG(!a.split || (a.in_lo && !a.pool), "split precision: lo twin required, no pool fusion");
     // conv + 2x2 max pool in one persistent kernel (conv3w8.hip POOL epilogue); the planner only
     // asks for it where conv3w8_pool_supported holds
     if (a.pool) {
@@ -777,14 +814,15 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     // the fragment reads per MFMA; removed, source and numbers in profiles/round3/wino/)
     // several 128-channel n-blocks (the VGG 256 / 512-channel layers): conv3w8 with one n-block
     // per persistent block (bit-identical; CONV3W8N=0: the 16-wave conv3_kernel)
-    if (s.nw == 16 && s.persist && nn > 1 && s.bn == 128 && a.sink && !a.out32 && VW > 16 &&
+    // (split precision runs the plain conv3_kernel below: its K loop knows the three passes)
+    if (!a.split && s.nw == 16 && s.persist && nn > 1 && s.bn == 128 && a.sink && !a.out32 && VW > 16 &&
         dev_switch("CONV3W8N", 1) != 0 && conv3w8_supported(a)) {
         launch_conv3w8(a, stream);
         return;
     }
     // measured: +3-10 % on the single-n-block layers, 3-8 % slower with 2-4 n-blocks (kept 16-wave)
-    if (s.nw == 16 && s.persist && nn == 1 && a.sink && a.cus >= nn && a.cout % s.bn == 0 && !a.out32 &&
-        VW > 16) {
+    if (!a.split && s.nw == 16 && s.persist && nn == 1 && a.sink && a.cus >= nn && a.cout % s.bn == 0 &&
+        !a.out32 && VW > 16) {
         bool aligned = true;
         // 16-byte stores of 8-channel groups
         for (int d = 0; d < a.ndst; ++d) aligned = aligned && ((a.dst_coff[d] | a.dst_cs[d]) & 7) == 0;
@@ -832,15 +870,25 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     }
 #define OPK3_LAUNCH(BM_, BN_, HR_, TAPU_, MINB_, KS_)                                          \
     do {                                                                                       \
-        note_launch("conv3_kernel<%d,%d,%d,%d,%d,%d>", BM_, BN_, HR_, TAPU_, MINB_, KS_);       \
-        hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, MINB_, KS_>), grid, dim3(512), 0, \
-                           stream, a);                                                         \
+        note_launch("conv3_kernel<%d,%d,%d,%d,%d,%d%s>", BM_, BN_, HR_, TAPU_, MINB_, KS_,      \
+                    a.split ? ",8,split" : "");                                                \
+        if (a.split)                                                                           \
+            hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, MINB_, KS_, 8, true>), grid,  \
+                               dim3(512), 0, stream, a);                                       \
+        else                                                                                   \
+            hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, MINB_, KS_>), grid, dim3(512), 0, \
+                               stream, a);                                                     \
     } while (0)
 #define OPK3_LAUNCH16(BM_, BN_, HR_, TAPU_, KS_)                                                \
     do {                                                                                       \
-        note_launch("conv3_kernel<%d,%d,%d,%d,1,%d,16>", BM_, BN_, HR_, TAPU_, KS_);           \
-        hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, 1, KS_, 16>), grid, dim3(1024), 0, \
-                           stream, a);                                                         \
+        note_launch("conv3_kernel<%d,%d,%d,%d,1,%d,16%s>", BM_, BN_, HR_, TAPU_, KS_,          \
+                    a.split ? ",split" : "");                                                  \
+        if (a.split)                                                                           \
+            hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, 1, KS_, 16, true>), grid,     \
+                               dim3(1024), 0, stream, a);                                      \
+        else                                                                                   \
+            hipLaunchKernelGGL((conv3_kernel<BM_, BN_, HR_, TAPU_, 1, KS_, 16>), grid, dim3(1024), 0, \
+                               stream, a);                                                     \
     } while (0)
     if (ks == 7) {
         if (s.bn == 64) OPK3_LAUNCH(256, 64, 1024, 1, 1, 7);

@@ -55,7 +55,96 @@ __global__ __launch_bounds__(256) void maxpool2_kernel(uint16_t* __restrict__ ou
     *reinterpret_cast<uint4*>(out + opos * C + g * 8) = m;
 }
 
+// split precision: per channel the (hi, lo) pair of the pixel with the largest hi + lo (the
+// first on ties, as Caffe's ordered `>`); hi + lo of an fp16 pair is exact in fp32
+__global__ __launch_bounds__(256) void maxpool2_split_kernel(uint16_t* __restrict__ out,
+                                                             uint16_t* __restrict__ out_lo,
+                                                             const uint16_t* __restrict__ in,
+                                                             const uint16_t* __restrict__ in_lo,
+                                                             int frames, int H, int W, int C, int OH,
+                                                             int OW, int B)
+{
+    const int c8 = C / 8;
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t total = (size_t)frames * OH * OW * c8;
+    if (idx >= total) return;
+    const int g = (int)(idx % c8);
+    const int ox = (int)((idx / c8) % OW);
+    const int oy = (int)((idx / ((size_t)c8 * OW)) % OH);
+    const int f = (int)(idx / ((size_t)c8 * OW * OH));
+    const int y0 = 2 * oy, x0 = 2 * ox;
+    const int y1 = min(y0 + 2, H), x1 = min(x0 + 2, W);
+    uint16_t mh[8], ml[8];
+    float mv[8];
+    bool first = true;
+    for (int y = y0; y < y1; ++y)
+        for (int x = x0; x < x1; ++x) {
+            const size_t pos = ((size_t)f * (H + 2 * B) + y + B) * (W + 2 * B) + x + B;
+            const uint4 vh = *reinterpret_cast<const uint4*>(in + pos * C + g * 8);
+            const uint4 vl = *reinterpret_cast<const uint4*>(in_lo + pos * C + g * 8);
+            const uint16_t* h = reinterpret_cast<const uint16_t*>(&vh);
+            const uint16_t* l = reinterpret_cast<const uint16_t*>(&vl);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const float v = (float)__builtin_bit_cast(_Float16, h[e]) + (float)__builtin_bit_cast(_Float16, l[e]);
+                if (first || v > mv[e]) {
+                    mv[e] = v;
+                    mh[e] = h[e];
+                    ml[e] = l[e];
+                }
+            }
+            first = false;
+        }
+    const size_t opos = ((size_t)f * (OH + 2 * B) + oy + B) * (OW + 2 * B) + ox + B;
+    *reinterpret_cast<uint4*>(out + opos * C + g * 8) = *reinterpret_cast<const uint4*>(mh);
+    *reinterpret_cast<uint4*>(out_lo + opos * C + g * 8) = *reinterpret_cast<const uint4*>(ml);
+}
+
+// split precision, the first conv's input (see conv.h launch_image_split): one lane per pixel
+__global__ __launch_bounds__(256) void image_split_kernel(uint16_t* __restrict__ hi,
+                                                          uint16_t* __restrict__ lo, int cs,
+                                                          const float* __restrict__ img, int frames,
+                                                          int H, int W, int B)
+{
+    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= (size_t)frames * H * W) return;
+    const int x = (int)(idx % W), y = (int)((idx / W) % H), f = (int)(idx / ((size_t)W * H));
+    const size_t pos = ((size_t)f * (H + 2 * B) + y + B) * (W + 2 * B) + x + B;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        const float v = img[(((size_t)f * 3 + c) * H + y) * W + x];
+        const _Float16 h = (_Float16)v;
+        const _Float16 l = (_Float16)(v - (float)h);
+        hi[pos * cs + c] = __builtin_bit_cast(uint16_t, h);
+        lo[pos * cs + c] = __builtin_bit_cast(uint16_t, l);
+    }
+}
+
 }  // namespace
+
+void launch_maxpool2_split(uint16_t* out, uint16_t* out_lo, const uint16_t* in, const uint16_t* in_lo,
+                           int frames, int H, int W, int C, int OH, int OW, hipStream_t stream,
+                           int border)
+{
+    OPK_CHECK_ARG(border >= 1, "border >= 1");
+    OPK_CHECK_ARG(C % 8 == 0, "pool channels must be a multiple of 8");
+    const size_t total = (size_t)frames * OH * OW * (C / 8);
+    note_launch("maxpool2_split_kernel");
+    hipLaunchKernelGGL(maxpool2_split_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       stream, out, out_lo, in, in_lo, frames, H, W, C, OH, OW, border);
+    OPK_LAUNCH_CHECK();
+}
+
+void launch_image_split(uint16_t* hi, uint16_t* lo, int cs, const float* image, int frames, int H,
+                        int W, int border, hipStream_t stream)
+{
+    OPK_CHECK_ARG(cs >= 3 && border >= 1 && frames > 0 && H > 0 && W > 0, "image split: sizes");
+    const size_t total = (size_t)frames * H * W;
+    note_launch("image_split_kernel");
+    hipLaunchKernelGGL(image_split_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
+                       stream, hi, lo, cs, image, frames, H, W, border);
+    OPK_LAUNCH_CHECK();
+}
 
 void launch_maxpool2(uint16_t* out, const uint16_t* in, int frames, int H, int W, int C, int OH,
                      int OW, hipStream_t stream, int border)

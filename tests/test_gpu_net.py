@@ -37,7 +37,7 @@ def conv(name, bottom, cout, k, act=None):
     return out
 
 
-def run_graph(ctx, layers, x, seed=0):
+def run_graph(ctx, layers, x, seed=0, precision=None):
     text = prototxt.emit(layers)
     graph = prototxt.parse(text)
     params = synth.he_weights(graph, seed=seed)
@@ -47,6 +47,8 @@ def run_graph(ctx, layers, x, seed=0):
     try:
         net = Net(ctx, path)
         net.set_params(params)
+        if precision is not None:
+            net.set_precision(precision)
         net.forward(torch.from_numpy(x).cuda())
         got = net.output_numpy()
         net.close()
@@ -465,3 +467,64 @@ def test_prelu_slopes_outside_unit_interval(ctx):
     print("PReLU slopes in [-0.5, 1.5]: rel-L2 %.3e" % err)
     assert err < SMALL_TOL and ch_ok(outs[0], ref)
     np.testing.assert_array_equal(outs[0], outs[1])
+
+
+# ---- split precision (opk_net_set_precision OPK_PRECISION_SPLIT) --------------------------------
+# Every weight and activation an fp16 hi/lo pair, three MFMA passes per conv: the products are exact
+# in fp32, so the result differs from the fp32 oracle only by fp32 summation order and the dropped
+# x_lo * w_lo term (~2^-22 relative).  CPU emulation of the contract: rel-L2 6.3e-6
+# for BODY_25 at 368x656 with full-strength heads.
+SPLIT_TOL = 5e-5          # relative L2 of the net output
+SPLIT_CHANNEL_TOL = 5e-4  # relative L2 of any single output channel
+
+
+@pytest.mark.parametrize("n,h,w", [(2, 64, 96), (1, 368, 656)])
+def test_body25_split_precision_vs_oracle(ctx, n, h, w):
+    """BODY_25 in split precision against the fp32 oracle (three orders of magnitude closer than
+    fp16), and back in fp16 precision the net gives a fresh fp16 net's output bit for bit."""
+    from openpose_amd.api import PRECISION_FP16, PRECISION_SPLIT
+    graph = body25.layers()
+    params = synth.he_weights(graph, seed=23, out_scale=1.0)
+    x = np.random.default_rng(24).uniform(-0.5, 0.5, (n, 3, h, w)).astype(np.float32)
+    xd = torch.from_numpy(x).cuda()
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(params)
+    net.forward(xd)
+    fp16 = net.output_numpy()
+    net.set_precision(PRECISION_SPLIT)
+    with dev_switches(LAUNCH_LOG=1):
+        net.forward(xd)
+        kernels = {k for _, k in net.launch_log()}
+    got = net.output_numpy()
+    assert all("split" in k for k in kernels if k.startswith("conv3_kernel")), kernels
+    assert not any(k.startswith(("conv3w", "conv_head", "conv1_fused")) for k in kernels), kernels
+    ref = body25.forward(x, params, graph=graph)
+    err, err16 = rel_l2(got, ref), rel_l2(fp16, ref)
+    ch = channel_errors(got, ref)
+    print("BODY_25 %dx%dx%d split precision rel-L2 %.3e (fp16 %.3e), worst channel %.3e"
+          % (n, h, w, err, err16, ch.max()))
+    assert err < SPLIT_TOL and ch.max() < SPLIT_CHANNEL_TOL
+    assert err < err16 / 20
+    net.set_precision(PRECISION_FP16)
+    net.forward(xd)
+    np.testing.assert_array_equal(net.output_numpy(), fp16)
+
+
+def test_split_precision_blobs_and_graphs(ctx):
+    """Split precision on the other graph shapes the planner meets -- dense block + concat + 2x2 pool
+    (pooled pairs), 7x7 CPM stages, 1x1 heads into a concat output -- against the fp32 oracle; and a
+    named intermediate blob (caffe::Net::blob_by_name) reads back as hi + lo."""
+    from openpose_amd.api import PRECISION_SPLIT
+    x = np.random.default_rng(25).uniform(-0.5, 0.5, (2, 3, 64, 96)).astype(np.float32)
+    for layers, seed in ((cpm_stage_graph(True), 5), (cpm_stage_graph(False), 6)):
+        got, ref = run_graph(ctx, layers, x, seed=seed, precision=PRECISION_SPLIT)
+        assert got.shape == ref.shape and rel_l2(got, ref) < SPLIT_TOL, rel_l2(got, ref)
+    graph = body25.layers()
+    params = synth.he_weights(graph, seed=26)
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(params)
+    net.set_precision(PRECISION_SPLIT)
+    net.forward(torch.from_numpy(x).cuda())
+    blob = net.blob("pool2_stage1")
+    ref = body25.forward(x, params, graph=graph, stop_at="pool2_stage1")
+    assert blob.shape == ref.shape and rel_l2(blob, ref) < SPLIT_TOL, rel_l2(blob, ref)

@@ -144,23 +144,18 @@ UNSCALED_PEAKS_WITHIN_1PX = 0.96
 UNSCALED_PEOPLE_DELTA = 0.03      # |people - fp32 people| / fp32 people
 
 
-def test_end_to_end_unscaled_heads(ctx, record_property):
-    """Full-strength heads (out_scale 1, no overlay) at 656x368, two frames.
-
-    (1) post-processing isolated: the oracle's resize -> NMS -> connector run on the GPU's OWN net
-        output must give the GPU pipeline's peaks and keypoints bit for bit;
-    (2) fp16-vs-fp32 CNN drift, measured and bounded: the same chain on the fp32 oracle net
-        output; the fraction of fp32 NMS peaks (nmsCpu's integer pixels, oracle/parity.py) the GPU
-        finds at the identical pixel and within 1 heat-map pixel, the largest refined-peak and
-        keypoint shifts and the people counts are printed at the end of the run (conftest:
-        report_*) and checked against the UNSCALED_* bounds above.
-    poseExtractorCaffe.cpp:246-333 is the chain both sides follow."""
+def _unscaled_parity(ctx, precision=None):
+    """Full-strength heads (out_scale 1, no overlay) at 656x368, two frames: (1) post-processing
+    isolated, bit-exact; (2) the CNN's drift against the fp32 oracle through the whole chain.
+    Returns the measured quantities."""
     from oracle import parity
     graph = body25.layers()
     params = synth.he_weights(graph, seed=31, out_scale=1.0)
     x = np.random.default_rng(32).uniform(-0.5, 0.5, (2, 3, 368, 656)).astype(np.float32)
     net = Net(ctx, "builtin:BODY_25")
     net.set_params(params)
+    if precision is not None:
+        net.set_precision(precision)
     pose = PoseExtractor(ctx, net)
     pose.forward(_dev(x), (1280, 720))
     s = pose.scale_net_to_output()
@@ -200,23 +195,55 @@ def test_end_to_end_unscaled_heads(ctx, record_property):
         stats["kshift"] = max(stats["kshift"], kshift)
         stats["people"] += len(kp)
         stats["people32"] += len(rk32)
-    err = (stats["num"] / stats["den"]) ** 0.5
     total = stats["fp32_peaks"]
-    same, near = stats["same"] / total, stats["near"] / total
-    delta = abs(stats["people"] - stats["people32"]) / max(stats["people32"], 1)
-    for k, v in (("net_rel_l2", round(err, 6)), ("fp32_peaks", total),
-                 ("peak_index_identical", round(same, 5)), ("peaks_within_1px", round(near, 5)),
-                 ("max_refined_peak_shift_px", round(stats["shift"], 4)),
-                 ("max_keypoint_shift_px", round(stats["kshift"], 4)),
-                 ("people_gpu_fp32", (stats["people"], stats["people32"])),
-                 ("people_identical_1e-3", round(stats["exact"] / max(stats["people32"], 1), 4))):
-        record_property("report_" + k, v)
-    print("unscaled heads: rel-L2 %.2e, %d fp32 peaks, %.4f identical, %.4f within 1 px (max "
-          "shift %.3f px), people %d vs %d" % (err, total, same, near, stats["shift"],
-                                               stats["people"], stats["people32"]))
-    assert err < UNSCALED_REL_L2
-    assert total > 0 and same >= UNSCALED_PEAKS_IDENTICAL and near >= UNSCALED_PEAKS_WITHIN_1PX
-    assert delta <= UNSCALED_PEOPLE_DELTA
+    return {"net_rel_l2": (stats["num"] / stats["den"]) ** 0.5, "fp32_peaks": total,
+            "peak_index_identical": stats["same"] / total, "peaks_within_1px": stats["near"] / total,
+            "max_refined_peak_shift_px": stats["shift"], "max_keypoint_shift_px": stats["kshift"],
+            "people_gpu_fp32": (stats["people"], stats["people32"]),
+            "people_identical_1e-3": stats["exact"] / max(stats["people32"], 1)}
+
+
+def _report(record_property, m, tag=""):
+    for k, v in m.items():
+        record_property("report_" + tag + k, round(v, 6) if isinstance(v, float) else v)
+
+
+def test_end_to_end_unscaled_heads(ctx, record_property):
+    """Full-strength heads (out_scale 1, no overlay) at 656x368, two frames, fp16 precision.
+
+    (1) post-processing isolated: the oracle's resize -> NMS -> connector run on the GPU's OWN net
+        output must give the GPU pipeline's peaks and keypoints bit for bit;
+    (2) fp16-vs-fp32 CNN drift, measured and bounded: the same chain on the fp32 oracle net
+        output; the fraction of fp32 NMS peaks (nmsCpu's integer pixels, oracle/parity.py) the GPU
+        finds at the identical pixel and within 1 heat-map pixel, the largest refined-peak and
+        keypoint shifts and the people counts are printed at the end of the run (conftest:
+        report_*) and checked against the UNSCALED_* bounds above.
+    poseExtractorCaffe.cpp:246-333 is the chain both sides follow."""
+    m = _unscaled_parity(ctx)
+    _report(record_property, m)
+    assert m["net_rel_l2"] < UNSCALED_REL_L2
+    assert m["fp32_peaks"] > 0 and m["peak_index_identical"] >= UNSCALED_PEAKS_IDENTICAL
+    assert m["peaks_within_1px"] >= UNSCALED_PEAKS_WITHIN_1PX
+    p, p32 = m["people_gpu_fp32"]
+    assert abs(p - p32) / max(p32, 1) <= UNSCALED_PEOPLE_DELTA
+
+
+# Split precision (opk_net_set_precision OPK_PRECISION_SPLIT): the same field, the same chain.
+SPLIT_REL_L2 = 5e-5
+SPLIT_PEAKS_IDENTICAL = 0.998
+SPLIT_PEOPLE_IDENTICAL = 0.95   # fp32 people reproduced with every keypoint within 1e-3 net px
+
+
+def test_end_to_end_unscaled_heads_split_precision(ctx, record_property):
+    """The full-strength field of test_end_to_end_unscaled_heads with the net in split precision
+    (fp16 hi/lo pairs, three MFMA passes): the north star's "peak indices bit-exact, keypoints
+    within 1e-3 of the CPU reference" on a CNN-driven field, measured and bounded (SPLIT_*)."""
+    from openpose_amd.api import PRECISION_SPLIT
+    m = _unscaled_parity(ctx, PRECISION_SPLIT)
+    _report(record_property, m, "split_")
+    assert m["net_rel_l2"] < SPLIT_REL_L2
+    assert m["peak_index_identical"] >= SPLIT_PEAKS_IDENTICAL
+    assert m["people_identical_1e-3"] >= SPLIT_PEOPLE_IDENTICAL
 
 
 def test_pose_submit_collect_pipeline(ctx):
