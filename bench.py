@@ -91,6 +91,25 @@ def cpu_share():
     return (min(aff, omp) if omp else aff), aff, omp
 
 
+def cgroup_cpu_quota():
+    """CPUs' worth of time the process's cgroup allows (cpu.max quota / period, cgroup v2; v1's
+    cfs_quota_us / cfs_period_us), or None when unlimited or unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else int(q) / int(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def kernel_src_sha():
     """sha256 over the kernel sources (openpose_amd/csrc/kernels/*): which kernels a committed
     PMC summary was collected with (tools/pmc_round.sh records the same digest)."""
@@ -186,7 +205,14 @@ def cpu_baseline(args, params, frames_np, overlays_np):
     # beside the share's figure
     _, aff, _ = cpu_share()
     full = None
-    if aff > threads:
+    quota = cgroup_cpu_quota()
+    if aff > threads and quota is not None and quota < aff:
+        full = {"skipped": True, "affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                "note": "the process's CPU quota (cgroup cpu.max) is %.1f CPUs: threads beyond it "
+                        "time-share those CPUs (measured once on the 1-GPU box, round 5: 0.046 "
+                        "frames/s on 256 threads against 1.54 on 16, profiles/round5/r5d/bench.log)"
+                        % quota}
+    elif aff > threads:
         tf = time.perf_counter()
         nf = 0
         while True:
@@ -214,7 +240,7 @@ def cpu_baseline(args, params, frames_np, overlays_np):
     el1 = time.perf_counter() - t1
     _, aff, omp = cpu_share()
     return {"value": done / el, "unit": "frames/s", "cores": threads, "kind": "port",
-            "full_affinity": full,
+            "full_affinity": full, "cgroup_cpu_quota": quota,
             "affinity_cpus": aff, "omp_num_threads_env": omp, "host_cpus": os.cpu_count(),
             "cpu_model": cpu_model(),
             "cores_note": "threads = the CPUs in this process's affinity mask, capped by "

@@ -712,6 +712,38 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
     forward_steps(S, input, n, h, w, st);
 }
 
+// conv3 over the frames of a batch in as few launches as its 24-bit position arithmetic allows
+// (the full-resolution layers of a large batch run unfused only in split precision): each launch
+// takes a run of whole frames, its pointers moved to the run's first frame -- the positions just
+// before and after a run are frame borders, zero like the guards of a whole-batch launch.
+static void launch_conv3_frames(const ConvArgs& a, hipStream_t st)
+{
+    const int B = a.border > 0 ? a.border : 1;
+    const int ks = a.ntaps == 49 ? 7 : (a.ntaps == 9 ? 3 : 1);
+    const Conv3Shape s3 = conv3_shape(a.frames, a.H, a.W, a.cout, ks, B);
+    const long per_frame = (long)s3.nstrips * (a.H + 2 * B) * (s3.sw + 2 * B);
+    const long room = (1L << 24) - s3.bm - (long)(ks - 1) * (s3.sw + 2 * B + 1) - 1;
+    const int run = (int)std::max(1L, std::min<long>(a.frames, room / per_frame));
+    if (run >= a.frames) {
+        launch_conv3(a, st);
+        return;
+    }
+    const size_t frame_pos = (size_t)(a.H + 2 * B) * (a.W + 2 * B);   // padded image positions
+    for (int f0 = 0; f0 < a.frames; f0 += run) {
+        ConvArgs b = a;
+        b.frames = std::min(run, a.frames - f0);
+        b.M = b.frames * a.H * (a.W + 2 * B);
+        b.in = a.in + f0 * frame_pos * a.in_cs;
+        if (a.in_lo) b.in_lo = a.in_lo + f0 * frame_pos * a.in_cs;
+        for (int d = 0; d < a.ndst; ++d) {
+            b.dst[d] = a.dst[d] + f0 * frame_pos * a.dst_cs[d];
+            if (a.dst_lo[d]) b.dst_lo[d] = a.dst_lo[d] + f0 * frame_pos * a.dst_cs[d];
+        }
+        if (a.out32) b.out32 = a.out32 + (size_t)f0 * a.out32_c * a.H * a.W;
+        launch_conv3(b, st);
+    }
+}
+
 void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w, hipStream_t st)
 {
     LaunchLog* log = launch_log();
@@ -801,7 +833,7 @@ void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w
                 ConvArgs a3 = a;
                 a3.actmax = a.actmax && c.slope01;
                 if (a3.out32) a3.out32 = out32;
-                launch_conv3(a3, st);
+                launch_conv3_frames(a3, st);
             }
         } else {
             if (S.poolfused[s.idx]) continue;   // ran in its conv's epilogue

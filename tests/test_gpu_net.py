@@ -528,3 +528,21 @@ def test_split_precision_blobs_and_graphs(ctx):
     blob = net.blob("pool2_stage1")
     ref = body25.forward(x, params, graph=graph, stop_at="pool2_stage1")
     assert blob.shape == ref.shape and rel_l2(blob, ref) < SPLIT_TOL, rel_l2(blob, ref)
+
+
+def test_split_precision_large_batch_frame_runs(ctx):
+    """Split precision at a batch whose full-resolution layers exceed one conv3 launch's 24-bit
+    position range (70 x 370 x 658 padded positions): the convs run in frame runs
+    (launch_conv3_frames), and every frame's output equals the same frame forwarded alone, bit for
+    bit (an output's MFMA accumulation order does not depend on the batch)."""
+    from openpose_amd.api import PRECISION_SPLIT
+    n = 70
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(synth.he_weights(net.convs(), seed=27))
+    net.set_precision(PRECISION_SPLIT)
+    x = np.random.default_rng(28).uniform(-0.5, 0.5, (n, 3, 368, 656)).astype(np.float32)
+    net.forward(torch.from_numpy(x).cuda())
+    got = net.output_numpy()
+    for f in (0, n // 2, n - 1):
+        net.forward(torch.from_numpy(x[f:f + 1]).cuda())
+        np.testing.assert_array_equal(got[f], net.output_numpy()[0])
