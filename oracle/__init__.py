@@ -99,6 +99,7 @@ def ref_lib():
                                       _f, _f, _f, _i]
         R.ref_connect_gpu_assembly.argtypes = [_f32p, _f32p, _i, _f32p, _f32p, _i, _i, _i, _f, _f,
                                                _i]
+        R.ref_gpu_face_merge_reached.argtypes = [_f32p, _f32p, _i, _i, _i, _f, _i]
         _REF = R
     return _REF
 
@@ -219,10 +220,20 @@ def pose_tables():
         return json.load(f)
 
 
+def face_merge_reached(pair_scores, peaks, table, **params):
+    """Whether the reference's removePeopleBelowThresholdsAndFillFaces runs its BODY_135
+    face-fragment merge on this input (oracle/_ref)."""
+    p = _connect_args(params)
+    return bool(ref_lib().ref_gpu_face_merge_reached(
+        np.ascontiguousarray(pair_scores, np.float32), np.ascontiguousarray(peaks, np.float32),
+        table["id"], peaks.shape[1] - 1, p["min_subset_cnt"], p["min_subset_score"],
+        int(p["maximize_positives"])))
+
+
 def connect_gpu_semantics(pair_scores, peaks, table, use_reference=False, **params):
     """connectBodyPartsGpu host assembly for any model (table: a pose_tables() entry).  With
-    use_reference the reference's own pafVectorIntoPeopleVector / removePeople... run (None when
-    the input would reach getKeypointsRoi, which needs OpenCV)."""
+    use_reference the reference's own pafVectorIntoPeopleVector / removePeople... run (its
+    face-fragment merge with the restated getKeypointsRoi, oracle/ref_driver.cpp)."""
     p = _connect_args(params)
     pair_scores = np.ascontiguousarray(pair_scores, np.float32)
     peaks = np.ascontiguousarray(peaks, np.float32)

@@ -13,12 +13,14 @@
 // reference; the reference files are compiled where they lie.
 //
 // Not built (they need OpenCV, absent from the image): core/array.cpp (op::Array<T>) and
-// utilities/keypoint.cpp (getKeypointsRoi).  The library is linked with those symbols left
-// unresolved; the entry points below only reach code paths that never call them for the
-// BODY_25 / COCO / MPI models (Array<T> is touched only by the precomputed-score branch and by
-// peopleVectorToPeopleArray, which this driver does not call; getKeypointsRoi only for >=135
-// parts).  The final people -> array step (bodyPartConnectorBase.cpp:886-934) is a 10-line
-// copy-out done here on the returned std::vector.
+// utilities/keypoint.cpp.  The library is linked with those symbols left unresolved; the entry
+// points below never reach op::Array<T> (touched only by the precomputed-score branch and by
+// peopleVectorToPeopleArray, which this driver does not call).  The one keypoint.cpp function the
+// connector calls -- getKeypointsRoi(Rectangle, Rectangle), for the BODY_135 face-fragment merge
+// (removePeopleBelowThresholdsAndFillFaces, bodyPartConnectorBase.cpp:799-866) -- is plain
+// arithmetic, restated below (as pafPtrIntoVector's loop is further down), so that branch runs the
+// reference's own code around it.  The final people -> array step (bodyPartConnectorBase.cpp:
+// 886-934) is a 10-line copy-out done here on the returned std::vector.
 #include <algorithm>
 #include <cstring>
 #include <functional>
@@ -27,6 +29,36 @@
 #include <openpose/net/bodyPartConnectorBase.hpp>
 #include <openpose/pose/poseParameters.hpp>
 #include <openpose/utilities/fastMath.hpp>
+#include <openpose/utilities/keypoint.hpp>
+
+namespace op
+{
+// getKeypointsRoi(Rectangle, Rectangle) (utilities/keypoint.cpp:586-632), restated: both rectangles
+// shifted so that neither has a negative corner (the smallest negative x / y, or 0), then the
+// intersection area over the union area in float; 0 when they do not overlap.  Subtracting a zero
+// shift changes no value, so the shift is applied unconditionally.
+template <typename T>
+float getKeypointsRoi(const Rectangle<T>& a, const Rectangle<T>& b)
+{
+    const T sx = std::min(std::min(T{0}, a.x), b.x);
+    const T sy = std::min(std::min(T{0}, a.y), b.y);
+    Rectangle<T> ra = a, rb = b;
+    ra.x -= sx;
+    rb.x -= sx;
+    ra.y -= sy;
+    rb.y -= sy;
+    const T left = fastMax(ra.x, rb.x), top = fastMax(ra.y, rb.y);
+    const T right = fastMin(ra.x + ra.width, rb.x + rb.width);
+    const T bottom = fastMin(ra.y + ra.height, rb.y + rb.height);
+    if (!(left < right && top < bottom))
+        return 0.f;
+    const Rectangle<T> overlap{left, top, right - left, bottom - top};
+    const auto areaA = ra.area(), areaB = rb.area(), inter = overlap.area();
+    return float(inter) / float(areaA + areaB - inter);
+}
+template float getKeypointsRoi(const Rectangle<float>&, const Rectangle<float>&);
+template float getKeypointsRoi(const Rectangle<double>&, const Rectangle<double>&);
+}
 
 extern "C" int ref_connect_cpu(float* kp, float* ks, int max_people, const float* heat,
                                const float* peaks, int pose_model, int W, int H, int max_peaks,
@@ -106,17 +138,12 @@ extern "C" int ref_pose_keys(int pose_model, int* keys)
     return 0;
 }
 
-// connectBodyPartsGpu's host half (bodyPartConnectorBase.cu:147-250) on host pair scores
-// [npairs][max_peaks][max_peaks]: the reference's pafVectorIntoPeopleVector,
-// removePeopleBelowThresholdsAndFillFaces and the people -> array copy-out.  pafPtrIntoVector takes
-// an op::Array (OpenCV-dependent array.cpp, not built), so its loop -- collect (total, paf, q, i, j)
-// for score > 1e-6 with total = paf + 0.1 sA + 0.1 sB, sort descending -- is restated here.
-// Returns -2 when the call would reach getKeypointsRoi (keypoint.cpp, not built): a >= 135-part
-// model with face-only fragments next to valid people; callers skip such inputs.
-extern "C" int ref_connect_gpu_assembly(float* kp, float* ks, int max_people,
-                                        const float* pair_scores, const float* peaks,
-                                        int pose_model, int max_peaks, int min_cnt,
-                                        float min_score, float scale, int maxpos)
+// pafPtrIntoVector's loop (it takes an op::Array: OpenCV-dependent array.cpp, not built), restated:
+// collect (total, paf, q, i, j) for score > 1e-6 with total = paf + 0.1 sA + 0.1 sB, sort
+// descending, then the reference's pafVectorIntoPeopleVector
+static std::vector<std::pair<std::vector<int>, float>> gpu_people(const float* pair_scores,
+                                                                  const float* peaks, int pose_model,
+                                                                  int max_peaks)
 {
     const auto model = (op::PoseModel)pose_model;
     const auto& pairs = op::getPosePartPairs(model);
@@ -138,35 +165,60 @@ extern "C" int ref_connect_gpu_assembly(float* kp, float* ks, int max_people,
             }
     }
     std::sort(conn.begin(), conn.end(), std::greater<std::tuple<double, double, int, int, int>>());
-    auto people = op::pafVectorIntoPeopleVector<float>(conn, peaks, max_peaks, pairs, nparts);
-    if (nparts >= 135) {   // would removePeople... call getKeypointsRoi? (its counting, :740-798)
-        auto disc = [](int& c, const std::vector<int>& r, int a, int b, int minimum) {
-            int k = 0;
-            for (int i = a; i < b; ++i) k += r[i] > 0;
-            if (k > minimum) c += minimum - k;
-        };
-        std::function<bool(bool)> reaches = [&](bool mp) {
-            int valid = 0, face_valid = 0, face_invalid = 0;
-            for (const auto& p : people) {
-                int c = p.first.back();
-                const int before = c;
-                disc(c, p.first, 65, 135, 1);
-                if (c == 1) { ++face_invalid; continue; }
-                if (c != before) ++face_valid;
-                disc(c, p.first, 45, 65, 1);
-                disc(c, p.first, 25, 45, 1);
-                if (!mp) {
-                    const int b2 = c;
-                    disc(c, p.first, 19, 25, 0);
-                    if (c != b2 && c <= 4) continue;
-                }
-                if (c >= min_cnt && (p.second / c) >= min_score) ++valid;
+    return op::pafVectorIntoPeopleVector<float>(conn, peaks, max_peaks, pairs, nparts);
+}
+
+// 1 when removePeopleBelowThresholdsAndFillFaces will run its face-fragment merge (and so call
+// getKeypointsRoi) on this input: a >= 135-part model with face-only fragments next to valid
+// people with faces (its counting, bodyPartConnectorBase.cpp:740-798) -- the fixture generator
+// checks that the BODY_135 face cases exercise that branch
+extern "C" int ref_gpu_face_merge_reached(const float* pair_scores, const float* peaks,
+                                          int pose_model, int max_peaks, int min_cnt,
+                                          float min_score, int maxpos)
+{
+    const auto people = gpu_people(pair_scores, peaks, pose_model, max_peaks);
+    if (op::getPoseNumberBodyParts((op::PoseModel)pose_model) < 135) return 0;
+    auto disc = [](int& c, const std::vector<int>& r, int a, int b, int minimum) {
+        int k = 0;
+        for (int i = a; i < b; ++i) k += r[i] > 0;
+        if (k > minimum) c += minimum - k;
+    };
+    std::function<bool(bool)> reaches = [&](bool mp) {
+        int valid = 0, face_valid = 0, face_invalid = 0;
+        for (const auto& p : people) {
+            int c = p.first.back();
+            const int before = c;
+            disc(c, p.first, 65, 135, 1);
+            if (c == 1) { ++face_invalid; continue; }
+            if (c != before) ++face_valid;
+            disc(c, p.first, 45, 65, 1);
+            disc(c, p.first, 25, 45, 1);
+            if (!mp) {
+                const int b2 = c;
+                disc(c, p.first, 19, 25, 0);
+                if (c != b2 && c <= 4) continue;
             }
-            if (valid > 0) return face_invalid > 0 && face_valid > 0;
-            return !mp && reaches(true);
-        };
-        if (reaches(maxpos != 0)) return -2;
-    }
+            if (c >= min_cnt && (p.second / c) >= min_score) ++valid;
+        }
+        if (valid > 0) return face_invalid > 0 && face_valid > 0;
+        return !mp && reaches(true);
+    };
+    return reaches(maxpos != 0) ? 1 : 0;
+}
+
+// connectBodyPartsGpu's host half (bodyPartConnectorBase.cu:147-250) on host pair scores
+// [npairs][max_peaks][max_peaks]: the restated pafPtrIntoVector loop, then the reference's
+// pafVectorIntoPeopleVector, removePeopleBelowThresholdsAndFillFaces (face-fragment merge
+// included) and the people -> array copy-out
+extern "C" int ref_connect_gpu_assembly(float* kp, float* ks, int max_people,
+                                        const float* pair_scores, const float* peaks,
+                                        int pose_model, int max_peaks, int min_cnt,
+                                        float min_score, float scale, int maxpos)
+{
+    const auto model = (op::PoseModel)pose_model;
+    const auto nparts = op::getPoseNumberBodyParts(model);
+    const auto npairs = (unsigned)(op::getPosePartPairs(model).size() / 2);
+    auto people = gpu_people(pair_scores, peaks, pose_model, max_peaks);
     std::vector<int> keep;
     int npeople = 0;
     op::removePeopleBelowThresholdsAndFillFaces<float>(keep, npeople, people, nparts, min_cnt,

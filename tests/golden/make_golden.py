@@ -64,10 +64,10 @@ def make_connector():
 
 # connectBodyPartsGpu host assembly (GPU semantics), any model: (name, model, kind, n, seed, h, w,
 # maximize_positives).  kind "people": synthetic field -> oracle NMS -> oracle pair scores;
-# "random": random peaks and random pair scores (many merges and fragments).  BODY_135 cases blank
-# the face parts ("_noface"): with face-only fragments next to valid people the reference calls
-# getKeypointsRoi (utilities/keypoint.cpp, needs OpenCV: not built), so the face-fragment merge is
-# checked oracle-vs-product only (tests/test_connector_gpu.py, parity unpinned).
+# "random": random peaks and random pair scores (many merges and fragments).  The "_noface"
+# BODY_135 cases blank the face parts; the "_face" cases keep them and are checked to reach the
+# reference's face-fragment merge (removePeopleBelowThresholdsAndFillFaces with the restated
+# getKeypointsRoi, oracle/ref_driver.cpp; round 5).
 GPU_CONNECTOR_CASES = [
     ("b25_p5", 0, "people", 5, 111, 368, 656, False),
     ("b25_p20", 0, "people", 20, 112, 368, 656, False),
@@ -77,6 +77,10 @@ GPU_CONNECTOR_CASES = [
     ("b135_p8_maxpos", 14, "people_noface", 8, 116, 368, 656, True),
     ("b135_random", 14, "random_noface", 0, 117, 184, 328, False),
     ("b25b_p6", 13, "people", 6, 118, 184, 328, False),
+    ("b135_p3_face", 14, "people", 3, 131, 184, 328, False),
+    ("b135_p8_face", 14, "people", 8, 132, 368, 656, False),
+    ("b135_random_face", 14, "random", 0, 133, 184, 328, False),
+    ("b135_random_face_maxpos", 14, "random", 0, 134, 184, 328, True),
 ]
 
 
@@ -131,7 +135,9 @@ def make_connector_gpu():
         pk, ps = gpu_connector_inputs(t, kind, n, seed, h, w)
         res = oracle.connect_gpu_semantics(ps, pk, t, use_reference=True, scale=1.959128,
                                            maximize_positives=maxpos)
-        assert res is not None, name + ": reaches getKeypointsRoi (needs OpenCV); pick another seed"
+        if name.endswith(("_face", "_face_maxpos")):
+            assert oracle.face_merge_reached(ps, pk, t, maximize_positives=maxpos), \
+                name + ": does not reach the face-fragment merge; pick another seed"
         idx, val = sparse_scores(ps)
         np.savez_compressed(os.path.join(HERE, "gpuconn_%s.npz" % name), model=model, kind=kind,
                             n_people=n, seed=seed, h=h, w=w, maximize_positives=maxpos,

@@ -4,8 +4,10 @@ tables of every model.
 gpuconn_*.npz hold the REFERENCE's own outputs (pafVectorIntoPeopleVector,
 removePeopleBelowThresholdsAndFillFaces compiled from /root/reference into oracle/_ref;
 tests/golden/make_golden.py); pose_tables.json is the reference's poseParameters.cpp run here
-(tools/gen_pose_tables.py).  The BODY_135 face-fragment merge (getKeypointsRoi, OpenCV-dependent,
-not buildable here) is checked oracle-vs-product only: parity unpinned for that branch.
+(tools/gen_pose_tables.py).  The BODY_135 face-fragment merge runs the reference's code too, with
+its one helper from the OpenCV-dependent keypoint.cpp -- getKeypointsRoi(Rectangle, Rectangle),
+plain arithmetic -- restated in oracle/ref_driver.cpp (round 5); the gpuconn_b135_*_face fixtures
+reach that branch (make_golden.py checks it).
 """
 import glob
 import os
@@ -62,7 +64,8 @@ def test_gpu_assembly_product_matches_reference_fixture(path):
 
 @pytest.mark.parametrize("kind,n,seed", [("people", 3, 131), ("people", 8, 132), ("random", 0, 133)])
 def test_body135_face_merge_product_matches_oracle(kind, n, seed):
-    """Inputs with face-only fragments (the getKeypointsRoi branch): oracle vs product."""
+    """Inputs with face-only fragments (the getKeypointsRoi branch): product vs oracle, and vs the
+    reference compiled here when it is (build container)."""
     t = oracle.pose_tables()[BODY_135]
     pk, ps = gpu_connector_inputs(t, kind, n, seed, 184, 328)
     for maxpos in (False, True):
@@ -71,6 +74,35 @@ def test_body135_face_merge_product_matches_oracle(kind, n, seed):
                                   maximize_positives=maxpos, semantics=CONNECT_GPU)
         np.testing.assert_array_equal(got[0], ref[0])
         np.testing.assert_array_equal(got[1], ref[1])
+        if oracle.ref_lib() is not None:
+            assert oracle.face_merge_reached(ps, pk, t, maximize_positives=maxpos)
+            live = oracle.connect_gpu_semantics(ps, pk, t, use_reference=True, scale=1.959128,
+                                                maximize_positives=maxpos)
+            np.testing.assert_array_equal(got[0], live[0])
+            np.testing.assert_array_equal(got[1], live[1])
+
+
+@pytest.mark.skipif(oracle.ref_lib() is None, reason="needs /root/reference (oracle/_ref)")
+def test_body135_face_merge_random_vs_reference_live():
+    """80 BODY_135 inputs with face peaks (people fields and random scores, both
+    maximize_positives settings), nearly all reaching the face-fragment merge: product and oracle
+    equal the reference bit for bit."""
+    t = oracle.pose_tables()[BODY_135]
+    reached = 0
+    for kind, n in (("people", 3), ("people", 8), ("random", 0), ("random", 0)):
+        for seed in range(10):
+            pk, ps = gpu_connector_inputs(t, kind, n, 6000 + 37 * seed + n, 184, 328)
+            for maxpos in (False, True):
+                reached += oracle.face_merge_reached(ps, pk, t, maximize_positives=maxpos)
+                live = oracle.connect_gpu_semantics(ps, pk, t, use_reference=True, scale=1.5,
+                                                    maximize_positives=maxpos)
+                got = api.assemble_people(ps, pk, pose_model=BODY_135, scale=1.5,
+                                          maximize_positives=maxpos, semantics=CONNECT_GPU)
+                orc = oracle.connect_gpu_semantics(ps, pk, t, scale=1.5, maximize_positives=maxpos)
+                for a in (got, orc):
+                    np.testing.assert_array_equal(a[0], live[0])
+                    np.testing.assert_array_equal(a[1], live[1])
+    assert reached >= 60
 
 
 @pytest.mark.skipif(oracle.ref_lib() is None, reason="needs /root/reference (oracle/_ref)")
@@ -81,11 +113,8 @@ def test_gpu_assembly_random_vs_reference_live(model):
     t = oracle.pose_tables()[model]
     checked = 0
     for seed in range(20):
-        pk, ps = gpu_connector_inputs(t, "random_noface" if t["parts"] >= 135 else "random", 0,
-                                      1000 + seed, 184, 328)
+        pk, ps = gpu_connector_inputs(t, "random", 0, 1000 + seed, 184, 328)
         ref = oracle.connect_gpu_semantics(ps, pk, t, use_reference=True, scale=1.5)
-        if ref is None:
-            continue
         got = api.assemble_people(ps, pk, pose_model=model, scale=1.5, semantics=CONNECT_GPU)
         orc = oracle.connect_gpu_semantics(ps, pk, t, scale=1.5)
         for a in (got, orc):
