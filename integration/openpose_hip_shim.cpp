@@ -25,6 +25,7 @@
 // everything else follows the CPU path.  The double instantiations run the float
 // kernels between device conversions (AsFloat below).  Errors come back through op::error, the
 // reference's convention (errorAndLog.cpp:158-233).  See INTEGRATION.md for the build lines.
+#include <cstdlib>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -97,6 +98,27 @@ namespace op
         {
             if (rc != OPK_OK)
                 error(std::string{"libopk_hip: "} + opk_last_error(), line, function, __FILE__);
+        }
+
+        // opk_net_create + the arithmetic the deployment asks for: OPENPOSE_HIP_PRECISION=split runs
+        // every net of the process in OPK_PRECISION_SPLIT (fp16 hi/lo pairs, ~fp32 results at ~3.4x
+        // the CNN time); unset or "fp16" keeps the default.  Any other value is an error, not a
+        // silent default.
+        opk_net* createNet(opk_ctx* ctx, const std::string& proto, const std::string& model)
+        {
+            opk_net* net = nullptr;
+            check(opk_net_create(ctx, proto.c_str(), model.c_str(), &net), __LINE__, __FUNCTION__);
+            const char* env = std::getenv("OPENPOSE_HIP_PRECISION");
+            const std::string want = env ? env : "fp16";
+            if (want != "fp16" && want != "split")
+            {
+                opk_net_destroy(net);
+                error("OPENPOSE_HIP_PRECISION must be fp16 or split, not '" + want + "'.", __LINE__,
+                      __FUNCTION__, __FILE__);
+            }
+            if (want == "split")
+                check(opk_net_set_precision(net, OPK_PRECISION_SPLIT), __LINE__, __FUNCTION__);
+            return net;
         }
 
         // Conversion buffers of the double instantiations, kept per thread and reused in stream
@@ -358,7 +380,7 @@ namespace op
         void initializationOnThread()
         {
             mCtx = opkShimThreadContext(mGpuId);   // binds this thread to the GPU (netCaffe.cpp:169-170)
-            check(opk_net_create(mCtx.get(), mProto.c_str(), mModel.c_str(), &mNet), __LINE__, __FUNCTION__);
+            mNet = createNet(mCtx.get(), mProto, mModel);
         }
 
         void forwardPass(const Array<float>& inputNetData) const
@@ -518,8 +540,7 @@ namespace op
             impl.ctxOwner = opkShimThreadContext(impl.gpuId);   // binds this thread to the GPU (netCaffe.cpp:169-170)
             impl.ctx = impl.ctxOwner.get();
             if (impl.enableNet)
-                check(opk_net_create(impl.ctx, impl.proto.c_str(), impl.model.c_str(), &impl.net), __LINE__,
-                      __FUNCTION__);
+                impl.net = createNet(impl.ctx, impl.proto, impl.model);
             // the connector the reference would run: the CPU path's assembly where its CPU
             // connector exists, connectBodyPartsGpu's for the other models (BODY_135, ...)
             const auto numberBodyParts = (int)getPoseNumberBodyParts(impl.poseModel);
@@ -870,7 +891,7 @@ namespace op
             {
                 ctxOwner = opkShimThreadContext(gpuId);
                 ctx = ctxOwner.get();
-                check(opk_net_create(ctx, proto.c_str(), model.c_str(), &net), __LINE__, __FUNCTION__);
+                net = createNet(ctx, proto, model);
                 check(opk_extractor_create(ctx, net, kind, netSize.x, netSize.y, &ex), __LINE__,
                       __FUNCTION__);
                 check(opk_extractor_set_heatmaps(ex, heatMapScaleMode), __LINE__, __FUNCTION__);

@@ -202,3 +202,48 @@ def test_pose_shim_matches_abi(ctx):
                 np.testing.assert_array_equal(ts, gs)
                 np.testing.assert_array_equal(_read(d, "thread%d_%d_heat.f32" % (t, rep)),
                                               _read(d, "single_heat.f32"))
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(BIN), reason="driver not built (needs the reference headers)")
+def test_pose_shim_split_precision_env(ctx):
+    """OPENPOSE_HIP_PRECISION=split puts every net the drop-in creates into OPK_PRECISION_SPLIT: the
+    makeNetHip output blob and PoseExtractorHip's heat maps / peaks / keypoints equal the C-ABI run
+    with Net.set_precision(PRECISION_SPLIT), bit for bit; an unknown value fails through op::error."""
+    import torch
+    from openpose_amd.api import PRECISION_SPLIT, Net, PoseExtractor
+
+    with tempfile.TemporaryDirectory() as d:
+        path, producer, scales, sizes, xs, field = _inputs(d)
+        np.float32(2.0).tofile(os.path.join(d, "fns_scale.f32"))
+        env = dict(os.environ, OPENPOSE_HIP_PRECISION="split")
+        r = subprocess.run([BIN, d], capture_output=True, text=True, timeout=180, env=env)
+        assert r.returncode == 0 and "pose driver ok" in r.stdout, r.stderr + r.stdout
+
+        net = Net(ctx, "builtin:BODY_25", caffemodel=path)
+        net.set_precision(PRECISION_SPLIT)
+        dev = [torch.from_numpy(x).cuda() for x in xs]
+        pose = PoseExtractor(ctx, net)
+        pose.set_property(0, 0.06)
+        pose.forward(dev[0], producer)
+        kp, sc = pose.keypoints(0)
+        gk, gs, _ = _result(d, "single")
+        np.testing.assert_array_equal(gk, kp)
+        np.testing.assert_array_equal(gs, sc)
+        heat = pose.heatmaps_numpy()
+        np.testing.assert_array_equal(_read(d, "single_heat.f32").reshape(heat.shape[1:]), heat[0])
+        np.testing.assert_array_equal(_read(d, "single_cand.f32").reshape(25, 128, 3),
+                                      pose.peaks_numpy()[0])
+        pose.close()
+        net.forward(dev[0])
+        split_out = net.output_numpy().ravel()
+        np.testing.assert_array_equal(_read(d, "net_out0.f32"), split_out)
+        # and it is the split net, not the fp16 one
+        n16 = Net(ctx, "builtin:BODY_25", caffemodel=path)
+        n16.forward(dev[0])
+        assert not np.array_equal(n16.output_numpy().ravel(), split_out)
+
+        bad = dict(os.environ, OPENPOSE_HIP_PRECISION="fp32")
+        r = subprocess.run([BIN, d], capture_output=True, text=True, timeout=180, env=bad)
+        assert r.returncode != 0 and "OPENPOSE_HIP_PRECISION must be fp16 or split" in r.stderr, \
+            r.stderr + r.stdout
