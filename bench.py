@@ -72,6 +72,10 @@ def parse():
     ap.add_argument("--collective-gather", action="store_true",
                     help="test: at --gpus 1, create the RCCL process group anyway and move the "
                          "records through the collective gather an N-GPU run uses")
+    ap.add_argument("--precision", choices=["fp16", "split"], default="fp16",
+                    help="body25 / multiscale: the net's arithmetic (opk_net_set_precision): fp16 "
+                         "(the product path, the default) or split (fp16 hi/lo pairs, ~fp32 "
+                         "results, three MFMA passes per conv)")
     ap.add_argument("--dev", action="append", default=[], metavar="KEY=VAL",
                     help="kernel-variant switch for A/B runs (opk_dev_set; include/opk.h)")
     return ap.parse_args()
@@ -407,9 +411,9 @@ def _first(*rel):
 # records the commit and kernel-source digest it was collected at, reported beside the numbers
 # read from it): CNN HBM bytes per forward, time-weighted MFMA busy, and the post-processing
 # kernels' per-step VALU / HBM counts.  Their "batch" must equal the bench's frames per step.
-PMC_TRAFFIC = _first("round4/pmc/pmc_traffic.json", "round3/pmc_traffic.json")
-POST_PMC = _first("round4/pmc/report.json", "round3/pmc_r3i/report.json")
-POST_PMC_B135 = _first("round4/pmc_body135/report.json", "round3/pmc_body135_r3i/report.json")
+PMC_TRAFFIC = _first("round5/r5e/pmc/pmc_traffic.json", "round4/pmc/pmc_traffic.json")
+POST_PMC = _first("round5/r5e/pmc/report.json", "round4/pmc/report.json")
+POST_PMC_B135 = _first("round5/r5e/pmc_body135/report.json", "round4/pmc_body135/report.json")
 
 
 def pmc_traffic(batch):
@@ -524,6 +528,9 @@ def rank_main(args, rank, world, local):
     convs = net.convs()
     params = synth.he_weights(convs, seed=0, out_scale=0.02)
     net.set_params(params)
+    if args.precision == "split":
+        from openpose_amd.api import PRECISION_SPLIT
+        net.set_precision(PRECISION_SPLIT)
     pose = PoseExtractor(ctx, net)
 
     B = args.batch or tile_aligned_batch(torch.cuda.get_device_properties(local).multi_processor_count)
@@ -677,7 +684,8 @@ def rank_main(args, rank, world, local):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp16",
+        "dtype": "fp16" if args.precision == "fp16" else "fp16 hi/lo split (3 MFMA passes)",
+        "precision": args.precision,
         "dev_switches": args.dev or None,
         "data": "synthetic uint8 BGR 1280x720 frames (uniform random), random-init weights",
         "config": {
@@ -689,7 +697,10 @@ def rank_main(args, rank, world, local):
             "parallelism": ("frame-parallel replicas x%d (one process per GPU, RCCL ordered "
                             "gather of per-frame records to rank 0)" % world) if comm_dev == "cuda"
                            else "REHEARSAL x%d: every rank on GPU 0, gloo gather" % world,
-            "compute": "warp u8 fixed-point; conv fp16 x fp16 -> fp32 MFMA; resize/NMS/PAF fp32",
+            "compute": ("warp u8 fixed-point; conv fp16 x fp16 -> fp32 MFMA; resize/NMS/PAF fp32"
+                        if args.precision == "fp16" else
+                        "warp u8 fixed-point; conv as fp16 hi/lo pairs (x_hi w_hi + x_lo w_hi + "
+                        "x_hi w_lo -> fp32 MFMA, stored as hi/lo); resize/NMS/PAF fp32"),
             "people_per_frame_found": people,
             "net_output_std_before_overlay": None if out_std is None else round(out_std, 5),
             "frames_gathered_in_order": total_frames,
@@ -705,8 +716,9 @@ def rank_main(args, rank, world, local):
             "peak": PEAK_FP16_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
-            "traffic": pmc_traffic(B) if nscales == 1 else None,
-            "mfma_busy": pmc_mfma_busy(B) if nscales == 1 else None,
+            "traffic": pmc_traffic(B) if nscales == 1 and args.precision == "fp16" else None,
+            "mfma_busy": pmc_mfma_busy(B) if nscales == 1 and args.precision == "fp16" else None,
+            "mfma_passes_per_useful_flop": 1 if args.precision == "fp16" else 3,
             "pmc": {"traffic": pmc_provenance(PMC_TRAFFIC), "mfma_busy": pmc_provenance(POST_PMC)},
             "traffic_unit": "bytes per launch (HBM, PMC)",
             "algorithmic_gflop_per_launch": round(flops_frame * B / 1e9, 2),
@@ -719,7 +731,7 @@ def rank_main(args, rank, world, local):
         "host_ms": host_ms,
         "per_rank_host": rank_hosts,
     }
-    if rank == 0 and world == 1 and nscales == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and nscales == 1 and not args.no_cpu_baseline and args.precision == "fp16":
         frames_np = frames[first_content][:2].cpu().numpy()   # uint8 [2][720][1280][3]
         result["cpu_baseline"] = cpu_baseline(args, params, frames_np, ov_np[first_content][:2])
         # keypoint parity at full strength on the same frames, fp16 and split precision, and the

@@ -20,38 +20,48 @@ namespace {
 
 __device__ __forceinline__ int round_pos(float a) { return int(a + 0.5f); }
 
-// heat_at's cv::resize arithmetic (heat_dev.h, the M.nsrc lazy sources, CPU semantics) with the
-// plane's source images read from their LDS copies: src + loff[n] holds source n's sh x sw plane
-__device__ __forceinline__ float heat_at_lds(const HeatMap& M, const float* src, const int* loff, int x,
-                                            int y)
+// heat_at's cv::resize arithmetic (heat_dev.h, the M.nsrc lazy sources, CPU semantics) for the x
+// and y PAF planes at once, their source images read from the interleaved LDS copy (src + 2 *
+// loff[n]: source n's sh x sw pixels as (x, y) float pairs): one ds_read_b64 per tap serves both
+// planes, each plane's arithmetic is heat_at's, operation for operation (bit-identical)
+__device__ __forceinline__ float2 heat_at_lds2(const HeatMap& M, const float* src, const int* loff,
+                                               int x, int y)
 {
-    float acc = 0.f;
+    float accx = 0.f, accy = 0.f;
     for (int n = 0; n < M.nsrc; ++n) {
         const ResizeSource& S = M.src[n];
-        const float* pl = src + loff[n];
+        const float2* pl = reinterpret_cast<const float2*>(src) + loff[n];
         const int x0 = S.xofs[x];
         const float4 c = *reinterpret_cast<const float4*>(S.xcoef + 4 * x);
-        const float a[4] = {c.x, c.y, c.z, c.w};
         const float4 b = *reinterpret_cast<const float4*>(S.ycoef + 4 * y);
         const int yb = S.yofs[y] - 1;
-        float h[4];
+        const int c0 = heat_clampi(x0 - 1, 0, S.sw - 1), c1 = heat_clampi(x0, 0, S.sw - 1);
+        const int c2 = heat_clampi(x0 + 1, 0, S.sw - 1), c3 = heat_clampi(x0 + 2, 0, S.sw - 1);
+        float hx[4], hy[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
-            h[k] = cubic_hpass(pl + heat_clampi(yb + k, 0, S.sh - 1) * S.sw, S.sw, x0, a);
-        const float v = cubic_vpass(h, b.x, b.y, b.z, b.w, cubic_simd_column(x, M.w));
-        acc = (n == 0) ? v : v + acc;
+        for (int k = 0; k < 4; ++k) {
+            const float2* row = pl + heat_clampi(yb + k, 0, S.sh - 1) * S.sw;
+            const float2 v0 = row[c0], v1 = row[c1], v2 = row[c2], v3 = row[c3];
+            hx[k] = v0.x * c.x + v1.x * c.y + v2.x * c.z + v3.x * c.w;   // cubic_hpass
+            hy[k] = v0.y * c.x + v1.y * c.y + v2.y * c.z + v3.y * c.w;
+        }
+        const bool simd = cubic_simd_column(x, M.w);
+        const float vx = cubic_vpass(hx, b.x, b.y, b.z, b.w, simd);
+        const float vy = cubic_vpass(hy, b.x, b.y, b.z, b.w, simd);
+        accx = (n == 0) ? vx : vx + accx;
+        accy = (n == 0) ? vy : vy + accy;
     }
-    return M.nsrc > 1 ? acc * M.inv_n : acc;
+    return M.nsrc > 1 ? make_float2(accx * M.inv_n, accy * M.inv_n) : make_float2(accx, accy);
 }
 
-// LDS: the x and y PAF planes' sources staged once per (pair, frame) workgroup; every sample of
-// every candidate line then reads LDS instead of the L2/HBM source rows (dependent loads that set
+// LDS: the x and y PAF planes' sources staged once per (pair, frame) workgroup (interleaved, see
+// heat_at_lds2); every sample of every candidate line then reads LDS instead of the L2/HBM source rows (dependent loads that set
 // the kernel's pace: ~2.4 ms per 64 BODY_135 frames, 152 pairs of ~20 x 20 candidates)
 template <bool LDS>
 __device__ __forceinline__ float score_ab(const float* a, const float* b, const HeatMap& M,
                                           int plane_x, int plane_y, float inter_th,
                                           float inter_min_above, float reject_score,
-                                          double near_dist, const float* lx, const float* ly,
+                                          double near_dist, const float* lxy,
                                           const int* loff)
 {
     const int W = M.w, H = M.h;
@@ -68,9 +78,9 @@ __device__ __forceinline__ float score_ab(const float* a, const float* b, const 
     for (int s = 0; s < n; ++s) {
         const int px = max(0, min(W - 1, round_pos(a[0] + (float)s * stepx)));
         const int py = max(0, min(H - 1, round_pos(a[1] + (float)s * stepy)));
-        const float hx = LDS ? heat_at_lds(M, lx, loff, px, py) : heat_at(M, plane_x, px, py);
-        const float hy = LDS ? heat_at_lds(M, ly, loff, px, py) : heat_at(M, plane_y, px, py);
-        const float v = ux * hx + uy * hy;
+        const float2 h = LDS ? heat_at_lds2(M, lxy, loff, px, py)
+                             : make_float2(heat_at(M, plane_x, px, py), heat_at(M, plane_y, px, py));
+        const float v = ux * h.x + uy * h.y;
         if (v > inter_th) {
             sum += v;
             ++count;
@@ -93,7 +103,7 @@ template <bool LDS>
 __device__ __forceinline__ float score_ab_spl(const float* a, const float* b, const HeatMap& M,
                                               int plane_x, int plane_y, float inter_th,
                                               float inter_min_above, float reject_score,
-                                              double near_dist, const float* lx, const float* ly,
+                                              double near_dist, const float* lxy,
                                               const int* loff, bool valid, int s, int half)
 {
     const int W = M.w, H = M.h;
@@ -112,9 +122,9 @@ __device__ __forceinline__ float score_ab_spl(const float* a, const float* b, co
             const float stepx = vx / (float)n, stepy = vy / (float)n;
             const int px = max(0, min(W - 1, round_pos(a[0] + (float)s * stepx)));
             const int py = max(0, min(H - 1, round_pos(a[1] + (float)s * stepy)));
-            const float hx = LDS ? heat_at_lds(M, lx, loff, px, py) : heat_at(M, plane_x, px, py);
-            const float hy = LDS ? heat_at_lds(M, ly, loff, px, py) : heat_at(M, plane_y, px, py);
-            const float v = ux * hx + uy * hy;
+            const float2 h = LDS ? heat_at_lds2(M, lxy, loff, px, py)
+                                 : make_float2(heat_at(M, plane_x, px, py), heat_at(M, plane_y, px, py));
+            const float v = ux * h.x + uy * h.y;
             pass = v > inter_th;
             w = pass ? v : 0.f;
         }
@@ -160,13 +170,14 @@ __device__ __forceinline__ void pair_setup(const PafArgs& A, int b, int q, const
     py = b * A.heat.channels + A.mapy[q];
 }
 
-// dynamic LDS: [x plane of every source][y plane of every source]; loff[n] = source n's offset
-// (host: paf_lds_floats; 0 = not staged: materialised, CUDA-semantics or too large maps)
+// dynamic LDS: the x and y planes of every source interleaved as (x, y) float pairs; source n's
+// pixels start at pair loff[n] (host: paf_lds_floats; 0 = not staged: materialised, CUDA-semantics
+// or too large maps)
 extern __shared__ float paf_lds[];
 constexpr int kPafLdsMinLines = 64;
 template <bool LDS>
 __device__ __forceinline__ void stage_planes(const PafArgs& A, int plx, int ply, int* loff,
-                                             const float*& lx, const float*& ly)
+                                             const float*& lxy)
 {
     if constexpr (!LDS) return;
     const HeatMap& M = A.heat;
@@ -175,17 +186,14 @@ __device__ __forceinline__ void stage_planes(const PafArgs& A, int plx, int ply,
         loff[n] = tot;
         tot += M.src[n].sh * M.src[n].sw;
     }
-    lx = paf_lds;
-    ly = paf_lds + tot;
+    lxy = paf_lds;
+    float2* d = reinterpret_cast<float2*>(paf_lds);
     for (int n = 0; n < M.nsrc; ++n) {
         const ResizeSource& S = M.src[n];
         const int cnt = S.sh * S.sw;
         const float* gx = S.src + (size_t)plx * cnt;
         const float* gy = S.src + (size_t)ply * cnt;
-        for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
-            paf_lds[loff[n] + i] = gx[i];
-            paf_lds[tot + loff[n] + i] = gy[i];
-        }
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) d[loff[n] + i] = make_float2(gx[i], gy[i]);
     }
     __syncthreads();
 }
@@ -200,9 +208,9 @@ __global__ __launch_bounds__(256) void paf_dense_kernel(float* __restrict__ scor
     int plx, ply, na, nb;
     pair_setup(A, b, q, ca, cb, plx, ply, na, nb);
     int loff[kMaxResizeSources];
-    const float *lx = nullptr, *ly = nullptr;
+    const float* lxy = nullptr;
     const bool use = LDS && na * nb >= kPafLdsMinLines;
-    if (use) stage_planes<LDS>(A, plx, ply, loff, lx, ly);
+    if (use) stage_planes<LDS>(A, plx, ply, loff, lxy);
     float* out = scores + ((size_t)b * A.npairs + q) * A.max_peaks * A.max_peaks;
     // one sample per lane only for pairs with few candidate lines (< kPafLdsMinLines, never staged):
     // with many lines the half-waves' idle lanes and the in-order sums cost more than the
@@ -216,7 +224,7 @@ __global__ __launch_bounds__(256) void paf_dense_kernel(float* __restrict__ scor
             const int i = valid ? t / nb : 0, j = valid ? t - (t / nb) * nb : 0;
             const float sc = score_ab_spl<false>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply,
                                                  A.inter_th, A.inter_min_above, A.reject_score,
-                                                 A.near_dist, lx, ly, loff, valid, s, half);
+                                                 A.near_dist, lxy, loff, valid, s, half);
             if (valid && s == 0) out[(size_t)i * A.max_peaks + j] = sc;
         }
         return;
@@ -225,9 +233,9 @@ __global__ __launch_bounds__(256) void paf_dense_kernel(float* __restrict__ scor
         const int i = t / nb, j = t - (t / nb) * nb;
         out[(size_t)i * A.max_peaks + j] =
             use ? score_ab<true>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
-                                 A.inter_min_above, A.reject_score, A.near_dist, lx, ly, loff)
+                                 A.inter_min_above, A.reject_score, A.near_dist, lxy, loff)
                 : score_ab<false>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
-                                  A.inter_min_above, A.reject_score, A.near_dist, lx, ly, loff);
+                                  A.inter_min_above, A.reject_score, A.near_dist, lxy, loff);
     }
 }
 
@@ -254,11 +262,11 @@ __global__ __launch_bounds__(256) void paf_compact_kernel(float* __restrict__ re
     if (q == 0 && threadIdx.x == 0) rec[0] = fits ? (float)total : -1.f;
     if (!fits) return;
     int loff[kMaxResizeSources];
-    const float *lx = nullptr, *ly = nullptr;
+    const float* lxy = nullptr;
     // staged only for pairs with many candidate lines (block-uniform): a few lines read fewer
     // bytes than the two planes hold
     const bool use = LDS && na * nb >= kPafLdsMinLines;
-    if (use) stage_planes<LDS>(A, plx, ply, loff, lx, ly);
+    if (use) stage_planes<LDS>(A, plx, ply, loff, lxy);
     float* out = rec + 1 + offset;
     // one sample per lane only for pairs with few candidate lines (< kPafLdsMinLines, never staged):
     // with many lines the half-waves' idle lanes and the in-order sums cost more than the
@@ -272,7 +280,7 @@ __global__ __launch_bounds__(256) void paf_compact_kernel(float* __restrict__ re
             const int i = valid ? t / nb : 0, j = valid ? t - (t / nb) * nb : 0;
             const float sc = score_ab_spl<false>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply,
                                                  A.inter_th, A.inter_min_above, A.reject_score,
-                                                 A.near_dist, lx, ly, loff, valid, s, half);
+                                                 A.near_dist, lxy, loff, valid, s, half);
             if (valid && s == 0) out[t] = sc;
         }
         return;
@@ -280,9 +288,9 @@ __global__ __launch_bounds__(256) void paf_compact_kernel(float* __restrict__ re
     for (int t = threadIdx.x; t < na * nb; t += blockDim.x) {
         const int i = t / nb, j = t - (t / nb) * nb;
         out[t] = use ? score_ab<true>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
-                                      A.inter_min_above, A.reject_score, A.near_dist, lx, ly, loff)
+                                      A.inter_min_above, A.reject_score, A.near_dist, lxy, loff)
                      : score_ab<false>(ca + 3 * (i + 1), cb + 3 * (j + 1), A.heat, plx, ply, A.inter_th,
-                                       A.inter_min_above, A.reject_score, A.near_dist, lx, ly, loff);
+                                       A.inter_min_above, A.reject_score, A.near_dist, lxy, loff);
     }
 }
 
