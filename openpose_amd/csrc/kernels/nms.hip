@@ -567,7 +567,15 @@ __device__ __forceinline__ float dpp_from_right(float v)   // lane i gets lane i
     return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), 0x130, 0xF, 0xF, false));
 }
 
-template <int RC, int NS, int CPL>
+// COLD (one source, the pose pipeline's single-scale maps): source windows whose rows cannot reach
+// the threshold are not evaluated.  A map row is sum_k b_k h_k over the window's four horizontal
+// passes h_k, with OpenCV's cubic weights (A = -0.75: sum_k |b_k| = 1 + 2|A| t (1 - t) <= 1.375
+// for every phase t), so max |h_k| * 1.375 (+ a rounding margin) <= th bounds every row of the
+// window by th: none of them holds a pixel > th, so none is a peak, and as a neighbour of a tested
+// pixel p (p > th) any value <= th compares as -inf does.  Such rows are set to -inf instead of
+// evaluated (the candidate set is unchanged for NaN-free maps, as the neighbour maximum is).
+constexpr float kCubicAbsSumBound = 1.3751f;
+template <int RC, int NS, int CPL, bool COLD = false>
 __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ scratch,
                                                               const HeatMap M, int parts, float th)
 {
@@ -649,6 +657,21 @@ __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ 
         }
         taps(n, cur[n] + 3, nv[n]);                          // next advance's row, in flight
     }
+    // (COLD) wave-uniform: the current source window bounds all its rows by th
+    auto window_cold = [&]() -> bool {
+        if constexpr (!COLD || NS != 1) {
+            return false;
+        } else {
+            float m = 0.f;
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    m = fmaxf(m, fmaxf(fabsf(h[0][p][k].x), fabsf(h[0][p][k].y)));
+            return __ballot(m * kCubicAbsSumBound > th) == 0;
+        }
+    };
+    bool cold = window_cold();
     int* pl = scratch + ((size_t)b * parts + c) * (CAP + 1);
     // which lanes test a column, by the row's kind in nmsCpu's rules (testable: not the window's
     // halo columns, inside the map): an inner row tests inner and edge columns, an edge row (1,
@@ -682,8 +705,28 @@ __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ 
         constexpr bool WS = decltype(ws)::value;
         // merged values of map row y (in the map) from its table entries tr (source row per
         // source) and bq (vertical coefficients per source)
-        auto row = [&](const int tr[NS], const float4 bq[NS], Row out) {
+        // (returns true when the row was not evaluated: a cold window, every value <= th)
+        auto row = [&](const int tr[NS], const float4 bq[NS], Row out) -> bool {
             float2_t acc[NP];
+            if constexpr (COLD && NS == 1) {
+                if (cur[0] < tr[0]) {                        // uniform
+                    do {
+#pragma unroll
+                        for (int p = 0; p < NP; ++p) {
+                            h[0][p][0] = h[0][p][1]; h[0][p][1] = h[0][p][2]; h[0][p][2] = h[0][p][3];
+                            h[0][p][3] = hsum(0, p, nv[0][p]);
+                        }
+                        ++cur[0];
+                        taps(0, cur[0] + 3, nv[0]);
+                    } while (cur[0] < tr[0]);
+                    cold = window_cold();
+                }
+                if (cold) {
+#pragma unroll
+                    for (int p = 0; p < NP; ++p) out[p] = float2_t{-INFINITY, -INFINITY};
+                    return true;
+                }
+            }
 #pragma unroll
             for (int n = 0; n < NS; ++n) {
                 while (cur[n] < tr[n]) {                     // uniform
@@ -714,8 +757,9 @@ __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ 
             }
 #pragma unroll
             for (int p = 0; p < NP; ++p) out[p] = NS > 1 ? acc[p] * inv_n : acc[p];
+            return false;
         };
-        auto rowy = [&](int y, Row out) {                    // table entries loaded here
+        auto rowy = [&](int y, Row out) -> bool {            // table entries loaded here
             int tr[NS];
             float4 bq[NS];
 #pragma unroll
@@ -723,7 +767,7 @@ __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ 
                 tr[n] = yofs[n][y];
                 bq[n] = *reinterpret_cast<const float4*>(ycoef[n] + 4 * y);
             }
-            row(tr, bq, out);
+            return row(tr, bq, out);
         };
         auto val = [](const Row r, int k) { return r[k >> 1][k & 1]; };
         // test row ty (values mid) with its neighbour rows up / dn; INNER: ty in 2 .. h-3
@@ -770,11 +814,11 @@ __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ 
         else
 #pragma unroll
             for (int p = 0; p < NP; ++p) up[p] = float2_t{th, th};
-        rowy(ys, mid);                                       // ys < ye <= H
+        bool cmid = rowy(ys, mid);                           // ys < ye <= H
         int y = ys + 1;
         // rows y whose tested row y - 1 is 0 or 1 (top window only)
         for (; y < ye && y < 3; ++y) {
-            rowy(y, v);
+            cmid = rowy(y, v);                               // (v becomes mid)
             test(G, y - 1, up, mid, v);
 #pragma unroll
             for (int p = 0; p < NP; ++p) {
@@ -809,10 +853,12 @@ __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ 
                     yp[n] += 2;
                     cp[n] += 2;
                 }
-                row(tr0, bq0, v);
-                test(I, y - 1, up, mid, v);
-                row(tr1, bq1, w);
-                test(I, y, mid, v, w);
+                // a cold row (every value <= th) holds no candidate: its test is skipped
+                const bool cv = row(tr0, bq0, v);
+                if (!cmid) test(I, y - 1, up, mid, v);
+                const bool cw = row(tr1, bq1, w);
+                if (!cv) test(I, y, mid, v, w);
+                cmid = cw;
 #pragma unroll
                 for (int p = 0; p < NP; ++p) {
                     up[p] = v[p];
@@ -879,10 +925,15 @@ void launch_nms(float* peaks, int* scratch, const HeatMap& heat_in, int frames, 
         // 2.2-2.4x faster than the ring walk on configs 2 and 5, +0.8 % frames/s on config 4
         // (profiles/round4/nms_walk2/); NMS_WALK=0 (dev A/B): the ring walk
         const bool walk2 = dev_switch("NMS_WALK", 8) != 0;
+        // sub-threshold source windows skipped (one source; NMS_COLD=0: every row evaluated, A/B)
+        const bool cold = dev_switch("NMS_COLD", 1) != 0;
         const dim3 grid2((w + 2 * lt - 3) / (2 * lt - 2), (h + rc - 1) / rc, frames * parts);
 #define OPK_NMS_STREAM(NS_)                                                                    \
     do {                                                                                       \
-        if (walk2)                                                                             \
+        if (walk2 && cold && NS_ == 1)                                                         \
+            hipLaunchKernelGGL((nms_detect_walk2_kernel<rc, NS_, 2, true>), grid2, dim3(64), 0, stream, \
+                               scratch, heat, parts, threshold);                               \
+        else if (walk2)                                                                        \
             hipLaunchKernelGGL((nms_detect_walk2_kernel<rc, NS_, 2>), grid2, dim3(64), 0, stream, \
                                scratch, heat, parts, threshold);                               \
         else                                                                                   \

@@ -450,6 +450,49 @@ def test_nms_walk_variants_bitexact(ctx, walk, nscales):
     _multiscale_case(ctx, nscales, 0.25, 90 + nscales, 1, walk)
 
 
+@pytest.mark.parametrize("kind", ["spikes", "borderline_noise", "plateau", "negative"])
+def test_nms_cold_windows_bitexact(ctx, kind):
+    """The walk's cold-window skip (nms_detect_walk2_kernel COLD: a source window whose rows are
+    bounded by th is not evaluated) on fields built around its bound: isolated one-pixel spikes just
+    above the threshold in an otherwise zero map (hot windows next to cold ones), noise whose window
+    maxima straddle th / 1.375, a plateau at th / 1.375 +- 1 ulp, and negative fields (the bound is
+    on |h|).  Peaks bit-identical to the oracle's nmsCpu, and to the walk with the skip off."""
+    rng = np.random.default_rng({"spikes": 1, "borderline_noise": 2, "plateau": 3, "negative": 4}[kind])
+    shape = (2, 78, 46, 82)
+    th = np.float32(0.05)
+    if kind == "spikes":
+        f = np.zeros(shape, np.float32)
+        for _ in range(600):
+            k, c, y, x = rng.integers(0, 2), rng.integers(0, 25), rng.integers(0, 46), rng.integers(0, 82)
+            f[k, c, y, x] = rng.uniform(0.04, 0.2)
+    elif kind == "borderline_noise":
+        f = rng.normal(0, th / 1.375 / 2.5, shape).astype(np.float32)
+    elif kind == "plateau":
+        b = np.float32(th / np.float32(1.375))
+        f = np.full(shape, b, np.float32)
+        f += rng.choice(np.array([0, 1, -1], np.float32), shape) * np.spacing(b)
+        f[:, :, 20:26, 30:40] += np.float32(0.02) * rng.random((2, 78, 6, 10), np.float32)
+    else:
+        f = -np.abs(rng.normal(0, 0.06, shape)).astype(np.float32)
+        f[:, :, 10:14, 10:14] = np.float32(0.3) * rng.random((2, 78, 4, 4), np.float32)
+    got = {}
+    for cold in (1, 0):
+        pose = PoseExtractor(ctx, None)
+        with dev_switches(NMS_COLD=cold):
+            pose.forward_net_output(_dev(f), (656, 368), (1280, 720))
+        got[cold] = pose.peaks_numpy()
+        s = pose.scale_net_to_output()
+        pose.close()
+    off = float(np.float32(0.5 / np.float64(s)))
+    np.testing.assert_array_equal(got[1], got[0])
+    found = 0
+    for k in range(2):
+        peaks = oracle.nms(oracle.resize_merge([f[k]], 368, 656), 0.05, 128, (off, off))
+        np.testing.assert_array_equal(got[1][k], peaks)
+        found += int(peaks[:, 0, 0].sum())
+    assert found > 0
+
+
 def test_nms_one_frame(ctx):
     """A batch of one frame (25 planes) through the streaming walk: peaks and people the oracle's."""
     _multiscale_case(ctx, 1, 0.25, 97, 1, 8, frames=1)
