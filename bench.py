@@ -114,29 +114,51 @@ def cgroup_cpu_quota():
         return None
 
 
-def kernel_src_sha():
-    """sha256 over the kernel sources (openpose_amd/csrc/kernels/*): which kernels a committed
-    PMC summary was collected with (tools/pmc_round.sh records the same digest)."""
+# the kernel sources behind each group of PMC-derived figures: the CNN forward (traffic, MFMA
+# busy) and the post-processing step (overlay add, NMS, PAF: post_roofline)
+KERNEL_GROUPS = {
+    "cnn": ("conv.h", "conv1_fused.hip", "conv3.hip", "conv3_dev.h", "conv3w.hip", "conv3w8.hip",
+            "conv_head.hip", "conv_image.hip", "pool.hip"),
+    "post": ("heat_dev.h", "kernels.h", "misc.hip", "nms.hip", "paf.hip", "resize.hip"),
+}
+
+
+def kernel_src_sha(group=None, read=None):
+    """sha256 over the kernel sources (openpose_amd/csrc/kernels/*, or one KERNEL_GROUPS group):
+    which kernels a committed PMC summary was collected with (tools/pmc_round.sh records the
+    digests).  read(name) -> bytes: the sources of another tree (tools/pmc_stamp.py: a commit)."""
     import hashlib
     d = os.path.join(ROOT, "openpose_amd", "csrc", "kernels")
+    if read is None:
+        def read(name):
+            with open(os.path.join(d, name), "rb") as fh:
+                return fh.read()
+    names = sorted(os.listdir(d)) if group is None else sorted(KERNEL_GROUPS[group])
     h = hashlib.sha256()
-    for f in sorted(os.listdir(d)):
-        with open(os.path.join(d, f), "rb") as fh:
-            h.update(f.encode() + b"\0" + fh.read())
+    for f in names:
+        h.update(f.encode() + b"\0" + read(f))
     return h.hexdigest()[:16]
 
 
-def pmc_provenance(path):
-    """Commit + kernel-source digest a PMC summary was collected at, and whether the kernels are
-    still the ones running now."""
+def pmc_provenance(path, group=None):
+    """Commit + kernel-source digest a PMC summary was collected at, and whether the kernels its
+    figures describe (`group` of KERNEL_GROUPS, else every kernel) are still the ones running now."""
     try:
         with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
     sha = d.get("kernel_src_sha")
-    return {"source": os.path.relpath(path, ROOT), "pmc_commit": d.get("commit"),
-            "kernel_src_sha": sha, "kernels_match_this_tree": sha == kernel_src_sha() if sha else None}
+    out = {"source": os.path.relpath(path, ROOT), "pmc_commit": d.get("commit"),
+           "kernel_src_sha": sha, "all_kernels_match_this_tree": sha == kernel_src_sha() if sha else None}
+    gsha = d.get("%s_kernel_src_sha" % group) if group else None
+    if gsha:
+        out["kernel_group"] = group
+        out["group_kernel_src_sha"] = gsha
+        out["kernels_match_this_tree"] = gsha == kernel_src_sha(group)
+    else:
+        out["kernels_match_this_tree"] = out["all_kernels_match_this_tree"]
+    return out
 
 
 CONTENTS = 4   # distinct synthetic batches: global batch k carries content k % CONTENTS
@@ -484,7 +506,7 @@ def post_roofline(batch, post_ms, pmc_path=POST_PMC, ref_bytes_frame=POST_BYTES_
                     "unit": "GB/s", "frac": round(hf, 4)})
     out.update({"valu_frac": round(vf, 4), "hbm_frac": round(hf, 4),
                 "pmc_per_step": {"valu_wave_insts": pmc["valu_insts"], "hbm_bytes": pmc["hbm_bytes"]},
-                "pmc_source": pmc_provenance(pmc_path),
+                "pmc_source": pmc_provenance(pmc_path, "post"),
                 "note": "neither bound is near its peak: the NMS walk (the largest post kernel) is "
                         "bound by its scalar instruction stream (row tables, taps), DESIGN.md 4.8"})
     return out
@@ -719,7 +741,7 @@ def rank_main(args, rank, world, local):
             "traffic": pmc_traffic(B) if nscales == 1 and args.precision == "fp16" else None,
             "mfma_busy": pmc_mfma_busy(B) if nscales == 1 and args.precision == "fp16" else None,
             "mfma_passes_per_useful_flop": 1 if args.precision == "fp16" else 3,
-            "pmc": {"traffic": pmc_provenance(PMC_TRAFFIC), "mfma_busy": pmc_provenance(POST_PMC)},
+            "pmc": {"traffic": pmc_provenance(PMC_TRAFFIC, "cnn"), "mfma_busy": pmc_provenance(POST_PMC, "cnn")},
             "traffic_unit": "bytes per launch (HBM, PMC)",
             "algorithmic_gflop_per_launch": round(flops_frame * B / 1e9, 2),
             "avg_launch_ms": round(net_ms, 3),

@@ -1,5 +1,7 @@
 """CPU: the parity checker (oracle/parity.py) against the oracle's nmsCpu restatement -- the numpy
 peak test must accept exactly the pixels orc_nms counts, border rules included."""
+import os
+
 import numpy as np
 
 import oracle
@@ -43,3 +45,29 @@ def test_compare_peaks_and_keypoint_shift():
     assert parity.people_identical(r, g, 0.3) == 1 and parity.people_identical(r, g, 0.6) == 2
     g[0, 1] = [3, 3, 1]   # another part set: never matched
     assert parity.keypoint_shift(r, g) == (0.25, 1)
+
+
+def test_pmc_provenance_kernel_groups(tmp_path):
+    """bench.pmc_provenance: a summary stamped with per-group digests matches the running tree for
+    the group whose sources are unchanged and not for a group whose digest differs; without group
+    digests it falls back to the whole-tree digest (tools/pmc_stamp.py, tools/pmc_round.sh)."""
+    import json
+    import bench
+    assert set(bench.KERNEL_GROUPS) == {"cnn", "post"}
+    kdir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "openpose_amd", "csrc", "kernels")
+    for names in bench.KERNEL_GROUPS.values():
+        for n in names:
+            assert os.path.exists(os.path.join(kdir, n)), n
+    full, cnn, post = bench.kernel_src_sha(), bench.kernel_src_sha("cnn"), bench.kernel_src_sha("post")
+    assert len({full, cnn, post}) == 3
+    p = tmp_path / "report.json"
+    p.write_text(json.dumps({"commit": "x", "kernel_src_sha": "0" * 16,
+                             "cnn_kernel_src_sha": cnn, "post_kernel_src_sha": "1" * 16}))
+    c = bench.pmc_provenance(str(p), "cnn")
+    assert c["kernels_match_this_tree"] is True and c["all_kernels_match_this_tree"] is False
+    assert bench.pmc_provenance(str(p), "post")["kernels_match_this_tree"] is False
+    p.write_text(json.dumps({"commit": "x", "kernel_src_sha": full}))
+    assert bench.pmc_provenance(str(p), "cnn")["kernels_match_this_tree"] is True
+    # a reader over another tree gives that tree's digest
+    assert bench.kernel_src_sha("cnn", read=lambda n: b"") != cnn

@@ -18,17 +18,19 @@ batch=$(python -c "import sys; a=sys.argv[1:]; print(a[a.index('--batch')+1] if 
 [ -z "$batch" ] && batch=$(python -c "import torch, bench; print(bench.tile_aligned_batch(torch.cuda.get_device_properties(0).multi_processor_count))")
 python tools/pmc_report.py $out/p1 $out/p2 $out/p3 $out/p4 --json $out/report.json --batch $batch > $out/report.txt 2>&1 &&
 python tools/pmc_summary.py $out/p3/run_counter_collection.csv $out/p4/run_counter_collection.csv $batch $out/pmc_traffic.json > $out/pmc_traffic.log 2>&1
-# provenance: the commit (PMC_COMMIT, passed in by the caller: the box has no .git) and the digest
-# of the kernel sources these counters were collected with (bench.py reports both)
+# provenance: the commit (PMC_COMMIT, passed in by the caller: the box has no .git) and the digests
+# of the kernel sources these counters were collected with, whole and per group (bench.py reports
+# them and whether they still describe the running tree)
 python - "$out" <<'PY'
 import json, os, sys
-sys.path.insert(0, os.getcwd())
-import bench
 for name in ("report.json", "pmc_traffic.json"):
     p = os.path.join(sys.argv[1], name)
     if os.path.exists(p):
         d = json.load(open(p))
         d["commit"] = os.environ.get("PMC_COMMIT")
-        d["kernel_src_sha"] = bench.kernel_src_sha()
         json.dump(d, open(p, "w"), indent=1)
 PY
+for name in report.json pmc_traffic.json; do
+  [ -f $out/$name ] && python tools/pmc_stamp.py $out/$name
+done
+true
