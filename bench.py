@@ -433,9 +433,9 @@ def _first(*rel):
 # records the commit and kernel-source digest it was collected at, reported beside the numbers
 # read from it): CNN HBM bytes per forward, time-weighted MFMA busy, and the post-processing
 # kernels' per-step VALU / HBM counts.  Their "batch" must equal the bench's frames per step.
-PMC_TRAFFIC = _first("round5/r5e/pmc/pmc_traffic.json", "round4/pmc/pmc_traffic.json")
-POST_PMC = _first("round5/r5e/pmc/report.json", "round4/pmc/report.json")
-POST_PMC_B135 = _first("round5/r5e/pmc_body135/report.json", "round4/pmc_body135/report.json")
+PMC_TRAFFIC = _first("round5/r5f/pmc/pmc_traffic.json", "round5/r5e/pmc/pmc_traffic.json", "round4/pmc/pmc_traffic.json")
+POST_PMC = _first("round5/r5f/pmc/report.json", "round5/r5e/pmc/report.json", "round4/pmc/report.json")
+POST_PMC_B135 = _first("round5/r5f/pmc_body135/report.json", "round5/r5e/pmc_body135/report.json", "round4/pmc_body135/report.json")
 
 
 def pmc_traffic(batch):
