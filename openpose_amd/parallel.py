@@ -14,6 +14,8 @@ import subprocess
 import sys
 import time
 
+from collections.abc import Sequence
+
 import numpy as np
 import torch
 import torch.distributed as dist
@@ -286,7 +288,9 @@ class RecordGather:
         return heads, body
 
     def finish(self, parts):
-        """Rank 0: [(keypoints [people, parts, 3], scores [people]), ...] for frames 0..F-1."""
+        """Rank 0: every frame's record in frame order, as an OrderedRecords sequence of
+        (keypoints [people, parts, 3], scores [people]); raises if a frame is missing or produced
+        twice, or a block's records do not parse to its header's length."""
         if self.rank != 0:
             return None
         if self.local:   # headers and bodies in place (never-pushed steps: header -1)
@@ -297,7 +301,8 @@ class RecordGather:
             heads, body_all = self._unpack_device()
             lens = heads[:, :, 4].astype(np.int64)
             starts = np.concatenate([[0], np.cumsum(lens.reshape(-1))[:-1]]).reshape(lens.shape)
-        frames = {}
+        stride = parts * 3 + 1
+        ids, offs, counts = [], [], []
         for i in range(self.steps):
             for r in range(self.world):
                 head = heads[i, r]
@@ -305,25 +310,49 @@ class RecordGather:
                 if rank != r or step != i:
                     raise RuntimeError("step %d rank %d: record header %s" % (i, r, head.tolist()))
                 base = int(starts[i, r])
-                body = body_all[base:base + n]   # views (the result keeps the storage alive)
-                o = 0
-                for f in range(first, first + nf):
-                    people = int(body[o])
-                    o += 1
-                    kp = body[o:o + people * parts * 3].reshape(people, parts, 3)
-                    o += people * parts * 3
-                    ks = body[o:o + people]
-                    o += people
-                    if f in frames:
-                        raise RuntimeError("frame %d produced twice" % f)
-                    frames[f] = (kp, ks)
-                if o != n:
-                    raise RuntimeError("step %d rank %d: %d of %d record floats parsed" % (i, r, o, n))
-        ids = sorted(frames)
-        if ids != list(range(len(ids))):
+                o = base
+                for f in range(first, first + nf):   # the per-frame walk: one count read each
+                    people = int(body_all[o])
+                    ids.append(f)
+                    offs.append(o)
+                    counts.append(people)
+                    o += 1 + people * stride
+                if o - base != n:
+                    raise RuntimeError("step %d rank %d: %d of %d record floats parsed"
+                                       % (i, r, o - base, n))
+        ids = np.asarray(ids, np.int64)
+        order = np.argsort(ids, kind="stable")
+        ids = ids[order]
+        if len(ids) and (np.any(ids[1:] == ids[:-1])):
+            raise RuntimeError("frame %d produced twice" % int(ids[1:][ids[1:] == ids[:-1]][0]))
+        if len(ids) and not np.array_equal(ids, np.arange(len(ids))):
             raise RuntimeError("frames missing from the gather: %s"
-                               % sorted(set(range(ids[-1] + 1)) - set(ids)))
-        return [frames[i] for i in ids]
+                               % sorted(set(range(int(ids[-1]) + 1)) - set(ids.tolist())))
+        return OrderedRecords(body_all, np.asarray(offs, np.int64)[order],
+                              np.asarray(counts, np.int64)[order], parts)
+
+
+class OrderedRecords(Sequence):
+    """The gathered records of frames 0..F-1 in frame order (RecordGather.finish): item f is
+    (keypoints [people, parts, 3], scores [people]) as views into the gathered storage, made on
+    access -- the parse (every frame's position and people count) and its checks are done."""
+
+    def __init__(self, body, offsets, counts, parts):
+        self._body, self._off, self._cnt, self.parts = body, offsets, counts, parts
+
+    def __len__(self):
+        return len(self._off)
+
+    def __getitem__(self, f):
+        if isinstance(f, slice):
+            return [self[i] for i in range(*f.indices(len(self)))]
+        if f < 0:
+            f += len(self)
+        if not 0 <= f < len(self):
+            raise IndexError(f)
+        o, n = int(self._off[f]) + 1, int(self._cnt[f])
+        k = n * self.parts * 3
+        return self._body[o:o + k].reshape(n, self.parts, 3), self._body[o + k:o + k + n]
 
 
 def pack_records(results, parts):

@@ -129,6 +129,29 @@ def test_record_gather_single_rank_roundtrip():
         g.finish(parts)
 
 
+def test_record_gather_duplicate_and_views():
+    """finish(): a frame delivered by two blocks is an error; the ordered result indexes like a
+    list (negative indices, slices) with views of the gathered records."""
+    from tests.rank_stub import frame_result
+    batch, parts = 3, 25
+    results = [frame_result(f, parts) for f in range(2 * batch)]
+    cap = max(parallel.pack_records(results[i * batch:(i + 1) * batch], parts).size for i in range(2))
+    g = parallel.RecordGather(1, 0, cap, 2, "cpu")
+    g.push(0, 0, batch, parallel.pack_records(results[:batch], parts))
+    g.push(1, 0, batch, parallel.pack_records(results[:batch], parts))   # frames 0..2 again
+    with pytest.raises(RuntimeError, match="twice"):
+        g.finish(parts)
+    g = parallel.RecordGather(1, 0, cap, 2, "cpu")
+    for i in range(2):
+        g.push(i, i * batch, batch, parallel.pack_records(results[i * batch:(i + 1) * batch], parts))
+    got = g.finish(parts)
+    assert len(got) == 2 * batch and len(got[1:4]) == 3
+    np.testing.assert_array_equal(got[-1][1], results[-1][1])
+    np.testing.assert_array_equal(got[2:3][0][0], np.asarray(results[2][0], np.float32).reshape(-1, parts, 3))
+    with pytest.raises(IndexError):
+        got[2 * batch]
+
+
 def test_record_gather_forced_collective_single_rank():
     """RecordGather(collective=True) at world size 1 (bench.py --collective-gather): the records
     go through dist.gather and the device-side unpack, here over a one-rank gloo group on CPU;
