@@ -332,6 +332,9 @@ int opk_pose_create(opk_ctx* ctx, opk_net* net /* may be NULL: net output inject
  * reference's CPU connector rejects fails with OPK_ERR_UNSUPPORTED. */
 int opk_pose_create_model(opk_ctx* ctx, opk_net* net, int pose_model, int maximize_positives,
                           int semantics, opk_pose** out);
+/* A pose uses its net until it is destroyed (its forwards, and the net's record of the
+ * post-processing still reading each output buffer): destroy the pose before the net, as the
+ * reference's PoseExtractorCaffe owns its net. */
 int opk_pose_destroy(opk_pose* pose);
 int opk_pose_set_property(opk_pose* pose, int property, double value);
 /* heat-map semantics of the pipeline's resize + NMS (OPK_MAPS_CPU, the default, or OPK_MAPS_CUDA:
