@@ -513,19 +513,48 @@ int PoseHip::collect()
     Slot& sl = slots_[si];
     const PoseModelInfo& m = pose_model(model_);
     const int n = sl.n;
-    const size_t peak_floats = (size_t)m.parts * (kMaxPeaks + 1) * 3;
+    const int P1 = kMaxPeaks + 1;
+    const size_t peak_floats = (size_t)m.parts * P1 * 3;
     const size_t rf = record_floats();
-    const size_t K = std::min<size_t>(kRecordHead, rf);
+    // Device-to-host copies sized from the previous batches (their blit kernels occupy CUs the
+    // next batch's nets need): the first R rows of every part's peak block (R > the largest peak
+    // count seen) and the first K floats of every frame's records; a frame with more peaks or
+    // longer records is fetched whole below.  The host layouts stay the full ones.
+    const size_t K = std::min<size_t>(record_head_, rf);
+    const int R = std::min(peak_rows_, P1);
     float* hp = static_cast<float*>(sl.hpeaks.get((size_t)n * peak_floats * 4));
     float* hr = static_cast<float*>(sl.hrecords.get((size_t)n * K * 4));
     OPK_HIP(hipStreamWaitEvent(copy_, sl.done, 0));
-    OPK_HIP(hipMemcpyAsync(hp, sl.peaks.ptr, (size_t)n * peak_floats * 4, hipMemcpyDeviceToHost,
-                           copy_));
+    OPK_HIP(hipMemcpy2DAsync(hp, (size_t)P1 * 12, sl.peaks.ptr, (size_t)P1 * 12, (size_t)R * 12,
+                             (size_t)n * m.parts, hipMemcpyDeviceToHost, copy_));
     OPK_HIP(hipMemcpy2DAsync(hr, K * 4, sl.records.ptr, rf * 4, K * 4, n, hipMemcpyDeviceToHost,
                              copy_));
-    const auto tw0 = std::chrono::steady_clock::now();
+    auto tw0 = std::chrono::steady_clock::now();
     OPK_HIP(hipStreamSynchronize(copy_));
+    double wait_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count();
+    // frames with a part of R - 1 or more peaks: the whole peak block
+    int max_count = 0;
+    bool refetch = false;
+    for (int f = 0; f < n; ++f) {
+        int fmax = 0;
+        for (int p = 0; p < m.parts; ++p)
+            fmax = std::max(fmax, (int)std::lround(hp[(size_t)f * peak_floats + (size_t)p * P1 * 3]));
+        max_count = std::max(max_count, fmax);
+        if (fmax >= R - 1 && R < P1) {
+            OPK_HIP(hipMemcpyAsync(hp + (size_t)f * peak_floats,
+                                   static_cast<const float*>(sl.peaks.ptr) + (size_t)f * peak_floats,
+                                   peak_floats * 4, hipMemcpyDeviceToHost, copy_));
+            refetch = true;
+        }
+    }
+    if (refetch) {
+        tw0 = std::chrono::steady_clock::now();
+        OPK_HIP(hipStreamSynchronize(copy_));
+        wait_ms += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count();
+    }
+    peak_rows_ = std::min(P1, (max_count + 1 + 4 + 7) / 8 * 8);
     const auto tw1 = std::chrono::steady_clock::now();
+    double over_ms = 0.;   // the long records' copy (a wait, inside tw1 .. tw2)
 
     ConnectParams cp{(int)props_[OPK_PROP_MIN_SUBSET_CNT], (float)props_[OPK_PROP_MIN_SUBSET_SCORE],
                      sl.scale, maximize_positives_, semantics_};
@@ -566,8 +595,13 @@ int PoseHip::collect()
                                      hipMemcpyDeviceToHost, copy_));
             for (int f = r.f0; f <= r.f1; ++f) over_at[f] = r.at + (size_t)(f - r.f0) * r.w;
         }
+        tw0 = std::chrono::steady_clock::now();
         OPK_HIP(hipStreamSynchronize(copy_));
+        over_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw0).count();
     }
+    int max_total = 0;
+    for (int f = 0; f < n; ++f) max_total = std::max(max_total, total[f]);
+    record_head_ = std::min<size_t>(kRecordHead, ((size_t)max_total + 1 + max_total / 4 + 1023) / 1024 * 1024);
     // people assembly: frames are independent (connectBodyParts* per frame), so they run on the
     // pool's kAssemblyThreads host threads; every frame's result is the single-threaded one
     if (!pool_ && n > 1) pool_ = std::make_unique<WorkerPool>(assembly_threads());
@@ -586,8 +620,9 @@ int PoseHip::collect()
     else
         for (int f = 0; f < n; ++f) frame(f, 0);
     const auto tw2 = std::chrono::steady_clock::now();
-    collect_wait_ms_ += std::chrono::duration<double, std::milli>(tw1 - tw0).count();
-    collect_assembly_ms_ += std::chrono::duration<double, std::milli>(tw2 - tw1).count();
+    // (the waits for the copies: device time; the rest, from the first wait's end: assembly)
+    collect_wait_ms_ += wait_ms + over_ms;
+    collect_assembly_ms_ += std::chrono::duration<double, std::milli>(tw2 - tw1).count() - over_ms;
     ++collect_count_;
     head_ = (head_ + 1) & 1;
     --count_;

@@ -157,7 +157,9 @@ private:
 
     Slot slots_[2];
     int head_ = 0, count_ = 0, last_ = -1;
-    HostBuf overflow_;                   // records longer than kRecordHead (pinned)
+    HostBuf overflow_;                   // records longer than the copied head (pinned)
+    size_t record_head_ = kRecordHead;   // record floats per frame copied eagerly (adaptive)
+    int peak_rows_ = kMaxPeaks + 1;      // peak rows per part copied eagerly (adaptive)
     // people assembly: worker threads (started by the first multi-frame collect) and one
     // scratch per worker
     std::unique_ptr<WorkerPool> pool_;

@@ -450,6 +450,44 @@ def test_nms_walk_variants_bitexact(ctx, walk, nscales):
     _multiscale_case(ctx, nscales, 0.25, 90 + nscales, 1, walk)
 
 
+def test_collect_copy_sizes_adapt(ctx):
+    """collect() copies the first rows of every part's peak block and the first floats of every
+    frame's records, sized from the previous batches: a batch with far more peaks / longer records
+    than the last one (1 person, then 24 with noise peaks, then 1 again, on BODY_25 and the GPU-path
+    connector over BODY_135) is fetched whole where needed -- peaks, candidates and people
+    bit-exact against the oracle chain for every batch."""
+    for model, sem in ((0, None), (BODY_135, CONNECT_GPU)):
+        t = oracle.pose_tables()[model]
+        C = t["parts"] + int(t["bkg"]) + len(t["map_idx"])
+        pose = PoseExtractor(ctx, None, pose_model=model, **({"semantics": sem} if sem is not None else {}))
+        for k, people in enumerate((1, 24, 1)):
+            rng = np.random.default_rng(6100 + k)
+            fields = np.stack([synth.overlay(people, 46, 82, seed=6100 + 10 * k + f, table=t) +
+                               rng.normal(0, 0.03 if people > 1 else 0.005, (C, 46, 82))
+                               for f in range(2)]).astype(np.float32)
+            pose.forward_net_output(_dev(fields), (656, 368), (1280, 720))
+            s = pose.scale_net_to_output()
+            off = float(np.float32(0.5 / np.float64(s)))
+            gpu_peaks = pose.peaks_numpy()
+            for f in range(2):
+                heat = oracle.resize_merge([fields[f]], 368, 656)
+                peaks = oracle.nms(heat, 0.05, 128, (off, off), channels=t["parts"])
+                np.testing.assert_array_equal(gpu_peaks[f], peaks)
+                if sem is None:
+                    rk, rs = oracle.connect(heat, peaks, scale=s)
+                else:
+                    rk, rs = oracle.connect_gpu_semantics(oracle.pair_scores_table(heat, peaks, t),
+                                                          peaks, t, scale=s)
+                kp, ks = pose.keypoints(f)
+                np.testing.assert_array_equal(kp, rk)
+                np.testing.assert_array_equal(ks, rs)
+                cand = pose.candidates(f)   # (read from the host copy of the peaks)
+                counts = peaks[:, 0, 0].astype(int)
+                for part in range(t["parts"]):
+                    np.testing.assert_array_equal(cand[part][:, 2], peaks[part, 1:counts[part] + 1, 2])
+        pose.close()
+
+
 @pytest.mark.parametrize("kind", ["spikes", "borderline_noise", "plateau", "negative"])
 def test_nms_cold_windows_bitexact(ctx, kind):
     """The walk's cold-window skip (nms_detect_walk2_kernel COLD: a source window whose rows are
