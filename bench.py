@@ -20,9 +20,10 @@ the net output -- its cost is counted).
 Multi-GPU (--gpus N): one process per GPU.  Started under torch.distributed.run the ranks come
 from the environment; started directly, this process spawns N ranks (openpose_amd.parallel.
 launch_ranks) before any GPU call and waits for them.  Frames shard across ranks with no
-collective in the data path (frame-parallel replicas, weak scaling); every step, each rank's
-per-frame keypoint records are gathered to rank 0 in frame order (RCCL gather over xGMI, the
-reference's WQueueOrderer), inside the timed region.
+collective in the data path (frame-parallel replicas, weak scaling); each rank's per-frame keypoint
+records are gathered to rank 0 in frame order (RCCL gather over xGMI, the reference's
+WQueueOrderer) inside the timed region -- once at the end of the timed steps by default
+(--gather-interval 0: ranks meet only there), or every --gather-interval steps.
 """
 import argparse
 import json
@@ -76,6 +77,13 @@ def parse():
                     help="body25 / multiscale: the net's arithmetic (opk_net_set_precision): fp16 "
                          "(the product path, the default) or split (fp16 hi/lo pairs, ~fp32 "
                          "results, three MFMA passes per conv)")
+    ap.add_argument("--gather-interval", type=int, default=0,
+                    help="steps per gather of the per-frame records to rank 0 (N > 1); 0: one gather "
+                         "at the end of the timed steps, so ranks are coupled only there")
+    ap.add_argument("--no-extra-configs", action="store_true",
+                    help="the default run (1 GPU, body25, fp16) also times split precision, "
+                         "config 4 (multiscale) and config 5 (body135) in child processes and "
+                         "reports them under `configs`; this flag skips those legs")
     ap.add_argument("--dev", action="append", default=[], metavar="KEY=VAL",
                     help="kernel-variant switch for A/B runs (opk_dev_set; include/opk.h)")
     return ap.parse_args()
@@ -536,6 +544,61 @@ def dist_setup(world, local, collective=False):
     return dev, dist, "cpu" if rehearse and world > 1 else "cuda"
 
 
+# the legs the default run adds to its JSON line (`configs`): BASELINE.json's other 1-GPU
+# configurations and the parity-meeting precision, each a short bench.py run of its own
+EXTRA_LEGS = (
+    ("split_precision", ["--precision", "split", "--steps", "10", "--warmup", "2"]),
+    ("config4_multiscale", ["--config", "multiscale", "--steps", "10", "--warmup", "2"]),
+    ("config5_body135", ["--config", "body135", "--steps", "30", "--warmup", "3"]),
+)
+_TORCHRUN_ENV = ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                 "ROLE_WORLD_SIZE", "GROUP_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
+                 "TORCHELASTIC_RUN_ID", "TORCHELASTIC_RESTART_COUNT", "TORCHELASTIC_MAX_RESTARTS")
+
+
+def extra_legs(args, timeout=240):
+    """Run each EXTRA_LEGS configuration as a child bench.py process on this GPU (started after
+    every measurement of this run, which stays idle meanwhile; a child process, not an exec) and
+    return {name: summary of its JSON line} -- the driver's one bench line then carries
+    driver-observed config-4, config-5 and split-precision throughput."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in _TORCHRUN_ENV}
+    out = {}
+    for name, extra in EXTRA_LEGS:
+        cmd = [sys.executable, "-u", os.path.abspath(__file__), "--gpus", "1", "--no-cpu-baseline",
+               "--no-extra-configs"] + extra + sum((["--dev", d] for d in args.dev), [])
+        t0 = time.perf_counter()
+        try:
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, env=env)
+        except subprocess.TimeoutExpired:
+            out[name] = {"error": "timed out after %d s" % timeout, "args": extra}
+            continue
+        wall = time.perf_counter() - t0
+        line = next((ln for ln in reversed(r.stdout.splitlines()) if ln.startswith("{")), None)
+        if r.returncode != 0 or line is None:
+            out[name] = {"error": "exit %d" % r.returncode, "args": extra,
+                         "stderr_tail": r.stderr[-600:]}
+            continue
+        d = json.loads(line)
+        rf = d.get("roofline") or {}
+        leg = {"args": extra, "value": d["value"], "unit": d["unit"], "ms_per_step": d["ms_per_step"],
+               "steps": d["steps"], "warmup": d["warmup"], "dtype": d["dtype"],
+               "frames_per_step": d["config"].get("frames_per_step_per_gpu"),
+               "workload": d["config"]["workload"], "process_wall_s": round(wall, 1),
+               "roofline": {k: rf.get(k) for k in ("bound", "kernel", "achieved", "peak", "unit", "frac",
+                                                   "avg_launch_ms", "algorithmic_gflop_per_launch",
+                                                   "mfma_passes_per_useful_flop", "pass_tflops",
+                                                   "frac_of_measured_random_operand_mfma")
+                            if k in rf},
+               "host_ms": d.get("host_ms")}
+        if d.get("post_roofline"):
+            pr = d["post_roofline"]
+            leg["post_roofline"] = {k: pr.get(k) for k in ("bound", "achieved", "unit", "frac",
+                                                           "avg_launch_ms")}
+        out[name] = leg
+    return out
+
+
 def rank_main(args, rank, world, local):
     local, dist, comm_dev = dist_setup(world, local, args.collective_gather)
 
@@ -582,7 +645,7 @@ def rank_main(args, rank, world, local):
     # per-step ordered gather of the per-frame records (capacity: 4x the synthetic people + 8)
     cap = B * (1 + (4 * args.people + 8) * (PARTS * 3 + 1))
     gather = parallel.RecordGather(world, rank, cap, args.steps, comm_dev,
-                                    collective=dist is not None)
+                                    collective=dist is not None, interval=args.gather_interval)
 
     # Two-stage pipeline (opk_pose_submit / opk_pose_collect): the device work of batch i+1 is
     # enqueued before the host assembly of batch i, which then overlaps it.
@@ -726,6 +789,7 @@ def rank_main(args, rank, world, local):
             "people_per_frame_found": people,
             "net_output_std_before_overlay": None if out_std is None else round(out_std, 5),
             "frames_gathered_in_order": total_frames,
+            "gather_interval_steps": args.gather_interval or "at the end of the timed steps",
         },
         "per_rank": [{"rank": int(r[0]), "s": round(r[1], 4), "cnn_ms_per_step": round(r[2], 3),
                       "post_ms_per_step": round(r[3], 3)} for r in per_rank],
@@ -741,6 +805,8 @@ def rank_main(args, rank, world, local):
             "traffic": pmc_traffic(B) if nscales == 1 and args.precision == "fp16" else None,
             "mfma_busy": pmc_mfma_busy(B) if nscales == 1 and args.precision == "fp16" else None,
             "mfma_passes_per_useful_flop": 1 if args.precision == "fp16" else 3,
+            # split: the MFMA work issued (three fp16 passes per useful FLOP)
+            "pass_tflops": round(achieved * (1 if args.precision == "fp16" else 3), 2),
             "pmc": {"traffic": pmc_provenance(PMC_TRAFFIC, "cnn"), "mfma_busy": pmc_provenance(POST_PMC, "cnn")},
             "traffic_unit": "bytes per launch (HBM, PMC)",
             "algorithmic_gflop_per_launch": round(flops_frame * B / 1e9, 2),
@@ -767,6 +833,9 @@ def rank_main(args, rank, world, local):
         p16["precision"] = "fp16 (the measured product path)"
         psp["precision"] = "split (opk_net_set_precision OPK_PRECISION_SPLIT)"
         result["parity"] = dict(p16, split_precision=psp)
+    if (rank == 0 and world == 1 and nscales == 1 and args.precision == "fp16" and not args.no_extra_configs
+            and not args.dump_records and not args.collective_gather):
+        result["configs"] = extra_legs(args)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
@@ -800,7 +869,7 @@ def rank_main_body135(args, rank, world, local):
     parts = t["parts"]
     cap = B * (1 + (4 * people + 8) * (parts * 3 + 1))
     gather = parallel.RecordGather(world, rank, cap, args.steps, comm_dev,
-                                    collective=dist is not None)
+                                    collective=dist is not None, interval=args.gather_interval)
     rec_buf = np.empty(cap, np.float32)
     collected = [0]
 
@@ -894,6 +963,7 @@ def rank_main_body135(args, rank, world, local):
                            else "REHEARSAL x%d: every rank on GPU 0, gloo gather" % world,
             "people_per_frame_found": found,
             "frames_gathered_in_order": total_frames,
+            "gather_interval_steps": args.gather_interval or "at the end of the timed steps",
         },
         "roofline": dict(post_roofline(B, post_ms, POST_PMC_B135, post_bytes), traffic=None),
         "host_ms": host_ms,

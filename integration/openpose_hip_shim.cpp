@@ -116,8 +116,12 @@ namespace op
                 error("OPENPOSE_HIP_PRECISION must be fp16 or split, not '" + want + "'.", __LINE__,
                       __FUNCTION__, __FILE__);
             }
-            if (want == "split")
-                check(opk_net_set_precision(net, OPK_PRECISION_SPLIT), __LINE__, __FUNCTION__);
+            if (want == "split" && opk_net_set_precision(net, OPK_PRECISION_SPLIT) != OPK_OK)
+            {
+                const std::string msg = opk_last_error();   // (read before the destroy resets it)
+                opk_net_destroy(net);   // not leaked on the error path
+                error(std::string{"libopk_hip: "} + msg, __LINE__, __FUNCTION__, __FILE__);
+            }
             return net;
         }
 

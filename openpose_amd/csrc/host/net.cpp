@@ -16,6 +16,7 @@
 #include "caffemodel.h"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <set>
 
@@ -327,13 +328,32 @@ void NetHip::pack(ConvPlan& c)
     const bool need_packed = c.from_image;   // conv_image's layout: [cout_pad][64]
     std::vector<uint16_t> packed(need_packed ? (size_t)c.cout_pad * K : 0, 0);
     auto f2h = [](float v) { _Float16 h = (_Float16)v; return __builtin_bit_cast(uint16_t, h); };
+    // split precision: the layer's weights scaled by 2^e, max |w| * 2^e in [2^14, 2^15), so that
+    // w_lo = fp16(w' - w_hi) stays a normal fp16 number (ConvArgs::wscale); the kernels multiply
+    // the sums by 2^-e (exact) before the bias.  fp16: unscaled.
+    int wexp = 0;
+    if (split) {
+        float mx = 0.f;
+        for (size_t e = 0; e < c.hw.size(); ++e) mx = std::max(mx, std::fabs(w[e]));
+        if (mx > 0.f && std::isfinite(mx)) {
+            int ex = 0;
+            (void)std::frexp(mx, &ex);   // mx in [2^(ex-1), 2^ex)
+            wexp = std::max(-100, std::min(100, 15 - ex));
+        }
+    }
+    c.wscale = std::ldexp(1.f, -wexp);
+    auto wsc = [&](float v) { return std::ldexp(v, wexp); };   // exact (no overflow / underflow here)
     for (int co = 0; co < c.info.cout && need_packed; ++co) {
         uint16_t* dst = packed.data() + (size_t)co * K;
-        if (c.from_image) {   // K index (ky*3 + kx)*3 + ci
+        if (c.from_image) {   // K index (ky*3 + kx)*3 + ci; split: w_lo at K + 32
             for (int ci = 0; ci < 3; ++ci)
                 for (int ky = 0; ky < 3; ++ky)
-                    for (int kx = 0; kx < 3; ++kx)
-                        dst[(ky * 3 + kx) * 3 + ci] = f2h(w[(((size_t)co * 3 + ci) * 3 + ky) * 3 + kx]);
+                    for (int kx = 0; kx < 3; ++kx) {
+                        const float wv = wsc(w[(((size_t)co * 3 + ci) * 3 + ky) * 3 + kx]);
+                        const int kk = (ky * 3 + kx) * 3 + ci;
+                        dst[kk] = f2h(wv);
+                        if (split) dst[32 + kk] = f2h(wv - (float)(_Float16)wv);
+                    }
             continue;
         }
         for (int t = 0; t < c.ntaps; ++t) {
@@ -343,10 +363,9 @@ void NetHip::pack(ConvPlan& c)
         }
     }
     // conv3.hip layout: [cout_pad/BN][cin_pad/32][ky][kx][n BN][ci 32]; split precision: three
-    // passes of chunks, [cout_pad/BN][3][cin_pad/32]..., holding w_hi, w_hi, w_lo (ConvArgs::split;
-    // the first conv then runs on conv3 too, over the 32-channel split image)
+    // passes of chunks, [cout_pad/BN][3][cin_pad/32]..., holding w_hi, w_hi, w_lo (ConvArgs::split)
     std::vector<uint16_t> packed3;
-    if (!c.from_image || split) {
+    if (!c.from_image) {
         const int BN = conv3_shape(1, 1, 1, c.info.cout, k, border_).bn;   // BN depends on cout only
         const int nb = (c.info.cout + BN - 1) / BN, cpt = c.cin_pad / 32, kt = k * k;
         const int passes = split ? 3 : 1;
@@ -354,7 +373,7 @@ void NetHip::pack(ConvPlan& c)
         for (int co = 0; co < c.info.cout; ++co)
             for (int ci = 0; ci < cin; ++ci)
                 for (int t = 0; t < kt; ++t) {
-                    const float wv = w[(((size_t)co * cin + ci) * k + t / k) * k + t % k];
+                    const float wv = wsc(w[(((size_t)co * cin + ci) * k + t / k) * k + t % k]);
                     const _Float16 hi = (_Float16)wv;
                     for (int ps = 0; ps < passes; ++ps) {
                         const size_t idx = ((((size_t)(co / BN) * passes * cpt + ps * cpt + ci / 32) * kt + t) *
@@ -494,8 +513,8 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
     for (size_t i = 0; i < bufs_.size(); ++i) {
         S.mem.push_back(std::make_unique<DevBuf>());
         S.mem_lo.push_back(std::make_unique<DevBuf>());
-        // conv_image reads the NCHW input itself (split precision: the split image, 32 channels)
-        if ((int)i == image_buf_ && !S.split) continue;
+        // conv_image reads the NCHW input itself (in both precisions)
+        if ((int)i == image_buf_) continue;
         bool head_buf = false;
         for (const auto& fh : heads_) head_buf = head_buf || fh.buf == (int)i;
         if (S.fusedh && head_buf) continue;   // Mconv6 outputs live only inside conv_head_kernel
@@ -535,14 +554,14 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
         a.in_cs = bufs_[c.in.buf].cs;
         a.in_coff = c.in.coff;
         a.cin_pad = c.cin_pad;
-        a.ntaps = c.from_image && S.split ? 9 : c.ntaps;   // (split: the first conv on conv3)
+        a.ntaps = c.ntaps;
         if (a.ntaps == 9)
             for (int t = 0; t < 9; ++t) a.tapoff[t] = (t / 3) * Wp + (t % 3);
         else if (a.ntaps == 1)
             a.tapoff[0] = Wp + 1;
         a.border = border_;
         a.ksteps = c.ksteps;
-        const bool use3 = !c.from_image || S.split;
+        const bool use3 = !c.from_image;
         S.use3[ci] = use3;
         OPK_CHECK_ARG(use3 || c.w.ptr != nullptr, c.info.name + ": weights not set");
         if (use3) {
@@ -572,6 +591,7 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
             a.dst_lo[d] = S.base_lo[c.outs[d].buf];
         }
         a.split = S.split ? 1 : 0;
+        a.wscale = S.split ? c.wscale : 1.f;
         a.in_lo = S.base_lo[c.in.buf];
         for (size_t q = 0; q < pools_.size(); ++q)
             if (S.poolfused[q] && pool_conv_[q] == (int)ci) {   // the pooled image instead
@@ -716,22 +736,41 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
 // (the full-resolution layers of a large batch run unfused only in split precision): each launch
 // takes a run of whole frames, its pointers moved to the run's first frame -- the positions just
 // before and after a run are frame borders, zero like the guards of a whole-batch launch.
+//
+// Runs are sized evenly (ceil(frames / runs) frames each), and each run takes the strip geometry
+// conv3_shape chooses for ITS frame count: the planner's sw / nstrips were chosen for the whole
+// batch, and a run with fewer tiles may fall into another tile branch (another halo, so another
+// strip count) -- launch_conv3 requires the geometry of its own frame count.
+static bool conv3_run_fits(const ConvArgs& a, int frames, int ks, int B)
+{
+    const Conv3Shape s = conv3_shape(frames, a.H, a.W, a.cout, ks, B);
+    const long total = (long)frames * s.nstrips * (a.H + 2 * B) * (s.sw + 2 * B);
+    return total + s.bm + (long)(ks - 1) * (s.sw + 2 * B + 1) < (1L << 24);
+}
+
 static void launch_conv3_frames(const ConvArgs& a, hipStream_t st)
 {
     const int B = a.border > 0 ? a.border : 1;
     const int ks = a.ntaps == 49 ? 7 : (a.ntaps == 9 ? 3 : 1);
-    const Conv3Shape s3 = conv3_shape(a.frames, a.H, a.W, a.cout, ks, B);
-    const long per_frame = (long)s3.nstrips * (a.H + 2 * B) * (s3.sw + 2 * B);
-    const long room = (1L << 24) - s3.bm - (long)(ks - 1) * (s3.sw + 2 * B + 1) - 1;
-    const int run = (int)std::max(1L, std::min<long>(a.frames, room / per_frame));
-    if (run >= a.frames) {
+    if (conv3_run_fits(a, a.frames, ks, B)) {
         launch_conv3(a, st);
         return;
     }
+    int runs = 2;
+    for (;; ++runs) {   // the fewest even runs whose every run fits (a run of 1 frame always does)
+        const int run = (a.frames + runs - 1) / runs;
+        const int last = a.frames - ((a.frames + run - 1) / run - 1) * run;
+        if (conv3_run_fits(a, run, ks, B) && conv3_run_fits(a, last, ks, B)) break;
+        OPK_CHECK_ARG(run > 1, "launch_conv3_frames: one frame exceeds a launch's position range");
+    }
+    const int run = (a.frames + runs - 1) / runs;
     const size_t frame_pos = (size_t)(a.H + 2 * B) * (a.W + 2 * B);   // padded image positions
     for (int f0 = 0; f0 < a.frames; f0 += run) {
         ConvArgs b = a;
         b.frames = std::min(run, a.frames - f0);
+        const Conv3Shape sb = conv3_shape(b.frames, a.H, a.W, a.cout, ks, B);
+        b.sw = sb.sw;
+        b.nstrips = sb.nstrips;
         b.M = b.frames * a.H * (a.W + 2 * B);
         b.in = a.in + f0 * frame_pos * a.in_cs;
         if (a.in_lo) b.in_lo = a.in_lo + f0 * frame_pos * a.in_cs;
@@ -752,9 +791,6 @@ void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w
     const std::vector<int>& lh_ = S.lh;
     const std::vector<int>& lw_ = S.lw;
     size_t first = 0;
-    if (S.split)   // the first conv's input as the split 32-channel image
-        launch_image_split(ptr[image_buf_], S.base_lo[image_buf_], bufs_[image_buf_].cs, input, n, h,
-                           w, border_, st);
     if (S.fused1) {
         const ConvPlan& a = convs_[fuse1_.a];
         const ConvPlan& b = convs_[fuse1_.b];
@@ -825,7 +861,7 @@ void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w
                 continue;
             }
             if (log) log->layer = c.info.name + (a.pool ? "+pool" : "");
-            if (c.from_image && !S.split) {
+            if (c.from_image) {
                 ConvArgs ai = a;
                 if (ai.out32) ai.out32 = out32;
                 launch_conv_image(ai, input, st);

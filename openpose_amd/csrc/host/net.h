@@ -59,6 +59,9 @@ public:
     // out -- through PoseHip or a direct opk_net_forward -- first makes its stream wait for ev, so
     // the forward never overwrites values a post-processing still reads.  One event per buffer
     // (the readers run in order on one stream, so the latest covers the earlier ones).
+    // expires when the net is destroyed: a PoseHip holding this net detects a net destroyed
+    // before it (~PoseHip's forget_reader_events on a dead net)
+    std::weak_ptr<void> liveness() const { return alive_; }
     void note_reader(const float* out, hipEvent_t ev);
     void forget_reader_events(const hipEvent_t* evs, int n);   // (the owner destroys them)
     int out_channels() const { return out_c_; }
@@ -102,6 +105,7 @@ private:
         int head = -1;        // index into heads_ (as either half), -1 none
         bool loaded = false;
         bool slope01 = true;  // PReLU slopes all in [0, 1] (ConvArgs::actmax)
+        float wscale = 1.f;   // split precision: 2^-e of the packed weights' scaling (ConvArgs::wscale)
         std::vector<float> hw, hb, hs;   // host copies of the weights (re-packed per precision)
     };
     void pack(ConvPlan& c);   // device layouts of one conv's weights for the current precision
@@ -164,6 +168,7 @@ private:
     std::vector<std::unique_ptr<ShapePlan>> shapes_;   // oldest first
     ShapePlan* cur_ = nullptr;    // shape of the last forward
     std::vector<std::pair<const float*, hipEvent_t>> readers_;   // note_reader
+    std::shared_ptr<int> alive_ = std::make_shared<int>(0);       // liveness()
     DevBuf sink_;                 // persistent conv3: target of masked-off stores
     EventTimer timer_;            // forwards bracketed by HIP events (set_timing)
 };

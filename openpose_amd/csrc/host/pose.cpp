@@ -38,6 +38,7 @@ double resize_scale_factor(int iw, int ih, int tw, int th)
 PoseHip::PoseHip(Context* ctx, NetHip* net, bool maxpos, int pose_model_id, int semantics)
     : ctx_(ctx), net_(net), maximize_positives_(maxpos), model_(pose_model_id), semantics_(semantics)
 {
+    if (net_) net_alive_ = net_->liveness();
     const PoseModelInfo& m = pose_model(model_);   // throws for unknown models
     OPK_CHECK_ARG(semantics == kConnectCpu || semantics == kConnectGpu, "unknown connector semantics");
     if (semantics == kConnectCpu && !m.cpu_connector())   // bodyPartConnectorBase.cpp:165-167
@@ -56,6 +57,14 @@ PoseHip::PoseHip(Context* ctx, NetHip* net, bool maxpos, int pose_model_id, int 
     }
 }
 
+NetHip* PoseHip::live_net() const
+{
+    OPK_CHECK_ARG(net_ != nullptr, "no net: a pose extractor over injected net outputs");
+    if (net_alive_.expired())
+        throw Error(4, "the net was destroyed before this pose extractor (destroy the pose first)");
+    return net_;
+}
+
 PoseHip::~PoseHip()
 {
     if (copy_) {
@@ -64,7 +73,7 @@ PoseHip::~PoseHip()
     }
     if (post_) {
         (void)hipStreamSynchronize(post_);
-        if (net_) net_->forget_reader_events(post_done_, 2);
+        if (net_ && !net_alive_.expired()) net_->forget_reader_events(post_done_, 2);
         ctx_->remove_side_stream(post_);
         (void)hipStreamDestroy(post_);
         (void)hipEventDestroy(nets_done_);
@@ -213,8 +222,8 @@ void PoseHip::submit(const float* frames, int n, int net_h, int net_w, int prod_
     OPK_CHECK_ARG(count_ < 2, "two batches already in flight: collect first");
     ctx_->bind();
     next_output(n, net_h, net_w, true);
-    net_->forward(frames, n, net_h, net_w);
-    const NetOutput o{net_->output(), net_->out_h(), net_->out_w()};
+    live_net()->forward(frames, n, net_h, net_w);
+    const NetOutput o{live_net()->output(), live_net()->out_h(), live_net()->out_w()};
     submit_outputs(&o, 1, n, net_h, net_w, prod_w, prod_h, true);
 }
 
@@ -246,7 +255,7 @@ void PoseHip::next_output(int n, int h, int w, bool alternate)
     // (the forward that writes the buffer waits for the post-processings reading it:
     // NetHip::note_reader)
     const bool alt = alternate && post_ != nullptr && dev_switch("NET_OUT_ALT", 1) != 0;
-    (void)net_->select_output(n, h, w, alt);
+    (void)live_net()->select_output(n, h, w, alt);
 }
 
 void PoseHip::set_input(int net_w, int net_h, float dyn, int scale_number, double scale_gap)
@@ -340,8 +349,8 @@ void PoseHip::submit_multi(const float* const* frames, const int* net_hw, int ns
     for (int i = 0; i < nscales; ++i) next_output(n, net_hw[2 * i], net_hw[2 * i + 1], nscales == 1 || distinct);
     if (nscales == 1 || !distinct) {
         for (int i = 0; i < nscales; ++i) {
-            net_->forward(frames[i], n, net_hw[2 * i], net_hw[2 * i + 1]);
-            outs[i] = NetOutput{net_->output(), net_->out_h(), net_->out_w()};
+            live_net()->forward(frames[i], n, net_hw[2 * i], net_hw[2 * i + 1]);
+            outs[i] = NetOutput{live_net()->output(), live_net()->out_h(), live_net()->out_w()};
         }
     } else {
         if (!fork_) {
@@ -351,21 +360,21 @@ void PoseHip::submit_multi(const float* const* frames, const int* net_hw, int ns
                 OPK_HIP(hipEventCreateWithFlags(&join_[i], hipEventDisableTiming));
             }
         }
-        for (int i = 0; i < nscales; ++i) net_->prepare(n, net_hw[2 * i], net_hw[2 * i + 1]);
+        for (int i = 0; i < nscales; ++i) live_net()->prepare(n, net_hw[2 * i], net_hw[2 * i + 1]);
         hipStream_t s = ctx_->stream;
-        net_->time_begin(s);   // one timed region for all the scales' nets of the batch
+        live_net()->time_begin(s);   // one timed region for all the scales' nets of the batch
         OPK_HIP(hipEventRecord(fork_, s));   // inputs warped, new plans zeroed
-        net_->forward_on(frames[0], n, net_hw[0], net_hw[1], s, false);
-        outs[0] = NetOutput{net_->output(), net_->out_h(), net_->out_w()};
+        live_net()->forward_on(frames[0], n, net_hw[0], net_hw[1], s, false);
+        outs[0] = NetOutput{live_net()->output(), live_net()->out_h(), live_net()->out_w()};
         for (int i = 1; i < nscales; ++i) {
             OPK_HIP(hipStreamWaitEvent(scale_streams_[i - 1], fork_, 0));
-            net_->forward_on(frames[i], n, net_hw[2 * i], net_hw[2 * i + 1], scale_streams_[i - 1],
+            live_net()->forward_on(frames[i], n, net_hw[2 * i], net_hw[2 * i + 1], scale_streams_[i - 1],
                              false);
-            outs[i] = NetOutput{net_->output(), net_->out_h(), net_->out_w()};
+            outs[i] = NetOutput{live_net()->output(), live_net()->out_h(), live_net()->out_w()};
             OPK_HIP(hipEventRecord(join_[i - 1], scale_streams_[i - 1]));
         }
         for (int i = 1; i < nscales; ++i) OPK_HIP(hipStreamWaitEvent(s, join_[i - 1], 0));
-        net_->time_end(s);
+        live_net()->time_end(s);
     }
     submit_outputs(outs.data(), nscales, n, net_hw[0], net_hw[1], prod_w, prod_h, true);
 }
@@ -474,7 +483,7 @@ void PoseHip::submit_outputs(const NetOutput* outs, int nscales, int n, int net_
         OPK_HIP(hipEventRecord(post_done_[k], post_));
         // every later forward writing one of these outputs (ours or a direct opk_net_forward)
         // waits for this post-processing first
-        for (int i = 0; i < nscales; ++i) net_->note_reader(outs[i].ptr, post_done_[k]);
+        for (int i = 0; i < nscales; ++i) live_net()->note_reader(outs[i].ptr, post_done_[k]);
         ++post_count_;
     }
     sl.n = n;

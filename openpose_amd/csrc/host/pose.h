@@ -113,6 +113,8 @@ private:
 
     Context* ctx_;
     NetHip* net_;
+    std::weak_ptr<void> net_alive_;   // NetHip::liveness (the net may be destroyed first)
+    NetHip* live_net() const;         // net_, or an error if it was destroyed
     // set_input(): --net_resolution, --net_resolution_dynamic, --scale_number, --scale_gap
     int in_net_w_ = -1, in_net_h_ = 368, scale_number_ = 1;
     float dyn_ = 1.f;

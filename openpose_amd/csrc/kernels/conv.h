@@ -54,10 +54,16 @@ struct ConvArgs {
     // The K loop runs three passes over the input channels -- x_hi * w_hi, x_lo * w_hi,
     // x_hi * w_lo (weights packed [cout_pad/BN][3 * cin_pad/32][ky][kx][BN][32], pass-major) --
     // each product exact in fp32, so only the fp32 summation and the dropped x_lo * w_lo term
-    // (~2^-22 relative) separate the result from an fp32 convolution.
+    // (~2^-22 relative) separate the result from an fp32 convolution.  The weights are packed
+    // scaled by a power of two per layer, w' = w * 2^e with max |w'| in [2^14, 2^15), so w_lo is
+    // a normal fp16 number (a He-init weight of ~0.03 would otherwise leave w - w_hi in fp16's
+    // subnormal range, ~8 bits); the epilogue multiplies the sums by wscale = 2^-e before the
+    // bias (exact: a power of two).  Kernels: conv3_kernel, conv3w8_kernel and conv_image_kernel
+    // (SPLIT instantiations; the fp16 instantiations ignore wscale).
     int split;
     const uint16_t* in_lo;
     uint16_t* dst_lo[kConvMaxDst];
+    float wscale;
 };
 
 // conv3.hip: 7x7, 3x3 and 1x1, input halo staged once per 32-channel chunk over a "virtual image" of
@@ -143,10 +149,6 @@ void launch_conv1_fused(const Conv1FusedArgs& a, int workgroups, hipStream_t str
 void launch_maxpool2_split(uint16_t* out, uint16_t* out_lo, const uint16_t* in, const uint16_t* in_lo,
                            int frames, int H, int W, int C, int OH, int OW, hipStream_t stream,
                            int border);
-// split precision, the first conv's input: fp32 NCHW [frames][3][H][W] -> padded NHWC fp16 hi / lo
-// images of `cs` channels (3 used, the rest zero; border zero)
-void launch_image_split(uint16_t* hi, uint16_t* lo, int cs, const float* image, int frames, int H,
-                        int W, int border, hipStream_t stream);
 void launch_maxpool2(uint16_t* out, const uint16_t* in, int frames, int H, int W, int C, int OH,
                      int OW, hipStream_t stream, int border = 1);
 

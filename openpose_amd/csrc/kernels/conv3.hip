@@ -288,7 +288,8 @@ void conv3_kernel(const ConvArgs a)
                 uint32_t pk[2][2], pl[2][2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const float4_t t = acc[i][j + h] + bv[j + h];
+                    // (split: the sums of the 2^e-scaled weights times 2^-e, exact; conv.h)
+                    const float4_t t = (SPLIT ? acc[i][j + h] * a.wscale : acc[i][j + h]) + bv[j + h];
                     const float4_t tm = t * mv[j + h];
                     float v[4];
 #pragma unroll
@@ -332,7 +333,7 @@ void conv3_kernel(const ConvArgs a)
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
             // packed f32 math (v_pk_add/v_pk_mul) and v_cvt_pk_f16_f32 (round to nearest even)
-            const float4_t t = acc[i][j] + bj;
+            const float4_t t = (SPLIT ? acc[i][j] * a.wscale : acc[i][j]) + bj;
             const float4_t tm = t * mj;
             float v[4];
 #pragma unroll
@@ -814,7 +815,15 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     // the fragment reads per MFMA; removed, source and numbers in profiles/round3/wino/)
     // several 128-channel n-blocks (the VGG 256 / 512-channel layers): conv3w8 with one n-block
     // per persistent block (bit-identical; CONV3W8N=0: the 16-wave conv3_kernel)
-    // (split precision runs the plain conv3_kernel below: its K loop knows the three passes)
+    // split precision: every 512-position 96 / 128 / 256 / 512-channel 3x3 layer on conv3w8's split
+    // instantiation (bit-identical to conv3_kernel's; SPLIT_W8=0: conv3_kernel, A/B) -- its three
+    // times longer K loop is the regime where conv3w8 keeps the MFMA pipe busiest; the rest
+    // (several destinations, the 64-channel full-resolution layer, 1x1 heads) on conv3_kernel
+    if (a.split && s.nw == 16 && s.persist && s.bn != 64 && a.sink && !a.out32 && VW > 16 &&
+        dev_switch("SPLIT_W8", 1) != 0 && conv3w8_supported(a)) {
+        launch_conv3w8(a, stream);
+        return;
+    }
     if (!a.split && s.nw == 16 && s.persist && nn > 1 && s.bn == 128 && a.sink && !a.out32 && VW > 16 &&
         dev_switch("CONV3W8N", 1) != 0 && conv3w8_supported(a)) {
         launch_conv3w8(a, stream);

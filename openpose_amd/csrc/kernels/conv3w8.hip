@@ -60,9 +60,14 @@ typedef unsigned int opk8_u4 __attribute__((ext_vector_type(4)));
 #define OPK_FAULT_POOL 0
 #endif
 
-template <int BN, int NB, bool POOL, bool MX, bool BST>
+// SPLIT: split precision (ConvArgs::split, conv.h): K runs over three passes of the input chunks
+// (x_hi w_hi, x_lo w_hi, x_hi w_lo; the halo DMA of pass 1 reads the lo twin), in the order of
+// conv3_kernel<..., SPLIT>, and the epilogue writes hi = fp16(v) and lo = fp16(v - hi) of
+// v = act(acc * wscale + bias) -- bit-identical to conv3_kernel's split instantiations.
+template <int BN, int NB, bool POOL, bool MX, bool BST, bool SPLIT>
 __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a)
 {
+    static_assert(!(POOL && SPLIT), "split precision: the pools run as their own kernel");
     constexpr int NW = k8_NW, BM = k8_BM, HR = k8_HR;
     constexpr int WROWS = BM / NW, MF = WROWS / 16, NF = BN / 16;
     static_assert(WROWS == 64 && (NF == 8 || NF == 6), "wave tiles 64 x 128 / 64 x 96");
@@ -114,7 +119,8 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
 
     const int lrow = lane >> 2, phys = lane & 3;
     const int cpt = a.cin_pad >> 5;
-    const int U = 3 * cpt;
+    const int cptk = SPLIT ? 3 * cpt : cpt;   // K chunks (split: three passes over the input's)
+    const int U = 3 * cptk;
     const int ublk = nblk * U;   // the n-block's first K unit in the packed weights
     const int bi = (BPI - wave + NW - 1) / NW;
     // weight piece of B DMA instruction j (recomputed at each issue: registers)
@@ -125,6 +131,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         rb_ * 32 + (phys ^ (((rb_ >> 2) & 1) << 1)) * 8;                                      \
     })
     const char* abase = reinterpret_cast<const char*>(a.in + a.in_coff - a.in_cs);
+    const char* abase_lo = SPLIT ? reinterpret_cast<const char*>(a.in_lo + a.in_coff - a.in_cs) : abase;
     uint32_t aoff[AIW];
 #define OPK8_AROW1(mt_, i_)                                                                   \
     ({                                                                                        \
@@ -142,10 +149,13 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     do {                                                                                      \
         if ((ky_) == 0 && (OPK8_ABLATE != 7 || !dma_ab)) {                                    \
             const int as_ = (aslot_) * ASLOT;                                                 \
+            /* split: pass 1 reads the lo twin, passes 0 and 2 the hi image */                \
+            const int ps_ = !SPLIT ? 0 : (c_) >= 2 * cpt ? 2 : ((c_) >= cpt ? 1 : 0);          \
+            const char* ab_ = ps_ == 1 ? abase_lo : abase;                                    \
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
                 if (API % NW == 0 || i_ * NW + wave < API)                                    \
                     __builtin_amdgcn_global_load_lds(                                         \
-                        (const void*)(abase + (c_) * 64 +                                     \
+                        (const void*)(ab_ + ((c_) - ps_ * cpt) * 64 +                          \
                                       ((nt_) ? OPK8_AROW1(m + GM, i_) : aoff[i_])),            \
                         (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * NW + wave) * 64]), \
                         16, 0, 0);                                                            \
@@ -291,16 +301,16 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
             const bool nt = u + 1 >= U;
             const int u1 = nt ? 0 : u + 1;
             const int c1 = u1 / 3, ky1 = u1 - 3 * (u1 / 3);
-            const int aslot1 = (gc + (nt ? cpt : 0) + c1) & 1;
+            const int aslot1 = (gc + (nt ? cptk : 0) + c1) & 1;
             const uint32_t nab = OPK8_ABASE(aslot1, ky1, 0);
             const uint32_t nbb = OPK8_BBASE((u + 1) % 3);
-            constexpr int S1 = MF * (NF / 2);   // epilogue stores per wave
+            constexpr int S1 = MF * (NF / 2) * (SPLIT ? 2 : 1);   // epilogue stores per wave
 #define OPK8_DMA_U2()                                                                         \
     do {                                                                                      \
         const bool nt_ = u + 2 >= U;                                                          \
         const int u2_ = nt_ ? u + 2 - U : u + 2;                                              \
         const int c2_ = u2_ / 3;                                                              \
-        OPK8_ISSUE(c2_, u2_ - 3 * c2_, (gc + (nt_ ? cpt : 0) + c2_) & 1, (u + 2) % 3, nt_);  \
+        OPK8_ISSUE(c2_, u2_ - 3 * c2_, (gc + (nt_ ? cptk : 0) + c2_) & 1, (u + 2) % 3, nt_); \
     } while (0)
             OPK8_TAP(0, ab0, ab1, bb_u, BN * 64, fbE, fbO);
             OPK8_TAP(1, ab1, ab2, bb_u, 2 * BN * 64, fbO, fbE);
@@ -351,6 +361,9 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         uint16_t* const d0 = a.dst[0] + a.dst_coff[0] + nblk * BN;
         const int cs0 = a.dst_cs[0];
         const __amdgpu_buffer_rsrc_t rs0 = buf_rsrc(d0);
+        // split: the lo twin of the destination (same layout and offsets)
+        uint16_t* const d0lo = SPLIT ? a.dst_lo[0] + a.dst_coff[0] + nblk * BN : d0;
+        const __amdgpu_buffer_rsrc_t rs0lo = buf_rsrc(d0lo);
         if constexpr (POOL) {
             // pooled position of each fragment's lane pair; phase 1 = the window's first row
             int qrow[MF];
@@ -385,7 +398,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
             __builtin_amdgcn_s_barrier();
             // (the slot bases are 256-byte aligned, so fragment pair j's piece is the lane's piece
             // for j = 0 with bits 6-7 flipped by 32 j: one XOR per access, four address registers)
-            char* const xch = reinterpret_cast<char*>(lds + ((gc + cpt - 1) & 1) * ASLOT);
+            char* const xch = reinterpret_cast<char*>(lds + ((gc + cptk - 1) & 1) * ASLOT);
             uint32_t xoff[MF];
 #pragma unroll
             for (int i = 0; i < MF; ++i) {
@@ -471,30 +484,50 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
             }
 #pragma unroll
             for (int i = 0; i < MF; ++i) {
-                uint32_t pk[2][2];
+                uint32_t pk[2][2], pl[2][2];
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const float4_t t = acc[i][j + h] + bq[h];
+                    // (split: the sums of the 2^e-scaled weights times 2^-e, exact; conv.h)
+                    const float4_t t = (SPLIT ? acc[i][j + h] * a.wscale : acc[i][j + h]) + bq[h];
                     const float4_t v = act_pick4<MX>(t, t * mq[h]);
-                    pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.xy, half2_t));
-                    pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.zw, half2_t));
+                    const half2_t h01 = __builtin_convertvector(v.xy, half2_t);
+                    const half2_t h23 = __builtin_convertvector(v.zw, half2_t);
+                    pk[h][0] = __builtin_bit_cast(uint32_t, h01);
+                    pk[h][1] = __builtin_bit_cast(uint32_t, h23);
+                    if constexpr (SPLIT) {   // lo = fp16(v - hi) (v - hi is exact in fp32)
+                        pl[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                            v.xy - __builtin_convertvector(h01, float2_t), half2_t));
+                        pl[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                            v.zw - __builtin_convertvector(h23, float2_t), half2_t));
+                    }
                 }
                 const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
                 const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
                 const uint4 val = make_uint4(sl[0], sh[0], sl[1], sh[1]);
+                uint4 lval = make_uint4(0, 0, 0, 0);
+                if constexpr (SPLIT) {
+                    const auto ll = __builtin_amdgcn_permlane16_swap(pl[0][0], pl[1][0], false, false);
+                    const auto lh = __builtin_amdgcn_permlane16_swap(pl[0][1], pl[1][1], false, false);
+                    lval = make_uint4(ll[0], lh[0], ll[1], lh[1]);
+                }
                 const int ch = cw + j * 16;
                 if constexpr (BST) {
                     const uint32_t off = pok[i] ? (__umul24((uint32_t)prow[i], (uint32_t)cs0) + ch) * 2 : kBufOOB;
                     __builtin_amdgcn_raw_buffer_store_b128((opk8_u4){val.x, val.y, val.z, val.w}, rs0,
                                                            (int)off, 0, 0);
+                    if constexpr (SPLIT)
+                        __builtin_amdgcn_raw_buffer_store_b128((opk8_u4){lval.x, lval.y, lval.z, lval.w},
+                                                               rs0lo, (int)off, 0, 0);
                 } else if (nd == 1) {
-                    uint4* p = reinterpret_cast<uint4*>(d0 + ch + (size_t)prow[i] * cs0);
-                    *(pok[i] ? p : sink4) = val;
+                    const size_t o = ch + (size_t)prow[i] * cs0;
+                    *(pok[i] ? reinterpret_cast<uint4*>(d0 + o) : sink4) = val;
+                    if constexpr (SPLIT) *(pok[i] ? reinterpret_cast<uint4*>(d0lo + o) : sink4) = lval;
                 } else {
                     for (int d = 0; d < nd; ++d) {
-                        uint4* p = reinterpret_cast<uint4*>(a.dst[d] + a.dst_coff[d] + nblk * BN + ch +
-                                                            (size_t)prow[i] * a.dst_cs[d]);
-                        *(pok[i] ? p : sink4) = val;
+                        const size_t o = a.dst_coff[d] + nblk * BN + ch + (size_t)prow[i] * a.dst_cs[d];
+                        *(pok[i] ? reinterpret_cast<uint4*>(a.dst[d] + o) : sink4) = val;
+                        if constexpr (SPLIT)
+                            *(pok[i] ? reinterpret_cast<uint4*>(a.dst_lo[d] + o) : sink4) = lval;
                     }
                 }
             }
@@ -506,7 +539,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
             for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
         if (!has_next) break;
         m = mn;
-        gc += cpt;
+        gc += cptk;
         OPK8_AROW(aoff, m);
     }
 #undef OPK8_TAP
@@ -567,19 +600,26 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
                         a.dst_cs[0] * 2;
     const long pextent = ((long)a.frames * (a.H / 2 + 2) * (a.W / 2 + 2) + kConvGuardTail) * a.dst_cs[0] * 2;
     b.bufst = a.ndst == 1 && (pool ? pextent : extent) < (1L << 31) - 4096 && dev_switch("BUFST", 1) != 0;
+#define OPK8_LAUNCH3(BN_, NB_, P_, MX_, SP_)                                                     \
+    do {                                                                                        \
+        note_launch("conv3w8_kernel<%d,%d,%d,%d,%d%s>", BN_, NB_, (int)P_, (int)MX_, b.bufst,     \
+                    SP_ ? ",split" : "");                                                       \
+        if (b.bufst)                                                                            \
+            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, MX_, true, SP_>), dim3(G), dim3(64 * k8_NW), 0, stream, b); \
+        else                                                                                    \
+            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, MX_, false, SP_>), dim3(G), dim3(64 * k8_NW), 0, stream, b); \
+    } while (0)
 #define OPK8_LAUNCH2(BN_, NB_, P_, MX_)                                                          \
     do {                                                                                        \
-        note_launch("conv3w8_kernel<%d,%d,%d,%d,%d>", BN_, NB_, (int)P_, (int)MX_, b.bufst);      \
-        if (b.bufst)                                                                            \
-            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, MX_, true>), dim3(G), dim3(64 * k8_NW), 0, stream, b); \
-        else                                                                                    \
-            hipLaunchKernelGGL((conv3w8_kernel<BN_, NB_, P_, MX_, false>), dim3(G), dim3(64 * k8_NW), 0, stream, b); \
+        if (P_ || !a.split) OPK8_LAUNCH3(BN_, NB_, P_, MX_, false);                             \
+        else OPK8_LAUNCH3(BN_, NB_, false, MX_, true);                                          \
     } while (0)
 #define OPK8_LAUNCH(BN_, NB_, P_)                                                                \
     do {                                                                                        \
         if (a.actmax) OPK8_LAUNCH2(BN_, NB_, P_, true);                                         \
         else OPK8_LAUNCH2(BN_, NB_, P_, false);                                                 \
     } while (0)
+    OPK_CHECK_ARG(!a.split || (!pool && a.in_lo && a.dst_lo[0]), "conv3w8 split: lo twins, no pool");
     if (pool) {
         if (nb == 4) OPK8_LAUNCH(128, 4, true);
         else if (nb == 2) OPK8_LAUNCH(128, 2, true);
@@ -590,6 +630,7 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
     else OPK8_LAUNCH(96, 1, false);
 #undef OPK8_LAUNCH
 #undef OPK8_LAUNCH2
+#undef OPK8_LAUNCH3
     OPK_LAUNCH_CHECK();
 }
 

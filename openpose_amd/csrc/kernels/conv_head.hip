@@ -64,9 +64,13 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     constexpr int N2P = NF2 * 16;
     constexpr int ASLOT = BM * 4, BSLOT = N1 * 4;            // 16-byte pieces per ring slot
     constexpr int RING = 3 * (ASLOT + BSLOT);
-    // partial products (float4 pieces), rows padded by one piece: at N2P / 4 pieces a row, the 16
-    // rows of a fragment fall on the same banks (PMC: 60 % of the LDS cycles were bank conflicts)
-    constexpr int PSTRIDE = N2P / 4 + 1;
+    // partial products (float4 pieces), N2P / 4 pieces a row, the piece column XOR-swizzled by the
+    // row (OPKH_PART): unswizzled, the 16 rows of a fragment fall on the same banks (round 2 PMC:
+    // 60 % of the LDS cycles were bank conflicts); padded by one piece (round 2-5) the writes were
+    // conflict-free but every read instruction paid one extra LDS cycle (round-5 PMC: 0.071 of the
+    // LDS cycles at <512, 4>); with the XOR both are conflict-free in the lane-group model of
+    // MI355X_MICROARCH.md §LDS (tools/lds_conflicts.py head_partials)
+    constexpr int PSTRIDE = N2P / 4;
     constexpr int PART = NW * WROWS * PSTRIDE;
     constexpr int MAIN = RING > PART ? RING : PART;
     constexpr int LDS_PIECES = MAIN + N1 / 2;                 // + bias / multiplier of Mconv6
@@ -318,12 +322,13 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     // ---- phase 3: sum the wave columns' partials in order, + bias, outputs ---------------------
     __syncthreads();   // every wave is past its last ring read
     float4_t* part = reinterpret_cast<float4_t*>(lds);
-    // partial of wave w: [WROWS positions][N2P channels] fp32
+    // partial of wave w: [WROWS positions][N2P channels] fp32; piece (row, c) at OPKH_PART
+#define OPKH_PART(row_, c_) ((row_) * PSTRIDE + ((c_) ^ ((row_) & (PSTRIDE - 1))))
 #pragma unroll
     for (int i = 0; i < MF; ++i)
 #pragma unroll
         for (int f = 0; f < NF2; ++f)
-            part[(wave * WROWS + i * 16 + r16) * PSTRIDE + f * 4 + q] = acc2[i][f];
+            part[OPKH_PART(wave * WROWS + i * 16 + r16, f * 4 + q)] = acc2[i][f];
     __syncthreads();
     // this lane's sums: output fragments f = wn, wn + WN1, ... of its wave row
     constexpr int NFO = (NF2 + WN1 - 1) / WN1;
@@ -335,10 +340,9 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         const float4_t b7 = *reinterpret_cast<const float4_t*>(a.b7 + f * 16 + 4 * q);   // zero-padded to N2P
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
-            const int row = wm * WROWS + i * 16 + r16;
-            float4_t v = part[((wm * WN1) * WROWS + row - wm * WROWS) * PSTRIDE + f * 4 + q];
+            float4_t v = part[OPKH_PART((wm * WN1) * WROWS + i * 16 + r16, f * 4 + q)];
             for (int w = 1; w < WN1; ++w)
-                v = v + part[((wm * WN1 + w) * WROWS + row - wm * WROWS) * PSTRIDE + f * 4 + q];
+                v = v + part[OPKH_PART((wm * WN1 + w) * WROWS + i * 16 + r16, f * 4 + q)];
             outv[k][i] = v + b7;
         }
     }
@@ -416,6 +420,7 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     }   // tiles
 #undef OPKH_ISSUE
 #undef OPKH_ASRC
+#undef OPKH_PART
 }
 
 }  // namespace

@@ -8,6 +8,11 @@
 // (ky*3 + kx)*3 + ci, zero past 27), the weights of all 64 output channels stay in registers,
 // and the MFMAs compute C^T so each lane stores 4 consecutive output channels (8 bytes) of one
 // pixel.  Replaces the im2col image + 1-step GEMM of conv.hip (two passes over HBM).
+// SPLIT (ConvArgs::split, net.h kPrecisionSplit): the weight rows carry w_lo = fp16(w - w_hi) in
+// their second 32 halves, each input value is split as x_hi = fp16(x), x_lo = fp16(x - x_hi) in
+// the gather, the three products x_hi w_hi, x_lo w_hi, x_hi w_lo accumulate in that order (the
+// pass order of conv3_kernel's split K loop), and the epilogue scales the sums by wscale (the
+// weights are packed times 2^e, conv.h) and writes hi = fp16(v) and lo = fp16(v - hi) to dst / dst_lo.
 #include "conv.h"
 
 #include "../common.h"
@@ -30,6 +35,7 @@ __device__ __forceinline__ uint16_t f2h_bits_i(float v)
     return __builtin_bit_cast(uint16_t, h);
 }
 
+template <bool SPLIT>
 __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const float* __restrict__ img)
 {
     __shared__ float tile[3 * (TH + 2) * LW];
@@ -56,7 +62,7 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
 
     const int r16 = lane & 15, q = lane >> 4;
     // weights (A operand of C^T): rows = output channels g*16 + r16, K = 8q .. 8q+7; row stride 64
-    half8_t wf[NG];
+    half8_t wf[NG], wl[NG];
     float4_t bv[NG], mv[NG];
     const float neg = a.act == 1 ? 0.f : 1.f;
 #pragma unroll
@@ -64,6 +70,9 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
         const int co = g * 16 + r16;
         wf[g] = co < a.cout ? *reinterpret_cast<const half8_t*>(a.w + (size_t)co * 64 + 8 * q)
                             : half8_t{0, 0, 0, 0, 0, 0, 0, 0};
+        if constexpr (SPLIT)
+            wl[g] = co < a.cout ? *reinterpret_cast<const half8_t*>(a.w + (size_t)co * 64 + 32 + 8 * q)
+                                : half8_t{0, 0, 0, 0, 0, 0, 0, 0};
         const int ch = g * 16 + 4 * q;   // bias/slope arrays are zero-padded to 128 channels
         bv[g] = *reinterpret_cast<const float4_t*>(a.bias + ch);
         const float4_t sl = *reinterpret_cast<const float4_t*>(a.slope + ch);
@@ -82,19 +91,31 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
     const int y = y0 + wave;
     if (y >= H) return;
     uint16_t* dbase[kConvMaxDst];
-    for (int d = 0; d < a.ndst; ++d)
-        dbase[d] = a.dst[d] + ((size_t)f * (H + 2 * B) + y + B) * (W + 2 * B) * a.dst_cs[d] + a.dst_coff[d];
+    uint16_t* dlo[kConvMaxDst];
+    for (int d = 0; d < a.ndst; ++d) {
+        const size_t o = ((size_t)f * (H + 2 * B) + y + B) * (W + 2 * B) * a.dst_cs[d] + a.dst_coff[d];
+        dbase[d] = a.dst[d] + o;
+        dlo[d] = SPLIT ? a.dst_lo[d] + o : nullptr;
+    }
 #pragma unroll
     for (int grp = 0; grp < TW / 16; ++grp) {
         const int xl = grp * 16 + r16;
-        half8_t xf;
+        half8_t xf, xl8;
 #pragma unroll
-        for (int e = 0; e < 8; ++e)
-            xf[e] = off[e] >= 0 ? (_Float16)tile[off[e] + wave * LW + xl] : (_Float16)0.f;
+        for (int e = 0; e < 8; ++e) {
+            const float xv = off[e] >= 0 ? tile[off[e] + wave * LW + xl] : 0.f;
+            xf[e] = (_Float16)xv;
+            if constexpr (SPLIT) xl8[e] = (_Float16)(xv - (float)xf[e]);
+        }
         float4_t acc[NG];
 #pragma unroll
-        for (int g = 0; g < NG; ++g)
+        for (int g = 0; g < NG; ++g) {
             acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[g], xf, float4_t{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+            if constexpr (SPLIT) {
+                acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[g], xl8, acc[g], 0, 0, 0);
+                acc[g] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl[g], xf, acc[g], 0, 0, 0);
+            }
+        }
         const int x = x0 + xl;
         if (x >= W) continue;
 #pragma unroll
@@ -104,13 +125,26 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
             float v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const float t = acc[g][r] + bv[g][r];
+                // (split: the sums of the 2^e-scaled weights times 2^-e, exact; ConvArgs::wscale)
+                const float t = (SPLIT ? acc[g][r] * a.wscale : acc[g][r]) + bv[g][r];
                 v[r] = t > 0.f ? t : t * mv[g][r];
             }
             const uint32_t lo = (uint32_t)f2h_bits_i(v[0]) | ((uint32_t)f2h_bits_i(v[1]) << 16);
             const uint32_t hi = (uint32_t)f2h_bits_i(v[2]) | ((uint32_t)f2h_bits_i(v[3]) << 16);
             for (int d = 0; d < a.ndst; ++d)
                 *reinterpret_cast<uint2*>(dbase[d] + (size_t)(x + B) * a.dst_cs[d] + ch) = make_uint2(lo, hi);
+            if constexpr (SPLIT) {   // the residues of the stored halves
+                uint16_t r[4];
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                    const uint16_t hb = f2h_bits_i(v[e]);
+                    r[e] = f2h_bits_i(v[e] - (float)__builtin_bit_cast(_Float16, hb));
+                }
+                const uint2 lv = make_uint2((uint32_t)r[0] | ((uint32_t)r[1] << 16),
+                                            (uint32_t)r[2] | ((uint32_t)r[3] << 16));
+                for (int d = 0; d < a.ndst; ++d)
+                    *reinterpret_cast<uint2*>(dlo[d] + (size_t)(x + B) * a.dst_cs[d] + ch) = lv;
+            }
         }
     }
 }
@@ -126,8 +160,14 @@ void launch_conv_image(const ConvArgs& a, const float* image, hipStream_t stream
         OPK_CHECK_ARG(((a.dst_cs[d] | a.dst_coff[d]) & 3) == 0, "conv_image: 8-byte aligned slices");
     const long blocks = (long)a.frames * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
     OPK_CHECK_ARG(blocks > 0 && blocks < (1L << 31), "conv_image: bad sizes");
-    note_launch("conv_image_kernel");
-    hipLaunchKernelGGL(conv_image_kernel, dim3((unsigned)blocks), dim3(256), 0, stream, a, image);
+    if (a.split) {
+        for (int d = 0; d < a.ndst; ++d) OPK_CHECK_ARG(a.dst_lo[d] != nullptr, "conv_image: split needs dst_lo");
+        note_launch("conv_image_kernel<split>");
+        hipLaunchKernelGGL(conv_image_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a, image);
+    } else {
+        note_launch("conv_image_kernel");
+        hipLaunchKernelGGL(conv_image_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a, image);
+    }
     OPK_LAUNCH_CHECK();
 }
 

@@ -25,6 +25,11 @@
 #include "heat_dev.h"
 #include "../common.h"
 
+// OPK_NMS_JUMP (dev A/B builds: 0): the walk leaves a cold source window in one jump
+#ifndef OPK_NMS_JUMP
+#define OPK_NMS_JUMP 1
+#endif
+
 namespace opk {
 
 namespace {
@@ -843,7 +848,25 @@ __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ 
                 tr0[n] = yp[n][0]; tr1[n] = yp[n][1];
                 bq0[n] = cp[n][0]; bq1[n] = cp[n][1];
             }
-            for (; y + 1 <= ylast; y += 2) {
+            while (y + 1 <= ylast) {
+                if constexpr (COLD && NS == 1 && OPK_NMS_JUMP) {
+                    // rows y .. of a cold window below a cold row: none is evaluated or tested,
+                    // so jump past all of them at once (their count from one load of the next 8
+                    // table entries)
+                    if (cold && cmid && tr0[0] == cur[0] && y + 8 <= ylast) {
+                        int k = 1;
+#pragma unroll
+                        for (int i = 1; i < 8; ++i) k += (k == i && yp[0][i] == cur[0]) ? 1 : 0;
+                        // (mid, the cold row above, already holds -inf; up is not read before
+                        // the next trip overwrites it: that trip skips the test of mid)
+                        y += k;
+                        yp[0] = yofs[0] + y;
+                        cp[0] = reinterpret_cast<const float4*>(ycoef[0]) + y;
+                        tr0[0] = yp[0][0]; tr1[0] = yp[0][1];
+                        bq0[0] = cp[0][0]; bq1[0] = cp[0][1];
+                        continue;
+                    }
+                }
                 int ntr0[NS], ntr1[NS];
                 float4 nbq0[NS], nbq1[NS];
 #pragma unroll
@@ -869,6 +892,7 @@ __global__ __launch_bounds__(64) void nms_detect_walk2_kernel(int* __restrict__ 
                     tr0[n] = ntr0[n]; tr1[n] = ntr1[n];
                     bq0[n] = nbq0[n]; bq1[n] = nbq1[n];
                 }
+                y += 2;
             }
         }
         for (; y < ye; ++y) {                                // the rest (tested rows h-2, h-1 among them)

@@ -14,6 +14,11 @@
 #include "heat_dev.h"
 #include "../common.h"
 
+// OPK_PAF_EXIT (dev A/B builds: 0): a line leaves its sample loop once it can no longer pass
+#ifndef OPK_PAF_EXIT
+#define OPK_PAF_EXIT 1
+#endif
+
 namespace opk {
 
 namespace {
@@ -54,6 +59,16 @@ __device__ __forceinline__ float2 heat_at_lds2(const HeatMap& M, const float* sr
     return M.nsrc > 1 ? make_float2(accx * M.inv_n, accy * M.inv_n) : make_float2(accx, accy);
 }
 
+// the fewest samples above inter_th with which the count test (float)c / (float)n > inter_min_above
+// passes (n + 1: never); the test is monotonic in c
+__device__ __forceinline__ int samples_needed(int n, float inter_min_above)
+{
+    int c = (int)fminf(fmaxf(inter_min_above * (float)n, 0.f), (float)n);
+    while (c > 0 && (float)(c - 1) / (float)n > inter_min_above) --c;
+    while (c <= n && !((float)c / (float)n > inter_min_above)) ++c;
+    return c;
+}
+
 // LDS: the x and y PAF planes' sources staged once per (pair, frame) workgroup (interleaved, see
 // heat_at_lds2); every sample of every candidate line then reads LDS instead of the L2/HBM source rows (dependent loads that set
 // the kernel's pace: ~2.4 ms per 64 BODY_135 frames, 152 pairs of ~20 x 20 candidates)
@@ -75,6 +90,12 @@ __device__ __forceinline__ float score_ab(const float* a, const float* b, const 
     const float stepx = vx / (float)n, stepy = vy / (float)n;
     float sum = 0.f;
     unsigned count = 0;
+    // a line with more than n - samples_needed() samples at or below inter_th cannot pass the
+    // count test below, whatever its other samples: it leaves the loop there (its result is the
+    // fallback, which does not depend on them) -- most candidate lines join parts of different
+    // people and fail within their first samples
+    const int maxfail = OPK_PAF_EXIT ? n - samples_needed(n, inter_min_above) : n;
+    int fails = 0;
     for (int s = 0; s < n; ++s) {
         const int px = max(0, min(W - 1, round_pos(a[0] + (float)s * stepx)));
         const int py = max(0, min(H - 1, round_pos(a[1] + (float)s * stepy)));
@@ -84,6 +105,8 @@ __device__ __forceinline__ float score_ab(const float* a, const float* b, const 
         if (v > inter_th) {
             sum += v;
             ++count;
+        } else if (++fails > maxfail) {
+            break;
         }
     }
     if ((float)count / (float)n > inter_min_above) return sum / (float)count;

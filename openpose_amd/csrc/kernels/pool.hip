@@ -100,26 +100,6 @@ __global__ __launch_bounds__(256) void maxpool2_split_kernel(uint16_t* __restric
     *reinterpret_cast<uint4*>(out_lo + opos * C + g * 8) = *reinterpret_cast<const uint4*>(ml);
 }
 
-// split precision, the first conv's input (see conv.h launch_image_split): one lane per pixel
-__global__ __launch_bounds__(256) void image_split_kernel(uint16_t* __restrict__ hi,
-                                                          uint16_t* __restrict__ lo, int cs,
-                                                          const float* __restrict__ img, int frames,
-                                                          int H, int W, int B)
-{
-    const size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= (size_t)frames * H * W) return;
-    const int x = (int)(idx % W), y = (int)((idx / W) % H), f = (int)(idx / ((size_t)W * H));
-    const size_t pos = ((size_t)f * (H + 2 * B) + y + B) * (W + 2 * B) + x + B;
-#pragma unroll
-    for (int c = 0; c < 3; ++c) {
-        const float v = img[(((size_t)f * 3 + c) * H + y) * W + x];
-        const _Float16 h = (_Float16)v;
-        const _Float16 l = (_Float16)(v - (float)h);
-        hi[pos * cs + c] = __builtin_bit_cast(uint16_t, h);
-        lo[pos * cs + c] = __builtin_bit_cast(uint16_t, l);
-    }
-}
-
 }  // namespace
 
 void launch_maxpool2_split(uint16_t* out, uint16_t* out_lo, const uint16_t* in, const uint16_t* in_lo,
@@ -132,17 +112,6 @@ void launch_maxpool2_split(uint16_t* out, uint16_t* out_lo, const uint16_t* in, 
     note_launch("maxpool2_split_kernel");
     hipLaunchKernelGGL(maxpool2_split_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
                        stream, out, out_lo, in, in_lo, frames, H, W, C, OH, OW, border);
-    OPK_LAUNCH_CHECK();
-}
-
-void launch_image_split(uint16_t* hi, uint16_t* lo, int cs, const float* image, int frames, int H,
-                        int W, int border, hipStream_t stream)
-{
-    OPK_CHECK_ARG(cs >= 3 && border >= 1 && frames > 0 && H > 0 && W > 0, "image split: sizes");
-    const size_t total = (size_t)frames * H * W;
-    note_launch("image_split_kernel");
-    hipLaunchKernelGGL(image_split_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0,
-                       stream, hi, lo, cs, image, frames, H, W, border);
     OPK_LAUNCH_CHECK();
 }
 

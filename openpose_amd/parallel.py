@@ -213,23 +213,32 @@ HEAD = 5   # record header: rank, step, first frame id, frames, payload floats
 
 
 class RecordGather:
-    """Gathers every rank's per-frame result records to rank 0 once per step, in frame order.
+    """Gathers every rank's per-frame result records to rank 0, in frame order.
 
     The reference's WQueueOrderer (include/openpose/thread/wQueueOrderer.hpp:62-141) re-sequences
     the datums that its per-GPU workers finish out of order.  Here the frames of step i are split
     into contiguous per-rank slices (rank r holds frames (i * world + r) * batch ...), each rank
     packs its slice's records (PoseExtractor.records(): per frame [people, keypoints, scores]),
-    and one gather per step (RCCL over xGMI on the GPU box, gloo on CPU) moves them to rank 0.
-    `finish()` on rank 0 returns the records of every frame in frame order and raises if a frame
-    is missing or duplicated.  `capacity` = floats per rank and step (records beyond it raise).
-    `collective`: move the records through the collective even at world size 1 (a process group
-    must exist) -- the 1-GPU box's test of the transport an N-GPU run uses (pinned staging,
-    events, dist.gather of device tensors, the device-side unpack)."""
+    and the records move to rank 0 (RCCL over xGMI on the GPU box, gloo on CPU) once per
+    `interval` steps: one gather of the group's blocks, the last (partial) group at finish();
+    interval <= 0: one gather of all steps, at finish().
+    A gather is a rendezvous of all ranks, so with interval 1 a rank that falls behind by one step
+    stalls every other rank at that step's gather (measured on gloo: tests/test_distributed.py
+    test_gather_interval_decouples_ranks); with interval k the ranks meet only every k steps --
+    interval 0 (bench.py's default) couples them only at finish(), as the reference's workers are
+    coupled only by its ordered output queue.  `finish()` on rank 0 returns the records of every frame in frame
+    order and raises if a frame is missing or duplicated.  `capacity` = floats per rank and step
+    (records beyond it raise).  `collective`: move the records through the collective even at
+    world size 1 (a process group must exist) -- the 1-GPU box's test of the transport an N-GPU
+    run uses (pinned staging, events, dist.gather of device tensors, the device-side unpack)."""
 
-    def __init__(self, world, rank, capacity, steps, device, group=None, collective=False):
+    def __init__(self, world, rank, capacity, steps, device, group=None, collective=False,
+                 interval=1):
         self.world, self.rank, self.steps, self.group = world, rank, steps, group
         self.device = torch.device(device)
         self.cap = int(capacity)
+        # (a group that never fills before the last step is gathered by finish())
+        self.interval = int(interval) if int(interval) > 0 else max(1, steps) + 1
         self.local = world == 1 and not collective
         if self.local:
             # nothing to move: the records stay on the host, one block per step (pages touched
@@ -238,19 +247,23 @@ class RecordGather:
             self.blocks.fill(-1.0)
             return
         cuda = self.device.type == "cuda"
-        self.send = torch.zeros(HEAD + self.cap, dtype=torch.float32, device=self.device)
-        # two host staging buffers: the upload of step i may still be in flight while step i+1
-        # packs (cuda: pinned memory + one event per buffer)
-        self.host = [torch.zeros(HEAD + self.cap, dtype=torch.float32, pin_memory=cuda)
+        g = min(self.interval, max(1, steps))   # staging rows
+        self.send = torch.zeros((g, HEAD + self.cap), dtype=torch.float32, device=self.device)
+        # two host staging groups: the upload of group k may still be in flight while group k+1
+        # packs (cuda: pinned memory + one event per group)
+        self.host = [torch.zeros((g, HEAD + self.cap), dtype=torch.float32, pin_memory=cuda)
                      for _ in range(2)]
         self.events = [torch.cuda.Event() if cuda else None for _ in range(2)]
-        self.recv = (torch.zeros((steps, world, HEAD + self.cap), dtype=torch.float32,
+        self.pending = 0          # steps packed into the current group, not yet gathered
+        self.gathered = 0         # steps already gathered
+        # rank-major, so that each rank's blocks of a group are one contiguous gather target
+        self.recv = (torch.zeros((world, steps, HEAD + self.cap), dtype=torch.float32,
                                  device=self.device) if rank == 0 else None)
         if self.recv is not None:
             # the device ops of finish() once here, so that their first-use costs (code object
             # loads on a GPU) fall outside any timed region
             self.recv[:, :, :HEAD].cpu()
-            torch.cat([self.recv[i, r, HEAD:HEAD + 1]
+            torch.cat([self.recv[r, i, HEAD:HEAD + 1]
                        for i in range(self.steps) for r in range(self.world)]).cpu()
 
     def push(self, step, first_frame, n_frames, records):
@@ -263,27 +276,44 @@ class RecordGather:
             blk[:HEAD] = (self.rank, step, first_frame, n_frames, n)
             blk[HEAD:HEAD + n] = records
             return
-        k = step % 2
-        if self.events[k] is not None and step >= 2:
-            self.events[k].synchronize()
-        h = self.host[k].numpy()
+        if step != self.gathered + self.pending:
+            raise RuntimeError("rank %d: step %d pushed out of order" % (self.rank, step))
+        grp = self.gathered // self.interval
+        k = grp % 2
+        if self.pending == 0 and self.events[k] is not None and grp >= 2:
+            self.events[k].synchronize()   # this staging group's previous upload has landed
+        h = self.host[k].numpy()[self.pending]
         h[:HEAD] = (self.rank, step, first_frame, n_frames, n)
         h[HEAD:HEAD + n] = records
-        self.send[:HEAD + n].copy_(self.host[k][:HEAD + n], non_blocking=True)
+        self.pending += 1
+        if self.pending == self.interval:
+            self._gather()
+
+    def _gather(self):
+        """One gather of the current group's blocks (all ranks have the same steps, so the same
+        groups)."""
+        g = self.pending
+        if g == 0:
+            return
+        k = (self.gathered // self.interval) % 2
+        self.send[:g].copy_(self.host[k][:g], non_blocking=True)
         if self.events[k] is not None:
             self.events[k].record()
-        dist.gather(self.send, list(self.recv[step].unbind(0)) if self.rank == 0 else None,
-                    dst=0, group=self.group)
+        s0 = self.gathered
+        dist.gather(self.send[:g], [self.recv[r, s0:s0 + g] for r in range(self.world)]
+                    if self.rank == 0 else None, dst=0, group=self.group)
+        self.gathered += g
+        self.pending = 0
 
     def _unpack_device(self):
         """(headers [steps, world, HEAD], the used part of every (step, rank) block, concatenated
         in (step, rank) order): two device-to-host copies, most of each worst-case-sized block
         stays behind."""
-        heads = self.recv[:, :, :HEAD].cpu().numpy()
+        heads = self.recv[:, :, :HEAD].transpose(0, 1).cpu().numpy()
         lens = heads[:, :, 4].astype(np.int64)
         if (lens < 0).any() or (lens > self.cap).any():
             raise RuntimeError("record headers hold impossible lengths: %s" % lens.tolist())
-        body = torch.cat([self.recv[i, r, HEAD:HEAD + int(lens[i, r])]
+        body = torch.cat([self.recv[r, i, HEAD:HEAD + int(lens[i, r])]
                           for i in range(self.steps) for r in range(self.world)]).cpu().numpy()
         return heads, body
 
@@ -291,6 +321,8 @@ class RecordGather:
         """Rank 0: every frame's record in frame order, as an OrderedRecords sequence of
         (keypoints [people, parts, 3], scores [people]); raises if a frame is missing or produced
         twice, or a block's records do not parse to its header's length."""
+        if not self.local:
+            self._gather()   # the last (partial) group
         if self.rank != 0:
             return None
         if self.local:   # headers and bodies in place (never-pushed steps: header -1)

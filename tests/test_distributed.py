@@ -85,6 +85,50 @@ def test_launcher_ordered_gather_gloo():
             np.testing.assert_array_equal(got["ks%d" % f], ks)
 
 
+@pytest.mark.parametrize("interval", [1, 2, 4, 7, 0])
+def test_launcher_ordered_gather_intervals(interval):
+    """The same flow with the records gathered once per `interval` steps (the last group partial
+    for 2 and 4 of 7 steps; 0 = once, at finish): every frame exactly once, in frame order."""
+    from tests.rank_stub import frame_result
+    steps, batch, parts = 7, 3, 25
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "res.npz")
+        stub = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rank_stub.py")
+        rc = parallel.launch_ranks(2, [stub, out, str(steps), str(batch), str(parts), str(interval)],
+                                   timeout=120)
+        assert rc == 0
+        got = np.load(out)
+        assert int(got["n"]) == 2 * steps * batch
+        for f in range(2 * steps * batch):
+            kp, ks = frame_result(f, parts)
+            np.testing.assert_array_equal(got["kp%d" % f], kp)
+            np.testing.assert_array_equal(got["ks%d" % f], ks)
+
+
+def test_gather_interval_decouples_ranks():
+    """rank 0 falls one step behind (sleeps 1.5 s before pushing step 1).  With
+    a gather per step (interval 1) rank 1 stalls in that step's gather until rank 0 arrives; with
+    the bench's interval (0: one gather, at finish) rank 1's step loop never waits for rank 0 -- the ranks
+    meet only at finish(), and the ordered records are the same."""
+    import json
+    steps, batch, parts, delay = 6, 2, 25, 1.5
+    stub = os.path.join(os.path.dirname(os.path.abspath(__file__)), "rank_stub.py")
+    loops = {}
+    for interval in (1, 0):
+        with tempfile.TemporaryDirectory() as d:
+            out = os.path.join(d, "res.npz")
+            rc = parallel.launch_ranks(2, [stub, out, str(steps), str(batch), str(parts), str(interval),
+                                           "0:1:%g" % delay], timeout=120)
+            assert rc == 0
+            assert int(np.load(out)["n"]) == 2 * steps * batch
+            loops[interval] = [json.load(open("%s.rank%d.json" % (out, r)))["loop_s"] for r in (0, 1)]
+    print("rank loop seconds, rank 0 delayed %.1f s at step 1: per-step gather %s, gather at "
+          "finish %s" % (delay, loops[1], loops[0]))
+    assert loops[1][1] >= 0.8 * delay        # coupled: rank 1 waited in step 1's gather
+    assert loops[0][1] < 0.3 * delay         # decoupled: rank 1 ran its steps without waiting
+    assert loops[0][0] >= delay              # (rank 0 did sleep)
+
+
 def test_launcher_propagates_failure():
     rc = parallel.launch_ranks(2, ["-c", "import os, sys; sys.exit(3 if os.environ['RANK'] == '1' "
                                          "else 0)"], timeout=60)

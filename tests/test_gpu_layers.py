@@ -143,3 +143,82 @@ def test_every_launch_within_fp16_bound(bench_net, record_property):
             assert (np.abs(got - ref) <= tol).all(), (b, f)
         off += ref.shape[1]
     assert off == 78
+
+
+# ---- split precision (opk_net_set_precision OPK_PRECISION_SPLIT) --------------------------------
+# The same bench geometry in split precision: every conv launch -- conv_image<split>, the 8-wave
+# conv3w8 split instantiations (96 / 128 channels, 2 and 4 n-blocks), conv3_kernel split for the
+# rest -- against the exact (float64) conv of the GPU's own hi + lo input blob (oracle/split.py).
+C_SPLIT = 2.0 ** -16   # fp32 accumulation + dropped lo*lo + weight residue (oracle/split.py)
+
+
+@pytest.fixture(scope="module")
+def split_net(ctx):
+    from bench import tile_aligned_batch
+    from openpose_amd.api import PRECISION_SPLIT
+    n = tile_aligned_batch(torch.cuda.get_device_properties(0).multi_processor_count)
+    graph = body25.layers()
+    params = random_params(graph, 31)
+    x = np.random.default_rng(32).uniform(-0.5, 0.5, (n, 3, NET_H, NET_W)).astype(np.float32)
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(params)
+    net.set_precision(PRECISION_SPLIT)
+    with dev_switches(LAUNCH_LOG=1):
+        net.forward(torch.from_numpy(x).cuda())
+    log = net.launch_log()
+    yield dict(net=net, graph=graph, params=params, x=x, n=n, log=log, frames=[0, n - 1])
+    net.close()
+
+
+def test_split_launch_log_uses_fused_kernels(split_net):
+    """Split precision runs the 8-wave persistent kernel's split instantiations for the 512-position
+    layers (1, 2 and 4 n-blocks of 128, and 96 channels) and the first conv on conv_image<split>;
+    every conv kernel is a split instantiation and every conv is in exactly one launch."""
+    inst = {k for _, k in split_net["log"]}
+    for nb in (1, 2, 4):
+        assert any(k.startswith("conv3w8_kernel<128,%d,0," % nb) and k.endswith(",split>") for k in inst), nb
+    assert any(k.startswith("conv3w8_kernel<96,1,0,") and k.endswith(",split>") for k in inst)
+    assert "conv_image_kernel<split>" in inst
+    convk = [k for k in inst if k.startswith(("conv3", "conv_image"))]
+    assert all("split" in k for k in convk), convk
+    assert not any(k.startswith(("conv3w_", "conv_head", "conv1_fused")) for k in inst), inst
+    # (the full-resolution layers of 130 frames run as frame runs: several launches, one layer)
+    named = {c for layer, _ in split_net["log"] if layer != "pool" for c in layer.split("+")}
+    convs = [l["name"] for l in split_net["graph"] if l["type"] == "Convolution"]
+    assert sorted(named) == sorted(convs)
+    print("%d launches: %s" % (len(split_net["log"]), sorted(inst)))
+
+
+def test_split_every_launch_within_bound(split_net, record_property):
+    """Each conv launch of the split-precision bench forward against the float64 conv of the GPU's
+    own hi + lo input blob (frames 0 and last): |gpu - ref| <= 2^-16 S + 2^-21 |ref| + 2^-24."""
+    from oracle import split as sp
+    net, graph, params = split_net["net"], split_net["graph"], split_net["params"]
+    worst = 0.0
+    rows = []
+    for layer, kernel in split_net["log"]:
+        if layer == "pool":
+            continue
+        u = emu.unit_from_launch(graph, layer)
+        frac = 0.0
+        for f in split_net["frames"]:
+            x = split_net["x"][f:f + 1] if u["input"] == "image" else net.blob(u["input"], (f, 1))
+            ref, tol = sp.unit(u, x, params, C_SPLIT)
+            got = net.blob(u["output"], (f, 1))   # (hi + lo; net_output heads: fp32)
+            assert got.shape == ref.shape, (layer, got.shape, ref.shape)
+            d = np.abs(got.astype(np.float64) - ref)
+            bad = d > tol
+            if bad.any():
+                i = np.unravel_index(np.argmax(d - tol), d.shape)
+                raise AssertionError("%s (%s) frame %d: %d of %d elements beyond the split bound; "
+                                     "worst at %s: gpu %r ref %r tol %r"
+                                     % (layer, kernel, f, int(bad.sum()), d.size, i, float(got[i]),
+                                        float(ref[i]), float(tol[i])))
+            frac = max(frac, float((d / tol).max()))
+        rows.append((layer, kernel, frac))
+        worst = max(worst, frac)
+    for layer, kernel, frac in rows:
+        print("%-40s %-40s %.3f of bound" % (layer, kernel, frac))
+    record_property("report_max_frac_of_split_bound", round(worst, 4))
+    record_property("report_split_worst_launch", max(rows, key=lambda r: r[2])[:2])
+

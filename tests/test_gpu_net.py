@@ -496,8 +496,8 @@ def test_body25_split_precision_vs_oracle(ctx, n, h, w):
         net.forward(xd)
         kernels = {k for _, k in net.launch_log()}
     got = net.output_numpy()
-    assert all("split" in k for k in kernels if k.startswith("conv3_kernel")), kernels
-    assert not any(k.startswith(("conv3w", "conv_head", "conv1_fused")) for k in kernels), kernels
+    assert all("split" in k for k in kernels if k.startswith(("conv3_kernel", "conv3w8", "conv_image"))), kernels
+    assert not any(k.startswith(("conv3w_", "conv_head", "conv1_fused")) for k in kernels), kernels
     ref = body25.forward(x, params, graph=graph)
     err, err16 = rel_l2(got, ref), rel_l2(fp16, ref)
     ch = channel_errors(got, ref)
@@ -546,3 +546,28 @@ def test_split_precision_large_batch_frame_runs(ctx):
     for f in (0, n // 2, n - 1):
         net.forward(torch.from_numpy(x[f:f + 1]).cuda())
         np.testing.assert_array_equal(got[f], net.output_numpy()[0])
+
+
+def test_split_precision_frame_runs_take_their_own_geometry(ctx):
+    """a batch whose frame runs are smaller than the whole batch may put a run into
+    another conv3 tile branch (another halo, so another strip count) than the planner chose for
+    the batch.  At 96x96 the 64-channel full-resolution layer (conv1_2, split precision) holds 1,711
+    frames per launch in 256-position tiles of two strips; 1,712 frames used to leave a 1-frame
+    tail, whose 37 tiles take the 512-position branch (one strip), and the forward threw.  Runs are
+    now even and each takes the geometry of its own frame count: every frame equals the frame
+    alone, bit for bit."""
+    from openpose_amd.api import PRECISION_SPLIT
+    n = 1712
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(synth.he_weights(net.convs(), seed=29))
+    net.set_precision(PRECISION_SPLIT)
+    x = np.random.default_rng(30).uniform(-0.5, 0.5, (n, 3, 96, 96)).astype(np.float32)
+    with dev_switches(LAUNCH_LOG=1):
+        net.forward(torch.from_numpy(x).cuda())
+        runs = sum(1 for layer, _ in net.launch_log() if layer == "conv1_2")
+    assert runs == 2, runs   # two even runs of 856 frames
+    got = net.output_numpy()
+    for f in (0, 855, 856, n - 1):
+        net.forward(torch.from_numpy(x[f:f + 1]).cuda())
+        np.testing.assert_array_equal(got[f], net.output_numpy()[0])
+    net.close()

@@ -642,3 +642,22 @@ def test_two_threads_own_contexts_concurrent(ctx):
                 np.testing.assert_array_equal(ks, rs)
             np.testing.assert_array_equal(peaks, ref[1])
             np.testing.assert_array_equal(heat, ref[2])
+
+
+def test_net_destroyed_before_its_pose_extractor(ctx):
+    """Net.close() while a PoseExtractor still refers to the net.  The extractor's
+    calls that need the net raise (NetHip::liveness), and destroying the extractor afterwards
+    -- whose destructor used to call into the dead net (forget_reader_events) -- is safe."""
+    from openpose_amd._lib import OpkError
+    net = Net(ctx, "builtin:BODY_25")
+    net.set_params(synth.he_weights(net.convs(), seed=3, out_scale=0.02))
+    pose = PoseExtractor(ctx, net)
+    x = torch.rand((1, 3, 64, 96), device="cuda") - 0.5
+    pose.forward(x, (96, 64))
+    pose.submit(x, (96, 64))   # leaves a post-processing reading the net's output buffer
+    pose.collect()
+    net.close()
+    with pytest.raises(OpkError, match="destroyed before"):
+        pose.forward(x, (96, 64))
+    pose.close()
+    ctx.sync()

@@ -130,6 +130,39 @@ def conv1(ver):
     return tot
 
 
+def head_partials(N1, NF2, layout):
+    """conv_head_kernel phase 3 (the wave columns' Mconv7 partials through LDS): the ds_write_b128
+    of every (fragment, output block) and the ds_read_b128 of the in-order sums, per tile.
+    layout "pad1": rows of N2P/4 + 1 pieces (rounds 2-5); "xor": N2P/4 pieces, the piece column
+    XOR the row (round 6)."""
+    NW = 8
+    WN1 = N1 // 128
+    WM = NW // WN1
+    WROWS = 128 // WM
+    MF = WROWS // 16
+    N2P = NF2 * 16
+    if layout == "pad1":
+        P = lambda row, c: (row * (N2P // 4 + 1) + c) * 16
+    else:
+        P = lambda row, c: (row * (N2P // 4) + (c ^ (row & (N2P // 4 - 1)))) * 16
+    tot = {"partial ds_write_b128": [0, 0], "partial ds_read_b128": [0, 0]}
+    for wave in range(NW):
+        wm, wn = wave // WN1, wave % WN1
+        for i in range(MF):
+            for f in range(NF2):
+                b, e = cost("w128", [P(wave * WROWS + i * 16 + (l & 15), f * 4 + (l >> 4)) for l in range(64)])
+                tot["partial ds_write_b128"][0] += b
+                tot["partial ds_write_b128"][1] += e
+        for f in range(wn, NF2, WN1):
+            for i in range(MF):
+                for w in range(WN1):
+                    b, e = cost("r128", [P((wm * WN1 + w) * WROWS + i * 16 + (l & 15), f * 4 + (l >> 4))
+                                         for l in range(64)])
+                    tot["partial ds_read_b128"][0] += b
+                    tot["partial ds_read_b128"][1] += e
+    return tot
+
+
 if __name__ == "__main__":
     for ver in (3, 4, 5):
         tot = conv1(ver)
@@ -139,3 +172,7 @@ if __name__ == "__main__":
         B = sum(b for b, _ in tot.values())
         E = sum(e for _, e in tot.values())
         print("  extra / all LDS cycles: %.3f" % (E / (B + E)))
+    for n1, nf2 in ((512, 4), (512, 2), (256, 4), (256, 2)):
+        for layout in ("pad1", "xor"):
+            print("conv_head<%d,%d> phase-3 partials, %s layout: %s" % (n1, nf2, layout,
+                                                                     head_partials(n1, nf2, layout)))
