@@ -441,27 +441,30 @@ def _first(*rel):
 # records the commit and kernel-source digest it was collected at, reported beside the numbers
 # read from it): CNN HBM bytes per forward, time-weighted MFMA busy, and the post-processing
 # kernels' per-step VALU / HBM counts.  Their "batch" must equal the bench's frames per step.
-PMC_TRAFFIC = _first("round5/r5f/pmc/pmc_traffic.json", "round5/r5e/pmc/pmc_traffic.json", "round4/pmc/pmc_traffic.json")
-POST_PMC = _first("round5/r5f/pmc/report.json", "round5/r5e/pmc/report.json", "round4/pmc/report.json")
-POST_PMC_B135 = _first("round5/r5f/pmc_body135/report.json", "round5/r5e/pmc_body135/report.json", "round4/pmc_body135/report.json")
+PMC_TRAFFIC = _first("round6/pmc/pmc_traffic.json", "round5/r5f/pmc/pmc_traffic.json", "round4/pmc/pmc_traffic.json")
+POST_PMC = _first("round6/pmc/report.json", "round5/r5f/pmc/report.json", "round4/pmc/report.json")
+POST_PMC_B135 = _first("round6/pmc_body135/report.json", "round5/r5f/pmc_body135/report.json", "round4/pmc_body135/report.json")
+# split precision's CNN (bench.py --precision split): its own counter passes
+PMC_SPLIT_TRAFFIC = _first("round6/pmc_split/pmc_traffic.json")
+PMC_SPLIT = _first("round6/pmc_split/report.json")
 
 
-def pmc_traffic(batch):
+def pmc_traffic(batch, path=PMC_TRAFFIC):
     """HBM bytes of one CNN forward from the committed PMC summary (FETCH_SIZE x2 on gfx950 +
     WRITE_SIZE over every kernel of one forward), or None when it was taken at another batch."""
     try:
-        with open(PMC_TRAFFIC) as f:
+        with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
     return d.get("cnn_forward_hbm_bytes") if d.get("batch") == batch else None
 
 
-def pmc_mfma_busy(batch):
+def pmc_mfma_busy(batch, path=POST_PMC):
     """Time-weighted MFMA busy of the CNN's conv kernels (SQ_VALU_MFMA_BUSY_CYCLES over 1,024
     SIMDs x the cycles each launch ran) from the committed PMC report, or None at another batch."""
     try:
-        with open(POST_PMC) as f:
+        with open(path) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None
@@ -588,8 +591,10 @@ def extra_legs(args, timeout=240):
                "roofline": {k: rf.get(k) for k in ("bound", "kernel", "achieved", "peak", "unit", "frac",
                                                    "avg_launch_ms", "algorithmic_gflop_per_launch",
                                                    "mfma_passes_per_useful_flop", "pass_tflops",
-                                                   "frac_of_measured_random_operand_mfma")
+                                                   "frac_of_measured_random_operand_mfma", "mfma_busy",
+                                                   "traffic")
                             if k in rf},
+               "pmc_mfma_busy_source": (rf.get("pmc") or {}).get("mfma_busy"),
                "host_ms": d.get("host_ms")}
         if d.get("post_roofline"):
             pr = d["post_roofline"]
@@ -802,12 +807,17 @@ def rank_main(args, rank, world, local):
             "peak": PEAK_FP16_TFLOPS,
             "unit": "TFLOP/s",
             "frac": round(achieved / PEAK_FP16_TFLOPS, 4),
-            "traffic": pmc_traffic(B) if nscales == 1 and args.precision == "fp16" else None,
-            "mfma_busy": pmc_mfma_busy(B) if nscales == 1 and args.precision == "fp16" else None,
+            "traffic": (None if nscales != 1 else pmc_traffic(B) if args.precision == "fp16"
+                        else pmc_traffic(B, PMC_SPLIT_TRAFFIC)),
+            # time-weighted MFMA busy of the conv kernels (PMC; split: over its three passes)
+            "mfma_busy": (None if nscales != 1 else pmc_mfma_busy(B) if args.precision == "fp16"
+                          else pmc_mfma_busy(B, PMC_SPLIT)),
             "mfma_passes_per_useful_flop": 1 if args.precision == "fp16" else 3,
             # split: the MFMA work issued (three fp16 passes per useful FLOP)
             "pass_tflops": round(achieved * (1 if args.precision == "fp16" else 3), 2),
-            "pmc": {"traffic": pmc_provenance(PMC_TRAFFIC, "cnn"), "mfma_busy": pmc_provenance(POST_PMC, "cnn")},
+            "pmc": ({"traffic": pmc_provenance(PMC_TRAFFIC, "cnn"), "mfma_busy": pmc_provenance(POST_PMC, "cnn")}
+                    if args.precision == "fp16" else
+                    {"traffic": pmc_provenance(PMC_SPLIT_TRAFFIC, "cnn"), "mfma_busy": pmc_provenance(PMC_SPLIT, "cnn")}),
             "traffic_unit": "bytes per launch (HBM, PMC)",
             "algorithmic_gflop_per_launch": round(flops_frame * B / 1e9, 2),
             "avg_launch_ms": round(net_ms, 3),

@@ -280,9 +280,13 @@ int opk_net_flops_per_frame(opk_net* net, int h, int w, double* flops);
  *   tuned fused kernels -- net output within rel-L2 ~2.5e-3 of fp32 on random He-initialised
  *   BODY_25 nets.
  * OPK_PRECISION_SPLIT: every weight and activation held as an fp16 hi/lo pair (x = hi + lo to
- *   ~22 bits), three MFMA passes per conv (x_hi w_hi + x_lo w_hi + x_hi w_lo, each product exact in
- *   fp32): fp32-level results (parity mode) at ~3x the MFMA work and 2x the activation bytes, on
- *   the generic conv kernel with no fusion.  Re-plans the net's shapes; loaded weights are kept. */
+ *   ~22 bits; each layer's weights scaled by a power of two so that w_lo stays a normal fp16
+ *   number), three MFMA passes per conv (x_hi w_hi + x_lo w_hi + x_hi w_lo, each product exact in
+ *   fp32): fp32-level results (parity mode: as close to the exact convolution as an fp32 CPU
+ *   implementation is) at 3x the MFMA work and 2x the activation bytes -- the 512-position
+ *   persistent 8-wave kernel's split instantiation for every 96/128/256/512-channel 3x3 layer,
+ *   conv_image's for the first conv, the generic kernel for the rest; no conv1 / head / pool
+ *   fusion.  Re-plans the net's shapes; loaded weights are kept. */
 #define OPK_PRECISION_FP16 0
 #define OPK_PRECISION_SPLIT 1
 int opk_net_set_precision(opk_net* net, int precision);

@@ -251,14 +251,15 @@ void NetHip::plan(const std::vector<LayerDesc>& layers)
             fuse1_ = {steps_[0].idx, steps_[1].idx, steps_[2].idx, abuf, bbuf};
     }
     // conv -> pool pairs whose conv output only the pool reads (pool2 after conv2_2, pool3 after
-    // conv3_4 in BODY_25): candidates for the pool-fused conv3w8 epilogue
+    // conv3_4 in BODY_25; pool1 after conv1_2 where conv1_fused does not run -- split precision):
+    // candidates for the pool-fused conv3w8 epilogue (128k or 64 outputs)
     pool_conv_.assign(pools_.size(), -1);
     for (size_t si = 0; si + 1 < steps_.size(); ++si) {
         if (!steps_[si].conv || steps_[si + 1].conv) continue;
         const ConvPlan& c = convs_[steps_[si].idx];
         const PoolPlan& p = pools_[steps_[si + 1].idx];
         if (c.from_image || c.info.k != 3 || c.outs.size() != 1 || c.outs[0].coff != 0 ||
-            c.out32_coff >= 0 || c.info.cout % 128 != 0 || border_ != 1 || fuse1_.b == steps_[si].idx ||
+            c.out32_coff >= 0 || (c.info.cout % 128 != 0 && c.info.cout != 64) || border_ != 1 ||
             p.in_buf != c.outs[0].buf)
             continue;
         int readers = 0;
@@ -362,13 +363,14 @@ void NetHip::pack(ConvPlan& c)
                 dst[t * c.cin_pad + ci] = f2h(w[(((size_t)co * cin + ci) * k + ky) * k + kx]);
         }
     }
-    // conv3.hip layout: [cout_pad/BN][cin_pad/32][ky][kx][n BN][ci 32]; split precision: three
-    // passes of chunks, [cout_pad/BN][3][cin_pad/32]..., holding w_hi, w_hi, w_lo (ConvArgs::split)
+    // conv3.hip layout: [cout_pad/BN][cin_pad/32][ky][kx][n BN][ci 32]; split precision: two
+    // blocks of chunks, [cout_pad/BN][2][cin_pad/32]..., holding w_hi and w_lo -- the K loop's
+    // three products per chunk read w_hi, w_lo, w_hi (ConvArgs::split)
     std::vector<uint16_t> packed3;
     if (!c.from_image) {
         const int BN = conv3_shape(1, 1, 1, c.info.cout, k, border_).bn;   // BN depends on cout only
         const int nb = (c.info.cout + BN - 1) / BN, cpt = c.cin_pad / 32, kt = k * k;
-        const int passes = split ? 3 : 1;
+        const int passes = split ? 2 : 1;
         packed3.assign((size_t)nb * passes * cpt * kt * BN * 32, 0);
         for (int co = 0; co < c.info.cout; ++co)
             for (int ci = 0; ci < cin; ++ci)
@@ -378,8 +380,8 @@ void NetHip::pack(ConvPlan& c)
                     for (int ps = 0; ps < passes; ++ps) {
                         const size_t idx = ((((size_t)(co / BN) * passes * cpt + ps * cpt + ci / 32) * kt + t) *
                                                 BN + co % BN) * 32 + ci % 32;
-                        packed3[idx] = ps < 2 ? __builtin_bit_cast(uint16_t, hi)
-                                              : f2h(wv - (float)hi);
+                        packed3[idx] = ps == 0 ? __builtin_bit_cast(uint16_t, hi)
+                                               : f2h(wv - (float)hi);
                     }
                 }
     }
@@ -486,7 +488,7 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
     std::vector<uint16_t*>& ptr = S.base;
     ptr.assign(bufs_.size(), nullptr);
     // CONV1_FUSED=0 (opk_dev_set, A/B tests): the three separate kernels instead of the fusion
-    S.split = precision_ == kPrecisionSplit;   // (split precision: no fused kernel)
+    S.split = precision_ == kPrecisionSplit;   // (split precision: no conv1 / head fusion)
     S.fused1 = !S.split && fuse1_.a >= 0 && dev_switch("CONV1_FUSED", 1) != 0 && border_ == 1 &&
                conv1_fused_supported(h, w, 64, 64);
     // HEAD_FUSE=0 (opk_dev_set, A/B tests): Mconv6 and Mconv7 as two conv3 launches
@@ -501,10 +503,19 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
     S.poolfused.assign(pools_.size(), 0);
     for (size_t q = 0; q < pools_.size(); ++q) {
         const int ci = pool_conv_[q];
-        if (ci < 0 || S.split || dev_switch("POOL_FUSE", 1) == 0) continue;
+        if (ci < 0 || dev_switch("POOL_FUSE", 1) == 0) continue;
+        if (S.fused1 && (int)q == fuse1_.p) continue;   // (pool1 inside conv1_fused_kernel)
         const ConvPlan& c = convs_[ci];
         const int H = lh_[c.level], W = lw_[c.level];
-        const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, 3, border_);
+        // (64 outputs: conv3w8's BN = 64 tile, when the conv may take it -- conv3_w8_eligible)
+        std::vector<int> pcs, pco;
+        for (const auto& o : c.outs) {
+            pcs.push_back(bufs_[o.buf].cs);
+            pco.push_back(o.coff);
+        }
+        const bool w8 = !pcs.empty() && conv3_w8_eligible(c.info.cout, c.ntaps, (int)c.outs.size(),
+                                                          pcs.data(), pco.data(), c.out32_coff >= 0);
+        const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, 3, border_, w8);
         S.poolfused[q] = s3.persist && s3.nw == 16 && H % 2 == 0 && W % 2 == 0 && s3.sw % 2 == 0 &&
                          6 * (s3.sw + 2) <= 512 && s3.sw + 2 > 16 &&
                          lh_[c.level + 1] == H / 2 && lw_[c.level + 1] == W / 2;
@@ -565,7 +576,15 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
         S.use3[ci] = use3;
         OPK_CHECK_ARG(use3 || c.w.ptr != nullptr, c.info.name + ": weights not set");
         if (use3) {
-            const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, c.info.k, border_);
+            // (conv3w8's 64-output tile: decided from the destinations as launch_conv3 decides)
+            std::vector<int> dcs, dco;
+            for (const auto& o : c.outs) {
+                dcs.push_back(bufs_[o.buf].cs);
+                dco.push_back(o.coff);
+            }
+            const bool w8 = !dcs.empty() && conv3_w8_eligible(c.info.cout, a.ntaps, (int)c.outs.size(),
+                                                              dcs.data(), dco.data(), c.out32_coff >= 0);
+            const Conv3Shape s3 = conv3_shape(n, H, W, c.info.cout, c.info.k, border_, w8);
             a.sw = s3.sw;
             a.nstrips = s3.nstrips;
             a.sink = sink;
@@ -598,6 +617,7 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
                 a.pool = 1;
                 a.ndst = 1;
                 a.dst[0] = ptr[pools_[q].out_buf];
+                a.dst_lo[0] = S.base_lo[pools_[q].out_buf];   // (split precision: its lo twin)
                 a.dst_cs[0] = bufs_[pools_[q].out_buf].cs;
                 a.dst_coff[0] = 0;
             }
@@ -743,7 +763,7 @@ void NetHip::forward_launches(ShapePlan& S, const float* input, int n, int h, in
 // strip count) -- launch_conv3 requires the geometry of its own frame count.
 static bool conv3_run_fits(const ConvArgs& a, int frames, int ks, int B)
 {
-    const Conv3Shape s = conv3_shape(frames, a.H, a.W, a.cout, ks, B);
+    const Conv3Shape s = conv3_shape(frames, a.H, a.W, a.cout, ks, B, conv3_w8_eligible(a));
     const long total = (long)frames * s.nstrips * (a.H + 2 * B) * (s.sw + 2 * B);
     return total + s.bm + (long)(ks - 1) * (s.sw + 2 * B + 1) < (1L << 24);
 }
@@ -765,18 +785,20 @@ static void launch_conv3_frames(const ConvArgs& a, hipStream_t st)
     }
     const int run = (a.frames + runs - 1) / runs;
     const size_t frame_pos = (size_t)(a.H + 2 * B) * (a.W + 2 * B);   // padded image positions
+    // a pooled destination (conv3w8 POOL epilogue) holds the pooled padded image per frame
+    const size_t dst_pos = a.pool ? (size_t)(a.H / 2 + 2 * B) * (a.W / 2 + 2 * B) : frame_pos;
     for (int f0 = 0; f0 < a.frames; f0 += run) {
         ConvArgs b = a;
         b.frames = std::min(run, a.frames - f0);
-        const Conv3Shape sb = conv3_shape(b.frames, a.H, a.W, a.cout, ks, B);
+        const Conv3Shape sb = conv3_shape(b.frames, a.H, a.W, a.cout, ks, B, conv3_w8_eligible(a));
         b.sw = sb.sw;
         b.nstrips = sb.nstrips;
         b.M = b.frames * a.H * (a.W + 2 * B);
         b.in = a.in + f0 * frame_pos * a.in_cs;
         if (a.in_lo) b.in_lo = a.in_lo + f0 * frame_pos * a.in_cs;
         for (int d = 0; d < a.ndst; ++d) {
-            b.dst[d] = a.dst[d] + f0 * frame_pos * a.dst_cs[d];
-            if (a.dst_lo[d]) b.dst_lo[d] = a.dst_lo[d] + f0 * frame_pos * a.dst_cs[d];
+            b.dst[d] = a.dst[d] + f0 * dst_pos * a.dst_cs[d];
+            if (a.dst_lo[d]) b.dst_lo[d] = a.dst_lo[d] + f0 * dst_pos * a.dst_cs[d];
         }
         if (a.out32) b.out32 = a.out32 + (size_t)f0 * a.out32_c * a.H * a.W;
         launch_conv3(b, st);

@@ -48,11 +48,14 @@ struct ConvArgs {
                           // through a buffer resource (set by launch_conv3w)
     int pool;             // conv3w8: 2x2/2 max pool fused into the epilogue; dst[0] is the pooled
                           // padded image [frames][H/2+2][W/2+2][cs] (conv3w8_pool_supported)
+    int nbx;              // conv3w8, several n-blocks: XCD x computes n-block x % NB only, so an
+                          // XCD's L2 holds one n-block's weights (set by launch_conv3w8)
     // Split precision (NetHip precision OPK_PRECISION_SPLIT; conv3_kernel only): every activation
     // x is held as two fp16 images, hi = fp16(x) and lo = fp16(x - hi) (in_lo / dst_lo: the lo
     // twins, same layout and offsets), and every weight w as w_hi = fp16(w), w_lo = fp16(w - w_hi).
-    // The K loop runs three passes over the input channels -- x_hi * w_hi, x_lo * w_hi,
-    // x_hi * w_lo (weights packed [cout_pad/BN][3 * cin_pad/32][ky][kx][BN][32], pass-major) --
+    // The K loop runs three products per 32-channel input chunk, chunk-major -- x_hi * w_hi,
+    // x_hi * w_lo (the same staged hi halo), x_lo * w_hi (weights packed
+    // [cout_pad/BN][2 * cin_pad/32][ky][kx][BN][32]: the w_hi chunks, then the w_lo chunks) --
     // each product exact in fp32, so only the fp32 summation and the dropped x_lo * w_lo term
     // (~2^-22 relative) separate the result from an fp32 convolution.  The weights are packed
     // scaled by a power of two per layer, w' = w * 2^e with max |w'| in [2^14, 2^15), so w_lo is
@@ -81,7 +84,16 @@ struct Conv3Shape {
     int sw, nstrips;
     bool persist;                 // 16-wave tiles: persistent kernel (conv3p) when the launch allows
 };
-Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border = 1);
+// w8: the conv may run on conv3w8 (conv3_w8_eligible): 64-output 3x3 layers of >= 768 tiles then
+// take the persistent 512-position geometry of the 8-wave kernel
+Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border = 1, bool w8 = false);
+// a 64-output 3x3 conv that conv3w8's BN = 64 instantiation can run (one aligned destination, no
+// fp32 output, a persistent sink): the planner and the launchers decide the same way from it
+bool conv3_w8_eligible(int cout, int ntaps, int ndst, const int* dst_cs, const int* dst_coff, bool out32);
+inline bool conv3_w8_eligible(const ConvArgs& a)
+{
+    return a.sink && a.cus > 0 && conv3_w8_eligible(a.cout, a.ntaps, a.ndst, a.dst_cs, a.dst_coff, a.out32 != nullptr);
+}
 void launch_conv3(const ConvArgs& a, hipStream_t stream);
 // conv3w.hip: the persistent 512 x {128, 96} 3x3 variant with one mid-unit barrier per K unit
 // (launched by launch_conv3 for single-n-block layers on the persistent path)

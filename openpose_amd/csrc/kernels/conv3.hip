@@ -109,8 +109,10 @@ void conv3_kernel(const ConvArgs a)
     // ---- DMA lane geometry: 16 rows x 4 pieces per wave instruction --------------------------
     const int lrow = lane >> 2, phys = lane & 3;
     const int cpt = a.cin_pad >> 5;               // 32-channel chunks of the input
-    // split precision: three passes over the chunks (x_hi w_hi, x_lo w_hi, x_hi w_lo; conv.h)
-    const int cptk = SPLIT ? 3 * cpt : cpt;       // K chunks
+    // split precision: three products per input chunk c, chunk-major -- virtual chunk 3c + k,
+    // k = 0 x_hi w_hi, 1 x_hi w_lo (the hi halo of k = 0 again: no DMA), 2 x_lo w_hi (the lo
+    // twin's halo); hi halos in slot 0 (UPC == 1: slots 0 / 2 by chunk parity), lo halos in slot 1
+    const int cptk = SPLIT ? 3 * cpt : cpt;       // K (virtual) chunks
     const int U = UPC * cptk;                     // units (chunk, taps)
     const ptrdiff_t dlo = SPLIT ? a.in_lo - a.in : 0;   // hi -> lo twin (elements)
     // halo row hr = (i*8 + wave)*16 + lrow holds virtual position p0 - VW - 1 + hr; its image
@@ -128,17 +130,28 @@ void conv3_kernel(const ConvArgs a)
     // this wave issues halo instructions i*8 + wave < API and B instructions j*8 + wave < BPI
     const int ai = (API - wave + NW - 1) / NW;
     const int bi = (BPI - wave + NW - 1) / NW;
-    const uint16_t* wbase = a.w + (size_t)nb * cptk * KT * BN * 32;
+    // split: the packed weights hold w_hi and w_lo (2 cpt chunks per n-block); virtual chunk
+    // 3c + k reads w_lo chunk c (cpt + c) for k = 1, w_hi chunk c otherwise -- OPK3_WUNIT
+    const uint16_t* wbase = a.w + (size_t)nb * (SPLIT ? 2 * cpt : cpt) * KT * BN * 32;
+#define OPK3_WUNIT(u_)                                                                        \
+    (!SPLIT ? (u_) : ({                                                                       \
+        const int cc_ = (u_) / UPC;                                                           \
+        const int wc_ = cc_ % 3 == 1 ? cpt + cc_ / 3 : cc_ / 3;                               \
+        wc_ * UPC + ((u_) - cc_ * UPC);                                                       \
+    }))
+    // halo slot of virtual chunk c_ and whether its first unit issues a halo DMA
+#define OPK3_ASLOT(c_) (!SPLIT ? (c_) % NAS : ((c_) % 3 == 2 ? 1 : (UPC == 1 ? 2 * (((c_) / 3) & 1) : 0)))
+#define OPK3_HALO(c_) (!SPLIT || (c_) % 3 != 1)
 
 #define OPK3_ISSUE(u_)                                                                        \
     do {                                                                                      \
         const int c_ = (u_) / UPC;                                                            \
         /* dev probe only: 6 = no halo DMA, 7 = no weight DMA after the prologue */           \
-        if ((u_) - c_ * UPC == 0 && (OPK3_ABLATE != 6 || (u_) < 2)) {                        \
-            const int as_ = (c_ % NAS) * ASLOT;                                               \
-            /* split precision: pass 1 reads the lo twin; passes 0 and 2 the hi image */       \
-            const int ps_ = !SPLIT ? 0 : c_ >= 2 * cpt ? 2 : (c_ >= cpt ? 1 : 0);             \
-            const ptrdiff_t ao_ = (ptrdiff_t)(c_ - ps_ * cpt) * 32 + (ps_ == 1 ? dlo : 0);    \
+        if ((u_) - c_ * UPC == 0 && OPK3_HALO(c_) && (OPK3_ABLATE != 6 || (u_) < 2)) {       \
+            const int as_ = OPK3_ASLOT(c_) * ASLOT;                                           \
+            /* split: k = 2 reads the lo twin, k = 0 the hi image */                          \
+            const ptrdiff_t ao_ = !SPLIT ? (ptrdiff_t)c_ * 32                                  \
+                                         : (ptrdiff_t)(c_ / 3) * 32 + (c_ % 3 == 2 ? dlo : 0); \
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
                 if (API % NW == 0 || i_ * NW + wave < API)                                    \
                     __builtin_amdgcn_global_load_lds(                                         \
@@ -147,7 +160,7 @@ void conv3_kernel(const ConvArgs a)
                         16, 0, 0);                                                            \
         }                                                                                     \
         const int bs_ = NAS * ASLOT + ((u_) % 3) * BSLOT;                                     \
-        const uint16_t* ub_ = wbase + (size_t)(u_) * BROWS * 32;                              \
+        const uint16_t* ub_ = wbase + (size_t)OPK3_WUNIT(u_) * BROWS * 32;                    \
         _Pragma("unroll") for (int j_ = 0; j_ < (BPI + NW - 1) / NW; ++j_) {                  \
             if ((BPI % NW == 0 || j_ * NW + wave < BPI) && (OPK3_ABLATE != 7 || (u_) < 2)) {  \
                 const int rb_ = (j_ * NW + wave) * 16 + lrow;                                 \
@@ -190,7 +203,8 @@ void conv3_kernel(const ConvArgs a)
     for (int u = 0; u < U; ++u) {
         const int c = u / UPC, t = u - (u / UPC) * UPC;
         // this wave's loads of unit u have landed once only unit u+1's may still be in flight
-        vm_wait_rt(u + 1 < U ? bi + (t == UPC - 1 ? ai : 0) : 0);
+        // (unit u+1 carries a halo DMA when it starts a virtual chunk that stages one)
+        vm_wait_rt(u + 1 < U ? bi + (t == UPC - 1 && OPK3_HALO(c + 1) ? ai : 0) : 0);
 #if OPK3_ABLATE != 3   // dev probe only (3): no block barrier
         __builtin_amdgcn_s_barrier();
 #endif
@@ -200,7 +214,7 @@ void conv3_kernel(const ConvArgs a)
 #else
         if (u + 2 < U) OPK3_ISSUE(u + 2);
 #endif
-        const uint4* As = lds + (c % NAS) * ASLOT;
+        const uint4* As = lds + OPK3_ASLOT(c) * ASLOT;
         const uint4* Bs = lds + NAS * ASLOT + (u % 3) * BSLOT;
 #pragma unroll
         for (int k = 0; k < TAPU; ++k) {
@@ -233,6 +247,9 @@ void conv3_kernel(const ConvArgs a)
         }
     }
 #undef OPK3_ISSUE
+#undef OPK3_WUNIT
+#undef OPK3_ASLOT
+#undef OPK3_HALO
     OPK3_STAMP(2);
     if constexpr (!BIAS_EARLY) OPK3_BIAS();   // 128-VGPR variants: not kept across the K loop
 #undef OPK3_BIAS
@@ -708,7 +725,13 @@ __global__ __launch_bounds__(64 * kP_NW, 1) void conv3p_kernel(const ConvArgs a)
 
 }  // namespace
 
-Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border)
+bool conv3_w8_eligible(int cout, int ntaps, int ndst, const int* dst_cs, const int* dst_coff, bool out32)
+{
+    return cout == 64 && ntaps == 9 && ndst == 1 && !out32 && ((dst_cs[0] | dst_coff[0]) & 7) == 0 &&
+           dev_switch("CONV3W8_64", 1) != 0;
+}
+
+Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border, bool w8)
 {
     // variant switches (opk_dev_set; read per call so tests can compare variants in one process):
     // CONV3_SMALL=0 -> no two-per-CU tiles, CONV3_W16=0 -> no 16-wave tiles,
@@ -754,7 +777,8 @@ Conv3Shape conv3_shape(int frames, int H, int W, int cout, int ks, int border)
                            ((cout + s.bn - 1) / s.bn);
         // (measured, round 1: 4-wave 256x128 two-per-CU tiles and 8-wave 512x128 tiles of 128x64
         // wave tiles were both slower than these on every BODY_25 layer)
-        if (s.bn != 64 && big16 && tiles >= 3 * 256) {   // 512 x {128,96} tiles, 16 waves
+        if ((s.bn != 64 || w8) && big16 && tiles >= 3 * 256) {   // 512 x {128,96} tiles, 16 waves
+            // (64 outputs: only for conv3w8's 8 waves of 64 x 64, conv3_w8_eligible)
             s.persist = dev_switch("CONV3_PERSIST", 1) != 0;
             // the persistent kernel keeps bias/slopes in LDS: 688 halo rows
             s.bm = 512; s.hr = s.persist ? kP_HR : 704; s.tapu = 3; s.minb = 1; s.nw = 16;
@@ -792,7 +816,8 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     OPK_CHECK_ARG(a.in_cs % 8 == 0 && a.in_coff % 8 == 0, "input slice must be 16-byte aligned");
     OPK_CHECK_ARG(a.in_coff + a.cin_pad <= a.in_cs, "input slice exceeds the buffer");
     OPK_CHECK_ARG(a.M > 0 && a.cout > 0 && a.ndst <= kConvMaxDst, "bad sizes");
-    const Conv3Shape s = conv3_shape(a.frames, a.H, a.W, a.cout, ks, B);
+    const bool w8 = conv3_w8_eligible(a);
+    const Conv3Shape s = conv3_shape(a.frames, a.H, a.W, a.cout, ks, B, w8);
     OPK_CHECK_ARG(a.sw == s.sw && a.nstrips == s.nstrips, "strip geometry differs from conv3_shape");
     const int VW = s.sw + 2 * B;
     OPK_CHECK_ARG(ks == 1 || s.bm + (ks - 1) * (VW + 1) <= s.hr, "strip too wide for the halo");
@@ -801,7 +826,9 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     const int nn = (a.cout + s.bn - 1) / s.bn;
     const long ntiles = ((total + s.bm - 1) / s.bm) * nn;
     dim3 grid((unsigned)ntiles);
-    OPK_CHECK_ARG(!a.split || (a.in_lo && !a.pool), "split precision: lo twin required, no pool fusion");
+    bool lo_ok = !a.split || a.in_lo;
+    for (int d = 0; d < a.ndst && a.split; ++d) lo_ok = lo_ok && a.dst_lo[d];
+    OPK_CHECK_ARG(lo_ok, "split precision: lo twins required");
     // conv + 2x2 max pool in one persistent kernel (conv3w8.hip POOL epilogue); the planner only
     // asks for it where conv3w8_pool_supported holds
     if (a.pool) {
@@ -815,6 +842,12 @@ void launch_conv3(const ConvArgs& args, hipStream_t stream)
     // the fragment reads per MFMA; removed, source and numbers in profiles/round3/wino/)
     // several 128-channel n-blocks (the VGG 256 / 512-channel layers): conv3w8 with one n-block
     // per persistent block (bit-identical; CONV3W8N=0: the 16-wave conv3_kernel)
+    // 64-output layers in the persistent geometry (both precisions): conv3w8's BN = 64 tile
+    if (w8 && s.persist && s.bn == 64) {
+        OPK_CHECK_ARG(s.nw == 16 && VW > 16 && conv3w8_supported(a), "conv3w8<64>: unsupported conv");
+        launch_conv3w8(a, stream);
+        return;
+    }
     // split precision: every 512-position 96 / 128 / 256 / 512-channel 3x3 layer on conv3w8's split
     // instantiation (bit-identical to conv3_kernel's; SPLIT_W8=0: conv3_kernel, A/B) -- its three
     // times longer K loop is the regime where conv3w8 keeps the MFMA pipe busiest; the rest

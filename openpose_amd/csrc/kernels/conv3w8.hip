@@ -60,17 +60,39 @@ typedef unsigned int opk8_u4 __attribute__((ext_vector_type(4)));
 #define OPK_FAULT_POOL 0
 #endif
 
-// SPLIT: split precision (ConvArgs::split, conv.h): K runs over three passes of the input chunks
-// (x_hi w_hi, x_lo w_hi, x_hi w_lo; the halo DMA of pass 1 reads the lo twin), in the order of
-// conv3_kernel<..., SPLIT>, and the epilogue writes hi = fp16(v) and lo = fp16(v - hi) of
-// v = act(acc * wscale + bias) -- bit-identical to conv3_kernel's split instantiations.
+// SPLIT: split precision (ConvArgs::split, conv.h): K runs chunk-major over three products per
+// input chunk c -- virtual chunk 3c + k: k = 0 x_hi w_hi, 1 x_hi w_lo, 2 x_lo w_hi -- so the hi
+// halo of a chunk is staged once for two products (k = 1 issues no halo DMA and reads k = 0's
+// slot; hi halos live in slot 0, lo halos in slot 1), in the order of conv3_kernel<..., SPLIT>;
+// the epilogue writes hi = fp16(v) and lo = fp16(v - hi) of v = act(acc * wscale + bias) --
+// bit-identical to conv3_kernel's split instantiations.
+// split-precision pooling (POOL && SPLIT): of two (hi, lo) fp16 pairs of 8 channels, keep per
+// channel the one with the larger hi + lo (exact in fp32), the first (h1, l1) on ties -- the rule
+// of maxpool2_split_kernel (pool.hip), whose raster-order scan this reproduces window-wise
+__device__ __forceinline__ void opk8_pair_max(uint4& h1, uint4& l1, const uint4& h2, const uint4& l2)
+{
+    uint32_t* a = reinterpret_cast<uint32_t*>(&h1);
+    uint32_t* al = reinterpret_cast<uint32_t*>(&l1);
+    const uint32_t* b = reinterpret_cast<const uint32_t*>(&h2);
+    const uint32_t* bl = reinterpret_cast<const uint32_t*>(&l2);
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        const float2_t fa = __builtin_convertvector(__builtin_bit_cast(half2_t, a[w]), float2_t) +
+                            __builtin_convertvector(__builtin_bit_cast(half2_t, al[w]), float2_t);
+        const float2_t fb = __builtin_convertvector(__builtin_bit_cast(half2_t, b[w]), float2_t) +
+                            __builtin_convertvector(__builtin_bit_cast(half2_t, bl[w]), float2_t);
+        const uint32_t m = (fb.x > fa.x ? 0x0000ffffu : 0u) | (fb.y > fa.y ? 0xffff0000u : 0u);
+        a[w] = (a[w] & ~m) | (b[w] & m);
+        al[w] = (al[w] & ~m) | (bl[w] & m);
+    }
+}
+
 template <int BN, int NB, bool POOL, bool MX, bool BST, bool SPLIT>
 __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a)
 {
-    static_assert(!(POOL && SPLIT), "split precision: the pools run as their own kernel");
     constexpr int NW = k8_NW, BM = k8_BM, HR = k8_HR;
     constexpr int WROWS = BM / NW, MF = WROWS / 16, NF = BN / 16;
-    static_assert(WROWS == 64 && (NF == 8 || NF == 6), "wave tiles 64 x 128 / 64 x 96");
+    static_assert(WROWS == 64 && (NF == 8 || NF == 6 || NF == 4), "wave tiles 64 x 128 / 96 / 64");
     constexpr int API = HR / 16, AIW = (API + NW - 1) / NW;
     constexpr int BROWS = 3 * BN, BPI = BROWS / 16, BIW = (BPI + NW - 1) / NW;
     constexpr int ASLOT = HR * 4, BSLOT = BROWS * 4;   // 16-byte pieces
@@ -78,10 +100,11 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     static_assert(LDS_PIECES * 16 <= 160 * 1024, "LDS budget");
     // counted lgkmcnt waits of steps 0..3 per tap kind (-1: none needed), from the issue order
     // (see OPK8_TAP): step 0 waits for the tap's last B fragment and everything older
+    // (NF = 4: taps 0 / 1 stream the next tap's B fragments in steps 0 and 1 only)
     constexpr int kWait[3][4] = {
-        {3, -1, 8, NF == 8 ? 8 : 6},                                   // tap 0
-        {NF == 8 ? 3 : 4, NF == 8 ? -1 : 6, 8, NF == 8 ? 8 : 6},       // tap 1
-        {NF == 8 ? 1 : 2, NF == 8 ? -1 : 2, 2, 2}};                    // tap 2
+        {3, -1, NF == 4 ? 6 : 8, NF == 8 ? 8 : (NF == 6 ? 6 : 4)},                               // tap 0
+        {NF == 8 ? 3 : 4, NF == 8 ? -1 : 6, NF == 4 ? 6 : 8, NF == 8 ? 8 : (NF == 6 ? 6 : 4)},   // tap 1
+        {NF == 8 ? 1 : 2, NF == 8 ? -1 : 2, 2, 2}};                                              // tap 2
     __shared__ uint4 lds[LDS_PIECES];
     float* lbias = reinterpret_cast<float*>(lds + 2 * ASLOT + 3 * BSLOT);
     float* lmul = lbias + BN;
@@ -103,9 +126,20 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     constexpr int LGNB = NB == 4 ? 2 : NB - 1;
     const int G = gridDim.x, GM = G >> LGNB;
     const int xcd = blockIdx.x & 7, qq = G >> 3, rr = G & 7;
-    const int tix = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (blockIdx.x >> 3);
-    const int nblk = tix & (NB - 1);
-    int m = tix >> LGNB;
+    int nblk, m;
+    if (NB > 1 && a.nbx) {
+        // (G % 8 == 0, host) the blocks of XCD x (blocks b = x mod 8, observed placement; speed
+        // only) all take n-block x % NB: an XCD's L2 then holds one n-block's weights instead of
+        // all NB (split precision: 1.8 MB per n-block of a 256-input layer, 3.5 MB at 512 inputs,
+        // against 4 MB of L2); the n-block's 8 / NB XCDs share its m-tiles, each XCD a contiguous
+        // range per round
+        nblk = xcd & (NB - 1);
+        m = (xcd >> LGNB) * qq + (blockIdx.x >> 3);
+    } else {
+        const int tix = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + (blockIdx.x >> 3);
+        nblk = tix & (NB - 1);
+        m = tix >> LGNB;
+    }
     if (m >= ntm) return;
 
     // bias / negative-side multiplier of the n-block: registers now, LDS after the prologue's
@@ -119,9 +153,11 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
 
     const int lrow = lane >> 2, phys = lane & 3;
     const int cpt = a.cin_pad >> 5;
-    const int cptk = SPLIT ? 3 * cpt : cpt;   // K chunks (split: three passes over the input's)
+    const int cptk = SPLIT ? 3 * cpt : cpt;   // K (virtual) chunks (split: three per input chunk)
     const int U = 3 * cptk;
-    const int ublk = nblk * U;   // the n-block's first K unit in the packed weights
+    // the n-block's first K unit in the packed weights (split: w_hi and w_lo, 2 cpt chunks of 3
+    // units; virtual chunk 3c + k reads w_lo chunk c (cpt + c) for k = 1, w_hi chunk c otherwise)
+    const int ublk = nblk * 3 * (SPLIT ? 2 * cpt : cpt);
     const int bi = (BPI - wave + NW - 1) / NW;
     // weight piece of B DMA instruction j (recomputed at each issue: registers)
 #define OPK8_BOFF(j_)                                                                         \
@@ -145,23 +181,24 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     do {                                                                                      \
         _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_) dst_[i_] = OPK8_AROW1(mt_, i_);     \
     } while (0)
-#define OPK8_ISSUE(c_, ky_, aslot_, bslot_, nt_)                                              \
+    // K unit (virtual chunk of product k_ over input chunk dc_, tap row ky_); split: k_ = 1
+    // reuses k_ = 0's hi halo (no DMA), k_ = 2 stages the lo twin's; fp16: k_ = 0, dc_ = chunk
+#define OPK8_ISSUE(k_, dc_, ky_, aslot_, bslot_, nt_)                                         \
     do {                                                                                      \
-        if ((ky_) == 0 && (OPK8_ABLATE != 7 || !dma_ab)) {                                    \
+        if ((ky_) == 0 && (k_) != 1 && (OPK8_ABLATE != 7 || !dma_ab)) {                       \
             const int as_ = (aslot_) * ASLOT;                                                 \
-            /* split: pass 1 reads the lo twin, passes 0 and 2 the hi image */                \
-            const int ps_ = !SPLIT ? 0 : (c_) >= 2 * cpt ? 2 : ((c_) >= cpt ? 1 : 0);          \
-            const char* ab_ = ps_ == 1 ? abase_lo : abase;                                    \
+            const char* ab_ = (k_) == 2 ? abase_lo : abase;                                   \
             _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_)                                \
                 if (API % NW == 0 || i_ * NW + wave < API)                                    \
                     __builtin_amdgcn_global_load_lds(                                         \
-                        (const void*)(ab_ + ((c_) - ps_ * cpt) * 64 +                          \
+                        (const void*)(ab_ + (dc_) * 64 +                                      \
                                       ((nt_) ? OPK8_AROW1(m + GM, i_) : aoff[i_])),            \
                         (__attribute__((address_space(3))) void*)(&lds[as_ + (i_ * NW + wave) * 64]), \
                         16, 0, 0);                                                            \
         }                                                                                     \
         const int bs_ = 2 * ASLOT + (bslot_) * BSLOT;                                         \
-        const uint16_t* ub_ = a.w + (size_t)(ublk + (c_) * 3 + (ky_)) * BROWS * 32;                  \
+        const int wc_ = (k_) == 1 ? cpt + (dc_) : (dc_);                                     \
+        const uint16_t* ub_ = a.w + (size_t)(ublk + wc_ * 3 + (ky_)) * BROWS * 32;            \
         _Pragma("unroll") for (int j_ = 0; j_ < BIW; ++j_)                                    \
             if ((BPI % NW == 0 || j_ * NW + wave < BPI) && (OPK8_ABLATE != 8 || !dma_ab)) {   \
                 const int bo_ = OPK8_BOFF(j_);                                                \
@@ -239,9 +276,11 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                 OPK8_WAIT(w_, fa[0], "+v"(fa[1]), "+v"(FC[0]), "+v"(FC[1]), "+v"(FC[2]),      \
                           "+v"(FC[3]), "+v"(FC[4]), "+v"(FC[5]), "+v"(FC[6 % NF]),            \
                           "+v"(FC[7 % NF]));                                                  \
-            else                                                                              \
+            else if constexpr (NF == 6)                                                       \
                 OPK8_WAIT(w_, fa[0], "+v"(FC[0]), "+v"(FC[1]), "+v"(FC[2]), "+v"(FC[3]),      \
-                          "+v"(FC[4]), "+v"(FC[5]));                                          \
+                          "+v"(FC[4 % NF]), "+v"(FC[5 % NF]));                                \
+            else                                                                              \
+                OPK8_WAIT(w_, fa[0], "+v"(FC[0]), "+v"(FC[1]), "+v"(FC[2]), "+v"(FC[3]));     \
         } else if constexpr (w_ >= 0) {                                                       \
             OPK8_WAIT(w_ < 0 ? 0 : w_, fa[I]);                                                \
         }                                                                                     \
@@ -267,8 +306,8 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     // ---- prologue: units 0 and 1 of the first tile in flight, unit 0 visible, tap 0 read ------
     OPK8_AROW(aoff, m);
     bool dma_ab = false;   // (dev ablations 7 / 8: set after the prologue)
-    OPK8_ISSUE(0, 0, 0, 0, false);
-    OPK8_ISSUE(0, 1, 0, 1, false);
+    OPK8_ISSUE(0, 0, 0, 0, 0, false);
+    OPK8_ISSUE(0, 0, 1, 0, 1, false);
     dma_ab = true;
     (void)dma_ab;
     vm_wait_rt(bi);
@@ -290,9 +329,13 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     for (;;) {
         const int mn = m + GM;
         const bool has_next = mn < ntm;
+        // split: the unit's product k (vk) and input chunk (dcc), advanced by compares -- no
+        // division by 3 in the loop (a % 3 slot rule cost the kernel 3 spilled VGPRs)
+        int vk = 0, dcc = 0;
         for (int u = 0; u < U; ++u) {
             const int c = u / 3, ky = u - 3 * (u / 3);
-            const int aslot = (gc + c) & 1;
+            // halo slot: split -- hi halos in 0, lo halos in 1; fp16 -- chunk parity
+            const int aslot = SPLIT ? (vk == 2 ? 1 : 0) : ((gc + c) & 1);
             const uint32_t bb_u = OPK8_BBASE(u % 3);
             const uint32_t ab0 = OPK8_ABASE(aslot, ky, 0);
             const uint32_t ab1 = OPK8_ABASE(aslot, ky, 1);
@@ -301,7 +344,9 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
             const bool nt = u + 1 >= U;
             const int u1 = nt ? 0 : u + 1;
             const int c1 = u1 / 3, ky1 = u1 - 3 * (u1 / 3);
-            const int aslot1 = (gc + (nt ? cptk : 0) + c1) & 1;
+            // (split: unit u+1 is the same virtual chunk unless this is its tap row 2)
+            const int vk1 = nt ? 0 : (ky < 2 ? vk : (vk == 2 ? 0 : vk + 1));
+            const int aslot1 = SPLIT ? (vk1 == 2 ? 1 : 0) : ((gc + (nt ? cptk : 0) + c1) & 1);
             const uint32_t nab = OPK8_ABASE(aslot1, ky1, 0);
             const uint32_t nbb = OPK8_BBASE((u + 1) % 3);
             constexpr int S1 = MF * (NF / 2) * (SPLIT ? 2 : 1);   // epilogue stores per wave
@@ -310,16 +355,28 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         const bool nt_ = u + 2 >= U;                                                          \
         const int u2_ = nt_ ? u + 2 - U : u + 2;                                              \
         const int c2_ = u2_ / 3;                                                              \
-        OPK8_ISSUE(c2_, u2_ - 3 * c2_, (gc + (nt_ ? cptk : 0) + c2_) & 1, (u + 2) % 3, nt_); \
+        if constexpr (SPLIT) {   /* unit u+2: this virtual chunk at ky 0, else the next */    \
+            const bool same_ = ky == 0 && !nt_;                                               \
+            const int k2_ = nt_ ? 0 : (same_ ? vk : (vk == 2 ? 0 : vk + 1));                  \
+            const int d2_ = nt_ ? 0 : (same_ || vk < 2 ? dcc : dcc + 1);                      \
+            OPK8_ISSUE(k2_, d2_, u2_ - 3 * c2_, k2_ == 2 ? 1 : 0, (u + 2) % 3, nt_);          \
+        } else {                                                                              \
+            OPK8_ISSUE(0, c2_, u2_ - 3 * c2_, (gc + (nt_ ? cptk : 0) + c2_) & 1, (u + 2) % 3, nt_); \
+        }                                                                                     \
     } while (0)
             OPK8_TAP(0, ab0, ab1, bb_u, BN * 64, fbE, fbO);
             OPK8_TAP(1, ab1, ab2, bb_u, 2 * BN * 64, fbO, fbE);
-            if (u == 0 && gc > 0) vm_wait<S1>();
+            // (several destinations: S1 stores per destination -- wait for all, rare layers)
+            if (u == 0 && gc > 0 && (BST || a.ndst == 1)) vm_wait<S1>();   // (BST: one destination)
             else vm_wait<0>();
             if (OPK8_ABLATE != 1) __builtin_amdgcn_s_barrier();
             OPK8_TAP(2, ab2, nab, nbb, 0, fbE, fbO);
             if (OPK8_ABLATE != 4 || u + 2 >= U) OPK8_DMA_U2();
 #undef OPK8_DMA_U2
+            if (SPLIT && ky == 2) {   // next virtual chunk
+                dcc += vk == 2 ? 1 : 0;
+                vk = vk == 2 ? 0 : vk + 1;
+            }
         }
 
         // ---- epilogue: bias + activation + fp16 pack, 16-byte stores (border lanes to the sink)
@@ -398,7 +455,8 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
             __builtin_amdgcn_s_barrier();
             // (the slot bases are 256-byte aligned, so fragment pair j's piece is the lane's piece
             // for j = 0 with bits 6-7 flipped by 32 j: one XOR per access, four address registers)
-            char* const xch = reinterpret_cast<char*>(lds + ((gc + cptk - 1) & 1) * ASLOT);
+            // (split: the lo-halo slot 1; the next tile's first DMA fills the hi slot 0)
+            char* const xch = reinterpret_cast<char*>(lds + (SPLIT ? 1 : ((gc + cptk - 1) & 1)) * ASLOT);
             uint32_t xoff[MF];
 #pragma unroll
             for (int i = 0; i < MF; ++i) {
@@ -408,6 +466,86 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                 xoff[i] = qok[i] ? (uint32_t)(slot * 256 + (((cw >> 3) ^ slot) & 15) * 16) : 0u;
             }
 #define OPK8_XCH(i_, j_) reinterpret_cast<uint4*>(xch + (xoff[i_] ^ (uint32_t)((j_) * 2)))
+            if constexpr (SPLIT) {
+                // Split precision: the window's winner is a (hi, lo) pair.  Per column pair the
+                // even lane (the left column) keeps its own pair unless the right one's hi + lo is
+                // larger; the first-row lanes leave the winner's hi and lo in the window slot, the
+                // second-row lanes take the larger of the two rows (the first on ties) -- bit for
+                // bit maxpool2_split_kernel over the stored pairs.  A slot holds hi and lo of four
+                // of the eight 16-channel fragments, so the fragment pairs go in two halves, with
+                // a barrier before the second half reuses the slots.
+                static_assert(NF == 8 || NF == 4, "split pooled epilogue: 128 / 64-channel n-blocks");
+#pragma unroll
+                for (int hh = 0; hh < NF / 4; ++hh) {
+                    uint4 kh[MF][2], kl[MF][2];
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj) {
+                        const int j = 4 * hh + 2 * jj;
+                        float4_t bq[2], mq[2];
+#pragma unroll
+                        for (int k = 0; k < 2; ++k) {
+                            bq[k] = *reinterpret_cast<const float4_t*>(lb + (j + k) * 64);
+                            mq[k] = *reinterpret_cast<const float4_t*>(lb + BN * 4 + (j + k) * 64);
+                        }
+#pragma unroll
+                        for (int i = 0; i < MF; ++i) {
+                            uint32_t ph[2][2], pl[2][2];
+#pragma unroll
+                            for (int h = 0; h < 2; ++h) {
+                                const float4_t t = acc[i][j + h] * a.wscale + bq[h];
+                                const float4_t tm = t * mq[h];
+                                _Float16 wh[4], wl[4];
+#pragma unroll
+                                for (int r = 0; r < 4; ++r) {
+                                    const float v = act_pick<MX>(t[r], tm[r]);
+                                    const float o = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(
+                                        __builtin_bit_cast(int, v), 0xB1, 0xF, 0xF, false));
+                                    const _Float16 hv = (_Float16)v, ho = (_Float16)o;
+                                    const _Float16 lv = (_Float16)(v - (float)hv), lo = (_Float16)(o - (float)ho);
+                                    const bool right = (float)ho + (float)lo > (float)hv + (float)lv;
+                                    wh[r] = right ? ho : hv;
+                                    wl[r] = right ? lo : lv;
+                                }
+                                ph[h][0] = __builtin_bit_cast(uint32_t, (half2_t){wh[0], wh[1]});
+                                ph[h][1] = __builtin_bit_cast(uint32_t, (half2_t){wh[2], wh[3]});
+                                pl[h][0] = __builtin_bit_cast(uint32_t, (half2_t){wl[0], wl[1]});
+                                pl[h][1] = __builtin_bit_cast(uint32_t, (half2_t){wl[2], wl[3]});
+                            }
+                            const auto sl = __builtin_amdgcn_permlane16_swap(ph[0][0], ph[1][0], false, false);
+                            const auto sh = __builtin_amdgcn_permlane16_swap(ph[0][1], ph[1][1], false, false);
+                            const auto ll = __builtin_amdgcn_permlane16_swap(pl[0][0], pl[1][0], false, false);
+                            const auto lh = __builtin_amdgcn_permlane16_swap(pl[0][1], pl[1][1], false, false);
+                            kh[i][jj] = make_uint4(sl[0], sh[0], sl[1], sh[1]);
+                            kl[i][jj] = make_uint4(ll[0], lh[0], ll[1], lh[1]);
+                            if (qok[i] && first[i]) {   // hi at pieces ^ {0, 4}, lo at ^ {8, 12}
+                                *OPK8_XCH(i, 2 * jj * 16) = kh[i][jj];
+                                *OPK8_XCH(i, (2 * jj + 4) * 16) = kl[i][jj];
+                            }
+                        }
+                    }
+                    __syncthreads();   // (the first rows' pairs are in LDS)
+#pragma unroll
+                    for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+                        for (int i = 0; i < MF; ++i) {
+                            const int j = 4 * hh + 2 * jj;
+                            uint4 h1 = *OPK8_XCH(i, 2 * jj * 16), l1 = *OPK8_XCH(i, (2 * jj + 4) * 16);
+                            opk8_pair_max(h1, l1, kh[i][jj], kl[i][jj]);   // (second-row lanes)
+                            if constexpr (BST) {
+                                __builtin_amdgcn_raw_buffer_store_b128((opk8_u4){h1.x, h1.y, h1.z, h1.w}, rs0,
+                                                                       (int)(qo2[i] + j * 32), 0, 0);
+                                __builtin_amdgcn_raw_buffer_store_b128((opk8_u4){l1.x, l1.y, l1.z, l1.w}, rs0lo,
+                                                                       (int)(qo2[i] + j * 32), 0, 0);
+                            } else {
+                                const size_t o = cw + j * 16 + (size_t)qrow[i] * cs0;
+                                const bool st = qok[i] && !first[i];
+                                *(st ? reinterpret_cast<uint4*>(d0 + o) : sink4) = h1;
+                                *(st ? reinterpret_cast<uint4*>(d0lo + o) : sink4) = l1;
+                            }
+                        }
+                    if (hh + 1 < NF / 4) __syncthreads();   // (every wave read the first half: slots reused)
+                }
+            } else {
             uint4 keep[MF][NF / 2];
 #pragma unroll
             for (int j = 0; j < NF; j += 2) {
@@ -453,7 +591,6 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
 #pragma unroll
                 for (int i = 0; i < MF; ++i)
                     got[i][j / 2] = *OPK8_XCH(i, j * 16);   // (used by the second-row lanes only)
-#undef OPK8_XCH
 #pragma unroll
             for (int j = 0; j < NF; j += 2)
 #pragma unroll
@@ -472,6 +609,8 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                         *(qok[i] && !first[i] ? p : sink4) = r;
                     }
                 }
+            }   // (fp16 pooled epilogue)
+#undef OPK8_XCH
         } else {
         // one destination under 2 GiB (BST, host): buffer stores, masked lanes out of range
 #pragma unroll
@@ -562,12 +701,13 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
 
 bool conv3w8_supported(const ConvArgs& a)
 {
-    // one 16-byte store per (fragment pair, destination): the counted vmcnt at a tile's first
-    // mid-unit assumes a single destination
-    bool aligned = a.ndst == 1;
+    // one 16-byte store per (fragment pair, destination), 16-byte aligned slices; several
+    // destinations (conv4_4_CPM's five concat slices) wait for every store at a tile's first
+    // mid-unit instead of counting them
+    bool aligned = a.ndst >= 1 && a.ndst <= kConvMaxDst;
     for (int d = 0; d < a.ndst; ++d) aligned = aligned && ((a.dst_coff[d] | a.dst_cs[d]) & 7) == 0;
-    // 96 or 128 channels, or several 128-channel blocks (the VGG 256 / 512-channel layers)
-    const bool nb_ok = a.cout == 96 || a.cout == 128 || a.cout == 256 || a.cout == 512;
+    // 64, 96 or 128 channels, or several 128-channel blocks (the VGG 256 / 512-channel layers)
+    const bool nb_ok = a.cout == 64 || a.cout == 96 || a.cout == 128 || a.cout == 256 || a.cout == 512;
     return a.ntaps == 9 && nb_ok && a.sink && a.cus > 0 && !a.out32 && aligned &&
            a.sw + 2 * a.border > 16;
 }
@@ -576,7 +716,7 @@ bool conv3w8_pool_supported(const ConvArgs& a)
 {
     // windows never straddle a strip or a 6-row tile: even sizes, even strips, 1-pixel border;
     // the pooled image is dst[0] (one destination)
-    return conv3w8_supported(a) && a.cout % 128 == 0 && a.ndst == 1 && a.border == 1 &&
+    return conv3w8_supported(a) && (a.cout % 128 == 0 || a.cout == 64) && a.ndst == 1 && a.border == 1 &&
            a.H % 2 == 0 && a.W % 2 == 0 && a.sw % 2 == 0 && 6 * (a.sw + 2) <= k8_BM;
 }
 
@@ -587,9 +727,9 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
     const int VW = a.sw + 2 * a.border;
     const bool pool = a.pool != 0;
     if (pool)
-        OPK_CHECK_ARG(conv3w8_pool_supported(a), "conv3w8 + pool: even H, W and strips, 128k outputs, border 1");
+        OPK_CHECK_ARG(conv3w8_pool_supported(a), "conv3w8 + pool: even H, W and strips, 64 / 128k outputs, border 1");
     const long ntm = pool ? (total / VW - 1 + 5) / 6 : (total + k8_BM - 1) / k8_BM;
-    const int nb = a.cout == 96 ? 1 : a.cout / 128;
+    const int nb = a.cout <= 128 ? 1 : a.cout / 128;
     // a multiple of the n-block count (each block keeps one n-block)
     const unsigned G = (unsigned)(std::min<long>(a.cus / nb, ntm) * nb);
     OPK_CHECK_ARG(G >= 1 && G <= 1024, "persistent grid exceeds the sink");
@@ -600,6 +740,10 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
                         a.dst_cs[0] * 2;
     const long pextent = ((long)a.frames * (a.H / 2 + 2) * (a.W / 2 + 2) + kConvGuardTail) * a.dst_cs[0] * 2;
     b.bufst = a.ndst == 1 && (pool ? pextent : extent) < (1L << 31) - 4096 && dev_switch("BUFST", 1) != 0;
+    // n-blocks by XCD (W8_NBX=1, dev A/B): measured neutral in both precisions (round 6,
+    // profiles/round6/r6c: split 104.0 vs 104.1 ms, fp16 33.6 vs 33.6 ms per 130-frame forward),
+    // so the m-tile-major order stays the default
+    b.nbx = nb > 1 && G % 8 == 0 && dev_switch("W8_NBX", 0) != 0;
 #define OPK8_LAUNCH3(BN_, NB_, P_, MX_, SP_)                                                     \
     do {                                                                                        \
         note_launch("conv3w8_kernel<%d,%d,%d,%d,%d%s>", BN_, NB_, (int)P_, (int)MX_, b.bufst,     \
@@ -611,23 +755,25 @@ void launch_conv3w8(const ConvArgs& a, hipStream_t stream)
     } while (0)
 #define OPK8_LAUNCH2(BN_, NB_, P_, MX_)                                                          \
     do {                                                                                        \
-        if (P_ || !a.split) OPK8_LAUNCH3(BN_, NB_, P_, MX_, false);                             \
-        else OPK8_LAUNCH3(BN_, NB_, false, MX_, true);                                          \
+        if (a.split) OPK8_LAUNCH3(BN_, NB_, P_, MX_, true);                                     \
+        else OPK8_LAUNCH3(BN_, NB_, P_, MX_, false);                                            \
     } while (0)
 #define OPK8_LAUNCH(BN_, NB_, P_)                                                                \
     do {                                                                                        \
         if (a.actmax) OPK8_LAUNCH2(BN_, NB_, P_, true);                                         \
         else OPK8_LAUNCH2(BN_, NB_, P_, false);                                                 \
     } while (0)
-    OPK_CHECK_ARG(!a.split || (!pool && a.in_lo && a.dst_lo[0]), "conv3w8 split: lo twins, no pool");
+    OPK_CHECK_ARG(!a.split || (a.in_lo && a.dst_lo[0]), "conv3w8 split: lo twins");
     if (pool) {
         if (nb == 4) OPK8_LAUNCH(128, 4, true);
         else if (nb == 2) OPK8_LAUNCH(128, 2, true);
+        else if (a.cout == 64) OPK8_LAUNCH(64, 1, true);
         else OPK8_LAUNCH(128, 1, true);
     } else if (nb == 4) OPK8_LAUNCH(128, 4, false);
     else if (nb == 2) OPK8_LAUNCH(128, 2, false);
     else if (a.cout == 128) OPK8_LAUNCH(128, 1, false);
-    else OPK8_LAUNCH(96, 1, false);
+    else if (a.cout == 96) OPK8_LAUNCH(96, 1, false);
+    else OPK8_LAUNCH(64, 1, false);
 #undef OPK8_LAUNCH
 #undef OPK8_LAUNCH2
 #undef OPK8_LAUNCH3

@@ -35,7 +35,11 @@ __device__ __forceinline__ uint16_t f2h_bits_i(float v)
     return __builtin_bit_cast(uint16_t, h);
 }
 
-template <bool SPLIT>
+// WIDE: cout % 32 == 0 and 16-byte aligned slices -- fragment pairs (g, g+1) exchanged between
+// lane rows q and q^1 by v_permlane16_swap (as conv3.hip's epilogues), so each lane stores 8
+// consecutive channels (16 bytes) and a store instruction covers 64 contiguous bytes of 16 pixels
+// instead of 32 (half the store instructions; same values)
+template <bool SPLIT, bool WIDE>
 __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const float* __restrict__ img)
 {
     __shared__ float tile[3 * (TH + 2) * LW];
@@ -117,6 +121,50 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
             }
         }
         const int x = x0 + xl;
+        if constexpr (WIDE) {
+            // lanes (r16, q) and (r16, q ^ 1) hold the same pixel: a column past W skips both
+            if (x >= W) continue;
+            const int cw = 16 * (q & 1) + 8 * (q >> 1);
+#pragma unroll
+            for (int g = 0; g < NG; g += 2) {
+                if (g * 16 >= a.cout) break;
+                uint32_t pk[2][2], pl[2][2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    float v[4];
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const float t = (SPLIT ? acc[g + h][r] * a.wscale : acc[g + h][r]) + bv[g + h][r];
+                        v[r] = t > 0.f ? t : t * mv[g + h][r];
+                    }
+                    pk[h][0] = (uint32_t)f2h_bits_i(v[0]) | ((uint32_t)f2h_bits_i(v[1]) << 16);
+                    pk[h][1] = (uint32_t)f2h_bits_i(v[2]) | ((uint32_t)f2h_bits_i(v[3]) << 16);
+                    if constexpr (SPLIT) {
+                        uint16_t r[4];
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const uint16_t hb = f2h_bits_i(v[e]);
+                            r[e] = f2h_bits_i(v[e] - (float)__builtin_bit_cast(_Float16, hb));
+                        }
+                        pl[h][0] = (uint32_t)r[0] | ((uint32_t)r[1] << 16);
+                        pl[h][1] = (uint32_t)r[2] | ((uint32_t)r[3] << 16);
+                    }
+                }
+                const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
+                const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
+                const uint4 val = make_uint4(sl[0], sh[0], sl[1], sh[1]);
+                for (int d = 0; d < a.ndst; ++d)
+                    *reinterpret_cast<uint4*>(dbase[d] + (size_t)(x + B) * a.dst_cs[d] + g * 16 + cw) = val;
+                if constexpr (SPLIT) {
+                    const auto ll = __builtin_amdgcn_permlane16_swap(pl[0][0], pl[1][0], false, false);
+                    const auto lh = __builtin_amdgcn_permlane16_swap(pl[0][1], pl[1][1], false, false);
+                    const uint4 lv = make_uint4(ll[0], lh[0], ll[1], lh[1]);
+                    for (int d = 0; d < a.ndst; ++d)
+                        *reinterpret_cast<uint4*>(dlo[d] + (size_t)(x + B) * a.dst_cs[d] + g * 16 + cw) = lv;
+                }
+            }
+            continue;
+        }
         if (x >= W) continue;
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
@@ -160,14 +208,22 @@ void launch_conv_image(const ConvArgs& a, const float* image, hipStream_t stream
         OPK_CHECK_ARG(((a.dst_cs[d] | a.dst_coff[d]) & 3) == 0, "conv_image: 8-byte aligned slices");
     const long blocks = (long)a.frames * ((a.H + TH - 1) / TH) * ((a.W + TW - 1) / TW);
     OPK_CHECK_ARG(blocks > 0 && blocks < (1L << 31), "conv_image: bad sizes");
+    // 16-byte stores (CONV_IMAGE_WIDE=0: the 8-byte epilogue, dev A/B; same values)
+    bool wide = a.cout % 32 == 0 && dev_switch("CONV_IMAGE_WIDE", 1) != 0;
+    for (int d = 0; d < a.ndst; ++d) wide = wide && ((a.dst_cs[d] | a.dst_coff[d]) & 7) == 0;
+#define OPKI_LAUNCH(SP_, WI_)                                                                    \
+    hipLaunchKernelGGL((conv_image_kernel<SP_, WI_>), dim3((unsigned)blocks), dim3(256), 0, stream, a, image)
     if (a.split) {
         for (int d = 0; d < a.ndst; ++d) OPK_CHECK_ARG(a.dst_lo[d] != nullptr, "conv_image: split needs dst_lo");
         note_launch("conv_image_kernel<split>");
-        hipLaunchKernelGGL(conv_image_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, a, image);
+        if (wide) OPKI_LAUNCH(true, true);
+        else OPKI_LAUNCH(true, false);
     } else {
         note_launch("conv_image_kernel");
-        hipLaunchKernelGGL(conv_image_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, a, image);
+        if (wide) OPKI_LAUNCH(false, true);
+        else OPKI_LAUNCH(false, false);
     }
+#undef OPKI_LAUNCH
     OPK_LAUNCH_CHECK();
 }
 

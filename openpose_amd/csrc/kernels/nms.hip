@@ -25,9 +25,11 @@
 #include "heat_dev.h"
 #include "../common.h"
 
-// OPK_NMS_JUMP (dev A/B builds: 0): the walk leaves a cold source window in one jump
+// OPK_NMS_JUMP (dev A/B builds: 1): the walk leaves a cold source window in one jump.  Measured
+// slower (round 6, profiles/round6/nms_jump_paf_exit/: nms_detect_walk2 980 -> 1,498 us per
+// 64-frame BODY_135 step; 88 VGPRs instead of 76, one wave per SIMD fewer), so off
 #ifndef OPK_NMS_JUMP
-#define OPK_NMS_JUMP 1
+#define OPK_NMS_JUMP 0
 #endif
 
 namespace opk {

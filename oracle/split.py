@@ -40,11 +40,25 @@ def _act64(t, act, slope):
     return t
 
 
+def _maxpool64(x, k, st):
+    """Caffe MAX pooling (ceil sizing, pad 0) in float64."""
+    n, c, h, w = x.shape
+    oh, ow = -(-(h - k) // st) + 1, -(-(w - k) // st) + 1
+    out = np.full((n, c, oh, ow), -np.inf)
+    for dy in range(k):
+        for dx in range(k):
+            v = x[:, :, dy::st, dx::st][:, :, :oh, :ow]
+            out[:, :, :v.shape[2], :v.shape[3]] = np.maximum(out[:, :, :v.shape[2], :v.shape[3]], v)
+    return out
+
+
 def unit(u, x, params, c_acc):
-    """Reference and per-element bound of a single-conv launch unit (oracle/fp16.py
-    unit_from_launch: split precision fuses no pool or head pair) for the input blob values x
-    (fp32: the GPU's hi + lo, or the fp32 image, which the first conv splits itself)."""
-    assert len(u["convs"]) == 1 and u["pool"] is None, "split precision runs single-conv units"
+    """Reference and per-element bound of a launch unit (oracle/fp16.py unit_from_launch: one conv,
+    or one conv + its 2x2 max pool in the epilogue -- split precision fuses no head pair) for the
+    input blob values x (fp32: the GPU's hi + lo, or the fp32 image, which the first conv splits
+    itself).  A pooled unit: the max of the reference and of the bound over each window (the
+    kernel's pair maximum is within the bound of the exact maximum)."""
+    assert len(u["convs"]) == 1, "split precision runs single-conv units"
     c = u["convs"][0]
     w, b, slope = params[c["name"]]
     x = np.asarray(x, np.float32)
@@ -54,4 +68,7 @@ def unit(u, x, params, c_acc):
         tol = c_acc * s + np.abs(t) * 2.0 ** -22 + 2.0 ** -30
     else:
         tol = c_acc * s + np.abs(t) * 2.0 ** -21 + 2.0 ** -24
+    if u["pool"] is not None:
+        k, st = u["pool"]["kernel_size"], u["pool"]["stride"]
+        t, tol = _maxpool64(t, k, st), _maxpool64(tol, k, st)
     return t, tol

@@ -149,7 +149,10 @@ def test_every_launch_within_fp16_bound(bench_net, record_property):
 # The same bench geometry in split precision: every conv launch -- conv_image<split>, the 8-wave
 # conv3w8 split instantiations (96 / 128 channels, 2 and 4 n-blocks), conv3_kernel split for the
 # rest -- against the exact (float64) conv of the GPU's own hi + lo input blob (oracle/split.py).
-C_SPLIT = 2.0 ** -16   # fp32 accumulation + dropped lo*lo + weight residue (oracle/split.py)
+# fp32 accumulation + dropped lo*lo + weight residue (oracle/split.py); the worst launch measured
+# 0.041 of 2^-16 (round 6, r6b), so 2^-19 keeps ~3x headroom -- a missing or misplaced pass
+# (~2^-11 S) is 250x beyond it
+C_SPLIT = 2.0 ** -19
 
 
 @pytest.fixture(scope="module")
@@ -172,18 +175,23 @@ def split_net(ctx):
 
 def test_split_launch_log_uses_fused_kernels(split_net):
     """Split precision runs the 8-wave persistent kernel's split instantiations for the 512-position
-    layers (1, 2 and 4 n-blocks of 128, and 96 channels) and the first conv on conv_image<split>;
-    every conv kernel is a split instantiation and every conv is in exactly one launch."""
+    layers (1, 2 and 4 n-blocks of 128, 96 and 64 channels; pool2 / pool3 in the epilogue) and the
+    first conv on conv_image<split>; every conv kernel is a split instantiation and every conv is
+    launched (the 64-channel full-resolution layer as frame runs)."""
     inst = {k for _, k in split_net["log"]}
     for nb in (1, 2, 4):
         assert any(k.startswith("conv3w8_kernel<128,%d,0," % nb) and k.endswith(",split>") for k in inst), nb
+    for nb in (1, 2):   # conv2_2 + pool2, conv3_4 + pool3: the split pooled epilogue
+        assert any(k.startswith("conv3w8_kernel<128,%d,1," % nb) and k.endswith(",split>") for k in inst), nb
+    # conv1_2 + pool1 on the 64-channel tile
+    assert any(k.startswith("conv3w8_kernel<64,1,1,") and k.endswith(",split>") for k in inst)
     assert any(k.startswith("conv3w8_kernel<96,1,0,") and k.endswith(",split>") for k in inst)
     assert "conv_image_kernel<split>" in inst
     convk = [k for k in inst if k.startswith(("conv3", "conv_image"))]
     assert all("split" in k for k in convk), convk
     assert not any(k.startswith(("conv3w_", "conv_head", "conv1_fused")) for k in inst), inst
     # (the full-resolution layers of 130 frames run as frame runs: several launches, one layer)
-    named = {c for layer, _ in split_net["log"] if layer != "pool" for c in layer.split("+")}
+    named = {c for layer, _ in split_net["log"] for c in layer.split("+") if c != "pool"}
     convs = [l["name"] for l in split_net["graph"] if l["type"] == "Convolution"]
     assert sorted(named) == sorted(convs)
     print("%d launches: %s" % (len(split_net["log"]), sorted(inst)))
@@ -191,7 +199,7 @@ def test_split_launch_log_uses_fused_kernels(split_net):
 
 def test_split_every_launch_within_bound(split_net, record_property):
     """Each conv launch of the split-precision bench forward against the float64 conv of the GPU's
-    own hi + lo input blob (frames 0 and last): |gpu - ref| <= 2^-16 S + 2^-21 |ref| + 2^-24."""
+    own hi + lo input blob (frames 0 and last): |gpu - ref| <= 2^-19 S + 2^-21 |ref| + 2^-24."""
     from oracle import split as sp
     net, graph, params = split_net["net"], split_net["graph"], split_net["params"]
     worst = 0.0

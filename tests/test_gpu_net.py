@@ -308,6 +308,32 @@ def torch_forward(graph, params, x):
     return blobs["net_output"].numpy()
 
 
+def torch_forward64(graph, params, x):
+    """float64 torch (CPU) evaluation of the same graph: the exact result the fp32 paths
+    approximate (test_body25_split_precision_vs_oracle)."""
+    import torch.nn.functional as F
+    d = torch.float64
+    blobs = {"image": torch.from_numpy(np.asarray(x, np.float64))}
+    producer = {}
+    for l in graph:
+        t = l["type"]
+        if t == "Convolution":
+            producer[l["top"][0]] = l["name"]
+            w, b = params[l["name"]][:2]
+            blobs[l["top"][0]] = F.conv2d(blobs[l["bottom"][0]], torch.from_numpy(np.asarray(w)).to(d),
+                                          torch.from_numpy(np.asarray(b)).to(d), padding=l.get("pad", 0))
+        elif t == "ReLU":
+            blobs[l["top"][0]] = torch.relu(blobs[l["bottom"][0]])
+        elif t == "PReLU":
+            s = torch.from_numpy(np.asarray(params[producer[l["bottom"][0]]][2])).to(d)
+            blobs[l["top"][0]] = F.prelu(blobs[l["bottom"][0]], s)
+        elif t == "Concat":
+            blobs[l["top"][0]] = torch.cat([blobs[b] for b in l["bottom"]], 1)
+        elif t == "Pooling":
+            blobs[l["top"][0]] = F.max_pool2d(blobs[l["bottom"][0]], 2, 2, ceil_mode=True)
+    return blobs["net_output"].numpy()
+
+
 @pytest.mark.parametrize("name,hw", [("builtin:COCO_18", (64, 96)), ("builtin:MPI_15_4", (48, 80)),
                                      ("builtin:HAND", (64, 64)), ("builtin:FACE", (48, 64))])
 def test_reference_cpm_nets_vs_oracle(ctx, name, hw):
@@ -501,10 +527,16 @@ def test_body25_split_precision_vs_oracle(ctx, n, h, w):
     ref = body25.forward(x, params, graph=graph)
     err, err16 = rel_l2(got, ref), rel_l2(fp16, ref)
     ch = channel_errors(got, ref)
-    print("BODY_25 %dx%dx%d split precision rel-L2 %.3e (fp16 %.3e), worst channel %.3e"
-          % (n, h, w, err, err16, ch.max()))
+    # against the exact (float64) forward, split precision is as close as the fp32 oracle itself:
+    # both sit at fp32's reassociation noise (CPU, round 6: oracle 8.0e-6, torch fp32 2.5e-6)
+    ex = torch_forward64(graph, params, x)
+    err_ex, err_or = rel_l2(got, ex), rel_l2(ref, ex)
+    print("BODY_25 %dx%dx%d split precision rel-L2 %.3e vs the fp32 oracle (fp16 %.3e), worst "
+          "channel %.3e; vs float64: split %.3e, fp32 oracle %.3e"
+          % (n, h, w, err, err16, ch.max(), err_ex, err_or))
     assert err < SPLIT_TOL and ch.max() < SPLIT_CHANNEL_TOL
     assert err < err16 / 20
+    assert err_ex < 2 * err_or + 1e-6
     net.set_precision(PRECISION_FP16)
     net.forward(xd)
     np.testing.assert_array_equal(net.output_numpy(), fp16)
@@ -571,3 +603,28 @@ def test_split_precision_frame_runs_take_their_own_geometry(ctx):
         net.forward(torch.from_numpy(x[f:f + 1]).cuda())
         np.testing.assert_array_equal(got[f], net.output_numpy()[0])
     net.close()
+
+
+def test_split_pool_fusion_bit_identical(ctx):
+    """Split precision with pool1 / pool2 / pool3 in conv3w8's epilogue (the pair of the larger hi + lo per
+    window, the first in raster order on ties) equals the unfused conv + maxpool2_split_kernel bit
+    for bit: the net output and the pooled blobs (8 frames at 368x656: enough tiles for the
+    persistent geometry the fusion needs at both pooled layers)."""
+    from openpose_amd.api import PRECISION_SPLIT
+    x = np.random.default_rng(33).uniform(-0.5, 0.5, (8, 3, 368, 656)).astype(np.float32)
+    params = synth.he_weights(body25.layers(), seed=34)
+    outs = []
+    for sw in ({}, {"POOL_FUSE": 0}):
+        with dev_switches(LAUNCH_LOG=1, **sw):
+            net = Net(ctx, "builtin:BODY_25")
+            net.set_params(params)
+            net.set_precision(PRECISION_SPLIT)
+            net.forward(torch.from_numpy(x).cuda())
+            fused = sum(1 for layer, _ in net.launch_log() if layer.endswith("+pool"))
+            outs.append((fused, net.output_numpy(), net.blob("pool1_stage1"), net.blob("pool2_stage1"),
+                         net.blob("pool3_stage1")))
+            net.close()
+    # conv1_2 + pool1 (conv3w8's 64-channel tile), conv2_2 + pool2, conv3_4 + pool3
+    assert outs[0][0] == 3 and outs[1][0] == 0, (outs[0][0], outs[1][0])
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        np.testing.assert_array_equal(a, b)
