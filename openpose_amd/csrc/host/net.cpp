@@ -385,22 +385,32 @@ void NetHip::pack(ConvPlan& c)
                     }
                 }
     }
-    // conv_head.hip layouts: Mconv6 [cin_pad/32][n1][32]; Mconv7 K-permuted [n2 <= 32 ? 32 : 64][n1]
+    // conv_head.hip layouts: Mconv6 [cin_pad/32][n1][32]; Mconv7 K-permuted [n2 <= 32 ? 32 : 64][n1];
+    // split precision: a w_hi block, then a w_lo block, of each (HeadArgs::split)
     std::vector<uint16_t> packedh;
     if (c.head >= 0) {
         const FuseHead& fh = heads_[c.head];
+        const int passes = split ? 2 : 1;
+        auto part = [&](float wv, int ps) {
+            const _Float16 hi = (_Float16)wv;
+            return ps == 0 ? __builtin_bit_cast(uint16_t, hi) : f2h(wv - (float)hi);
+        };
         if (&convs_[fh.a] == &c) {
             const int n1 = c.info.cout, cpt = c.cin_pad / 32;
-            packedh.assign((size_t)cpt * n1 * 32, 0);
-            for (int co = 0; co < n1; ++co)
-                for (int ci = 0; ci < cin; ++ci)
-                    packedh[((size_t)(ci / 32) * n1 + co) * 32 + ci % 32] = f2h(w[(size_t)co * cin + ci]);
+            packedh.assign((size_t)passes * cpt * n1 * 32, 0);
+            for (int ps = 0; ps < passes; ++ps)
+                for (int co = 0; co < n1; ++co)
+                    for (int ci = 0; ci < cin; ++ci)
+                        packedh[(((size_t)ps * cpt + ci / 32) * n1 + co) * 32 + ci % 32] =
+                            part(wsc(w[(size_t)co * cin + ci]), ps);
         } else {
-            const int n1 = cin, n2 = c.info.cout;
+            const int n1 = cin, n2 = c.info.cout, n2p = n2 <= 32 ? 32 : 64;
             std::vector<uint16_t> w7((size_t)n2 * n1);
-            for (size_t e = 0; e < w7.size(); ++e) w7[e] = f2h(w[e]);
-            packedh.assign((size_t)(n2 <= 32 ? 32 : 64) * n1, 0);
-            conv_head_pack_w7(packedh.data(), w7.data(), n1, n2);
+            packedh.assign((size_t)passes * n2p * n1, 0);
+            for (int ps = 0; ps < passes; ++ps) {
+                for (size_t e = 0; e < w7.size(); ++e) w7[e] = part(wsc(w[e]), ps);
+                conv_head_pack_w7(packedh.data() + (size_t)ps * n2p * n1, w7.data(), n1, n2);
+            }
         }
     }
     // bias/slope zero-padded to a multiple of 128 channels (conv3 reads whole 4-channel groups)
@@ -488,13 +498,16 @@ NetHip::ShapePlan* NetHip::shape_plan(int n, int h, int w, hipStream_t zero_stre
     std::vector<uint16_t*>& ptr = S.base;
     ptr.assign(bufs_.size(), nullptr);
     // CONV1_FUSED=0 (opk_dev_set, A/B tests): the three separate kernels instead of the fusion
-    S.split = precision_ == kPrecisionSplit;   // (split precision: no conv1 / head fusion)
+    S.split = precision_ == kPrecisionSplit;   // (split precision: no conv1 fusion)
     S.fused1 = !S.split && fuse1_.a >= 0 && dev_switch("CONV1_FUSED", 1) != 0 && border_ == 1 &&
                conv1_fused_supported(h, w, 64, 64);
     // HEAD_FUSE=0 (opk_dev_set, A/B tests): Mconv6 and Mconv7 as two conv3 launches
     // Positions are decoded by float-reciprocal division in conv_head_kernel, exact below 2^24:
     // larger batches run the pairs unfused.
-    S.fusedh = !S.split && !heads_.empty() && dev_switch("HEAD_FUSE", 1) != 0;
+    // (split precision: conv_head_kernel's split instantiations; HEAD_FUSE_SPLIT=0, dev A/B: the
+    // unfused split pair)
+    S.fusedh = (!S.split || dev_switch("HEAD_FUSE_SPLIT", 1) != 0) && !heads_.empty() &&
+               dev_switch("HEAD_FUSE", 1) != 0;
     for (const auto& fh : heads_) {
         const int L = convs_[fh.a].level;
         S.fusedh = S.fusedh && (long)n * (lh_[L] + 2) * (lw_[L] + 2) < (1L << 24);
@@ -877,6 +890,13 @@ void NetHip::forward_steps(ShapePlan& S, const float* input, int n, int h, int w
                 h.out32_coff = b.out32_coff;
                 // persistent grid (HEAD_PERSIST=0: one workgroup per tile, dev A/B)
                 h.cus = dev_switch("HEAD_PERSIST", 1) != 0 ? a.cus : 0;
+                if (S.split) {
+                    h.split = 1;
+                    h.in_lo = a.in_lo;
+                    for (int d = 0; d < b.ndst; ++d) h.dst_lo[d] = b.dst_lo[d];
+                    h.wscale6 = a.wscale;
+                    h.wscale7 = b.wscale;
+                }
                 if (log) log->layer = c.info.name + "+" + cb.info.name;
                 launch_conv_head(h, st);
                 ++si;   // Mconv7 ran inside

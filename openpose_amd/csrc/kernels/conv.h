@@ -126,6 +126,15 @@ struct HeadArgs {
     int out32_c, out32_coff;
     int cus;              // > 0: persistent grid of this many workgroups (conv_head.hip)
     int actmax;           // Mconv6's negative-side multipliers all in [0, 1] (ConvArgs::actmax)
+    // split precision (ConvArgs::split): the input as (in, in_lo) fp16 pairs, w6 packed
+    // [2][cin_pad/32][n1][32] (w_hi block, then w_lo), w7 [2][n2p][n1] (each K-permuted), both
+    // scaled by 2^e per layer (sums times wscale6 / wscale7 before the bias); Mconv6's activation
+    // is split into (hi, lo) on chip and Mconv7 runs x_hi w_hi + x_lo w_hi + x_hi w_lo; outputs
+    // hi to dst, lo to dst_lo
+    int split;
+    const uint16_t* in_lo;
+    uint16_t* dst_lo[kConvMaxDst];
+    float wscale6, wscale7;
 };
 bool conv_head_supported(int n1, int n2, int cin_pad);
 void conv_head_pack_w7(uint16_t* dst, const uint16_t* w7 /* [n2][n1] */, int n1, int n2);

@@ -21,6 +21,12 @@
 // PERSIST: one workgroup per CU walks tiles (XCD-aware order): no workgroup turnover, the bias
 // read once; the next tile's first two K steps are issued into the ring (which the partials
 // alias) as soon as every wave has read its partial sums and issued its stores.
+// SPLIT (split precision, HeadArgs::split): phase 1 runs three K steps per 32-channel chunk --
+// x_hi w_hi, x_lo w_hi, x_hi w_lo, each a plain ring step with its own A and B sources -- into one
+// fp32 accumulator; phase 2 scales by 2^-e6, activates and splits the Mconv6 value v into
+// hi = fp16(v), lo = fp16(v - hi) (the pair the unfused layer would have stored) and runs Mconv7 as
+// v_hi w7_hi + v_hi w7_lo + v_lo w7_hi; phase 3 scales by 2^-e7, adds the bias and stores the
+// (hi, lo) pair.  Mconv7's weights come from L2 in both grids (no W7LDS: hi + lo fill the ring).
 // MFMA f32_16x16x32_f16, C^T arrangement (weights as the A operand) as in conv3.hip.
 #include "conv.h"
 
@@ -56,7 +62,7 @@ constexpr int kH_BM = 128, kH_NW = 8;
 #ifndef OPKH_KSCHED
 #define OPKH_KSCHED 0
 #endif
-template <int N1, int NF2, bool PERSIST, bool MX>
+template <int N1, int NF2, bool PERSIST, bool MX, bool SPLIT>
 __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs a)
 {
     constexpr int NW = kH_NW, BM = kH_BM;
@@ -105,19 +111,24 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     // ---- phase 1: Mconv6 K loop ------------------------------------------------------------------
     const int lrow = lane >> 2, phys = lane & 3;
     const int KS = a.cin_pad >> 5;
+    const int KV = SPLIT ? 3 * KS : KS;                       // ring steps (split: 3 per chunk)
     constexpr int BIW = N1 / 16 / NW;                         // B DMA instructions per wave per step
     // A DMA: instruction `wave` covers tile rows wave*16 .. +15 (positions past the end read the
     // zeroed guard after the last frame, conv.h kConvGuardTail)
     const int arow = wave * 16 + lrow;
 #define OPKH_ASRC(p0_) (a.in + a.in_coff + (size_t)((p0_) + arow) * a.in_cs + (phys ^ (((arow >> 2) & 1) << 1)) * 8)
     const uint16_t* asrc = OPKH_ASRC(tile * BM);
+    // (split: the lo twin has the hi buffer's layout)
+    const ptrdiff_t lo_off = SPLIT ? a.in_lo - a.in : 0;
+    // step s_: chunk c_, product k_ (split: 0 x_hi w_hi, 1 x_lo w_hi, 2 x_hi w_lo)
 #define OPKH_ISSUE(s_)                                                                        \
     do {                                                                                      \
         const int sl_ = (s_) % 3;                                                             \
-        __builtin_amdgcn_global_load_lds((const void*)(asrc + (s_) * 32),                     \
+        const int c_ = SPLIT ? (s_) / 3 : (s_), k_ = SPLIT ? (s_) - 3 * ((s_) / 3) : 0;        \
+        __builtin_amdgcn_global_load_lds((const void*)(asrc + (k_ == 1 ? lo_off : 0) + c_ * 32), \
                                          (__attribute__((address_space(3))) void*)(&lds[sl_ * ASLOT + wave * 64]), \
                                          16, 0, 0);                                           \
-        const uint16_t* wb_ = a.w6 + (size_t)(s_) * N1 * 32;                                  \
+        const uint16_t* wb_ = a.w6 + (size_t)((k_ == 2 ? KS : 0) + c_) * N1 * 32;             \
         _Pragma("unroll") for (int j_ = 0; j_ < (OPKH_ABLATE == 1 && (s_) > 1 ? 0 : BIW); ++j_) { \
             const int rb_ = (j_ * NW + wave) * 16 + lrow;                                     \
             __builtin_amdgcn_global_load_lds(                                                 \
@@ -131,7 +142,7 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     // (r % N2P), 64 bytes, swizzled like a B slot; rows [h*N1, (h+1)*N1) fill B slot (KS + h) % 3
     // (NF2 / 2 slots: the ones of K steps KS-2 and KS-3, free once every wave passed step KS-1's
     // barrier; the next tile's DMA goes into the ring only after phase 3's barrier)
-    constexpr bool W7LDS = OPKH_W7LDS && !PERSIST;
+    constexpr bool W7LDS = OPKH_W7LDS && !PERSIST && !SPLIT;
     constexpr int W7ROWS = (N1 / 32) * N2P, W7IW = W7ROWS / 16 / NW;
     static_assert(W7ROWS <= 2 * N1 && W7ROWS % (16 * NW) == 0, "Mconv7 weights fit two B slots");
 #define OPKH_ISSUE_W7()                                                                       \
@@ -140,7 +151,7 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
             const int inst_ = k_ * NW + wave;                                                 \
             const int r_ = inst_ * 16 + lrow;                                                 \
             const int kb_ = r_ / N2P, o_ = r_ - (r_ / N2P) * N2P;                             \
-            const int sl_ = (KS + (inst_ * 16) / N1) % 3;                                     \
+            const int sl_ = (KV + (inst_ * 16) / N1) % 3;                                     \
             __builtin_amdgcn_global_load_lds(                                                 \
                 (const void*)(a.w7 + (size_t)o_ * N1 + kb_ * 32 + (phys ^ (((r_ >> 2) & 1) << 1)) * 8), \
                 (__attribute__((address_space(3))) void*)(&lds[3 * ASLOT + sl_ * BSLOT + ((inst_ * 16) % N1) * 4]), \
@@ -151,7 +162,7 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
     (void)lds0;
 
     OPKH_ISSUE(0);
-    if (KS > 1) OPKH_ISSUE(1);
+    if (KV > 1) OPKH_ISSUE(1);
     for (;;) {
     const int p0 = tile * BM;
     // lane terms re-derived per tile (opaque): nothing lane-dependent is hoisted out of the tile
@@ -167,14 +178,14 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
 #pragma unroll
         for (int j = 0; j < NF; ++j) acc[i][j] = float4_t{0.f, 0.f, 0.f, 0.f};
 
-    for (int s = 0; s < KS; ++s) {
+    for (int s = 0; s < KV; ++s) {
         // own DMA of step s landed once only step s+1's (1 + BIW instructions) may be in flight
         // (a previous tile's output stores are older)
-        if (s + 1 < KS) vm_wait<1 + BIW>();
+        if (s + 1 < KV) vm_wait<1 + BIW>();
         else vm_wait<0>();
         __builtin_amdgcn_s_barrier();
-        if (s + 2 < KS) OPKH_ISSUE(s + 2);
-        if (W7LDS && s == KS - 1) OPKH_ISSUE_W7();
+        if (s + 2 < KV) OPKH_ISSUE(s + 2);
+        if (W7LDS && s == KV - 1) OPKH_ISSUE_W7();
         half8_t fa[MF], fb[NF];
         if constexpr (OPKH_KSCHED) {
             // rows i*16 / j*16 keep the swizzle bit: fragment i (j) is base + 1 KiB * i (j)
@@ -275,16 +286,19 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         (const __attribute__((address_space(1))) uint16_t*)w7o;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb) {
-        half8_t a7[NF2];
+        half8_t a7[NF2], a7l[SPLIT ? NF2 : 1];
 #pragma unroll
         for (int f = 0; f < NF2; ++f) {
             if constexpr (W7LDS) {   // ring row (K block wn*4 + kb) x N2P + f*16 + r16
                 const int r = (wn * 4 + kb) * N2P + f * 16 + r16;
-                const int sl = (KS + r / N1) % 3;
+                const int sl = (KV + r / N1) % 3;
                 a7[f] = __builtin_bit_cast(half8_t, lds[3 * ASLOT + sl * BSLOT + swz64(r % N1, q)]);
             } else {
                 a7[f] = *reinterpret_cast<gh8p>(w7 + (size_t)(f * 16 + r16) * N1 + wn * 128 +
                                                           kb * 32 + q * 8);
+                if constexpr (SPLIT)   // w7_lo: the second [N2P][N1] block
+                    a7l[f] = *reinterpret_cast<gh8p>(w7 + (size_t)(N2P + f * 16 + r16) * N1 +
+                                                     wn * 128 + kb * 32 + q * 8);
             }
         }
         float4_t bq[2], mq[2];
@@ -295,13 +309,21 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         }
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
-            uint32_t pk[2][2];
+            uint32_t pk[2][2], pl[2][2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const float4_t t = acc[i][2 * kb + h] + bq[h];
+                const float4_t t = (SPLIT ? acc[i][2 * kb + h] * a.wscale6 : acc[i][2 * kb + h]) + bq[h];
                 const float4_t v = act_pick4<MX>(t, t * mq[h]);
-                pk[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.xy, half2_t));
-                pk[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.zw, half2_t));
+                const half2_t h01 = __builtin_convertvector(v.xy, half2_t);
+                const half2_t h23 = __builtin_convertvector(v.zw, half2_t);
+                pk[h][0] = __builtin_bit_cast(uint32_t, h01);
+                pk[h][1] = __builtin_bit_cast(uint32_t, h23);
+                if constexpr (SPLIT) {   // lo = fp16(v - hi) (v - hi exact in fp32)
+                    pl[h][0] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                        v.xy - __builtin_convertvector(h01, float2_t), half2_t));
+                    pl[h][1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                        v.zw - __builtin_convertvector(h23, float2_t), half2_t));
+                }
             }
             const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
             const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
@@ -309,6 +331,16 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
 #pragma unroll
             for (int f = 0; f < NF2; ++f)
                 acc2[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a7[f], b2, acc2[i][f], 0, 0, 0);
+            if constexpr (SPLIT) {
+                const auto ll = __builtin_amdgcn_permlane16_swap(pl[0][0], pl[1][0], false, false);
+                const auto lh = __builtin_amdgcn_permlane16_swap(pl[0][1], pl[1][1], false, false);
+                const half8_t b2l = __builtin_bit_cast(half8_t, make_uint4(ll[0], lh[0], ll[1], lh[1]));
+#pragma unroll
+                for (int f = 0; f < NF2; ++f) {
+                    acc2[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a7l[f], b2, acc2[i][f], 0, 0, 0);
+                    acc2[i][f] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a7[f], b2l, acc2[i][f], 0, 0, 0);
+                }
+            }
         }
     }
 
@@ -343,7 +375,7 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
             float4_t v = part[OPKH_PART((wm * WN1) * WROWS + i * 16 + r16, f * 4 + q)];
             for (int w = 1; w < WN1; ++w)
                 v = v + part[OPKH_PART((wm * WN1 + w) * WROWS + i * 16 + r16, f * 4 + q)];
-            outv[k][i] = v + b7;
+            outv[k][i] = (SPLIT ? v * a.wscale7 : v) + b7;
         }
     }
     // positions of this lane's MF rows: padded-image coordinates by float-reciprocal division
@@ -369,26 +401,41 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         const int ch = f * 16 + 4 * q;   // this lane's 4 output channels
         if (f >= NF2 || ch >= a.n2) continue;
         const int nv = min(4, a.n2 - ch);
-        uint32_t lo[MF], hi[MF];
+        // (lo / hi: channels 0-1 / 2-3 of the lane's four; split: the pair's second halves in
+        // lo2 / hi2)
+        uint32_t lo[MF], hi[MF], lo2[SPLIT ? MF : 1], hi2[SPLIT ? MF : 1];
 #pragma unroll
         for (int i = 0; i < MF; ++i) {
             const float4_t v = outv[k][i];
-            lo[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.xy, half2_t));
-            hi[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(v.zw, half2_t));
+            const half2_t h01 = __builtin_convertvector(v.xy, half2_t);
+            const half2_t h23 = __builtin_convertvector(v.zw, half2_t);
+            lo[i] = __builtin_bit_cast(uint32_t, h01);
+            hi[i] = __builtin_bit_cast(uint32_t, h23);
+            if constexpr (SPLIT) {
+                lo2[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                    v.xy - __builtin_convertvector(h01, float2_t), half2_t));
+                hi2[i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(
+                    v.zw - __builtin_convertvector(h23, float2_t), half2_t));
+            }
         }
         for (int d = 0; d < a.ndst; ++d) {
-            uint16_t* const od = a.dst[d] + a.dst_coff[d] + ch;
             const int cs = a.dst_cs[d];
-            if (nv == 4 && ((a.dst_coff[d] | cs) & 3) == 0) {
 #pragma unroll
-                for (int i = 0; i < MF; ++i)
-                    if (ok[i]) *reinterpret_cast<uint2*>(od + (size_t)pos[i] * cs) = make_uint2(lo[i], hi[i]);
-            } else {
+            for (int pass = 0; pass < (SPLIT ? 2 : 1); ++pass) {
+                uint16_t* const od = (pass ? a.dst_lo[d] : a.dst[d]) + a.dst_coff[d] + ch;
+                const uint32_t* const pa = pass ? lo2 : lo;
+                const uint32_t* const pb = pass ? hi2 : hi;
+                if (nv == 4 && ((a.dst_coff[d] | cs) & 3) == 0) {
 #pragma unroll
-                for (int i = 0; i < MF; ++i)
-                    if (ok[i])
-                        for (int e = 0; e < nv; ++e)
-                            od[(size_t)pos[i] * cs + e] = (uint16_t)((e < 2 ? lo[i] : hi[i]) >> (16 * (e & 1)));
+                    for (int i = 0; i < MF; ++i)
+                        if (ok[i]) *reinterpret_cast<uint2*>(od + (size_t)pos[i] * cs) = make_uint2(pa[i], pb[i]);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < MF; ++i)
+                        if (ok[i])
+                            for (int e = 0; e < nv; ++e)
+                                od[(size_t)pos[i] * cs + e] = (uint16_t)((e < 2 ? pa[i] : pb[i]) >> (16 * (e & 1)));
+                }
             }
         }
         if (a.out32) {
@@ -412,7 +459,7 @@ __global__ __launch_bounds__(64 * kH_NW, 1) void conv_head_kernel(const HeadArgs
         if (next < ntiles) {
             asrc = OPKH_ASRC(next * BM);
             OPKH_ISSUE(0);
-            if (KS > 1) OPKH_ISSUE(1);
+            if (KV > 1) OPKH_ISSUE(1);
         }
     }
     if (!PERSIST || next >= ntiles) break;
@@ -446,6 +493,11 @@ void launch_conv_head(const HeadArgs& a, hipStream_t stream)
 {
     OPK_CHECK_ARG(conv_head_supported(a.n1, a.n2, a.cin_pad), "conv_head: N1 256/512, N2 <= 64");
     OPK_CHECK_ARG(a.ndst <= kConvMaxDst, "conv_head: too many destinations");
+    if (a.split) {
+        OPK_CHECK_ARG(a.in_lo != nullptr, "conv_head: split precision needs the input's lo twin");
+        for (int d = 0; d < a.ndst; ++d)
+            OPK_CHECK_ARG(a.dst_lo[d] != nullptr, "conv_head: split precision: lo twins required");
+    }
     const long total = (long)a.frames * (a.H + 2) * (a.W + 2);
     // phase 3 decodes positions by float-reciprocal division, exact below 2^24 (conv3_dev.h)
     OPK_CHECK_ARG(total < (1L << 24), "conv_head: too many positions (split the batch)");
@@ -453,14 +505,21 @@ void launch_conv_head(const HeadArgs& a, hipStream_t stream)
     // persistent at N1 = 512 (one 143 KB workgroup per CU: 4-5 % faster than one workgroup per
     // tile); at N1 = 256 two per-tile workgroups share a CU and the persistent grid measured
     // 23 % slower (one per CU) or unchanged-slow (two per CU) -- profiles/round3/head/
-    const bool persist = a.cus > 0 && a.n1 == 512;
+    // Split precision: per-tile at both N1 (the persistent <512, 4, split> spills 10-14 VGPRs per
+    // tile; measured 98.5 against 98.7 ms per 130-frame split forward, profiles/round6/split_head/)
+    const bool persist = a.cus > 0 && a.n1 == 512 && !a.split;
     const unsigned G = (unsigned)(persist ? std::min<long>(a.cus, ntiles) : ntiles);
     const dim3 blk(64 * kH_NW);
+#define OPKH_LAUNCH3(N1_, NF2_, MX_, SP_)                                                       \
+    do {                                                                                       \
+        note_launch("conv_head_kernel<%d,%d,%d,%d%s>", N1_, NF2_, (int)persist, (int)MX_, SP_ ? ",split" : ""); \
+        if (persist) hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, true, MX_, SP_>), dim3(G), blk, 0, stream, a); \
+        else hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, false, MX_, SP_>), dim3(G), blk, 0, stream, a); \
+    } while (0)
 #define OPKH_LAUNCH2(N1_, NF2_, MX_)                                                            \
     do {                                                                                       \
-        note_launch("conv_head_kernel<%d,%d,%d,%d>", N1_, NF2_, (int)persist, (int)MX_);        \
-        if (persist) hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, true, MX_>), dim3(G), blk, 0, stream, a); \
-        else hipLaunchKernelGGL((conv_head_kernel<N1_, NF2_, false, MX_>), dim3(G), blk, 0, stream, a); \
+        if (a.split) OPKH_LAUNCH3(N1_, NF2_, MX_, true);                                       \
+        else OPKH_LAUNCH3(N1_, NF2_, MX_, false);                                              \
     } while (0)
 #define OPKH_LAUNCH(N1_, NF2_)                                                                 \
     do {                                                                                       \
@@ -476,6 +535,7 @@ void launch_conv_head(const HeadArgs& a, hipStream_t stream)
     }
 #undef OPKH_LAUNCH
 #undef OPKH_LAUNCH2
+#undef OPKH_LAUNCH3
     OPK_LAUNCH_CHECK();
 }
 

@@ -54,20 +54,35 @@ def _maxpool64(x, k, st):
 
 def unit(u, x, params, c_acc):
     """Reference and per-element bound of a launch unit (oracle/fp16.py unit_from_launch: one conv,
-    or one conv + its 2x2 max pool in the epilogue -- split precision fuses no head pair) for the
+    one conv + its 2x2 max pool in the epilogue, or a fused 1x1 head pair Mconv6 + Mconv7) for the
     input blob values x (fp32: the GPU's hi + lo, or the fp32 image, which the first conv splits
     itself).  A pooled unit: the max of the reference and of the bound over each window (the
-    kernel's pair maximum is within the bound of the exact maximum)."""
-    assert len(u["convs"]) == 1, "split precision runs single-conv units"
-    c = u["convs"][0]
-    w, b, slope = params[c["name"]]
+    kernel's pair maximum is within the bound of the exact maximum).  A head pair: Mconv6's value
+    never leaves the chip but is split into the same (hi, lo) pair a stored blob holds, so its
+    bound (times the activation's Lipschitz constant) propagates through |w7|."""
+    assert len(u["convs"]) in (1, 2), "split precision runs single convs and head pairs"
     x = np.asarray(x, np.float32)
-    t = _act64(_conv64(x, w, b, c["pad"]), c.get("act", 0), slope)
-    s = _conv64(np.abs(x), np.abs(w), np.abs(b), c["pad"])
-    if u["fp32_output"]:   # net_output: the fp32 activation, no pair
-        tol = c_acc * s + np.abs(t) * 2.0 ** -22 + 2.0 ** -30
-    else:
-        tol = c_acc * s + np.abs(t) * 2.0 ** -21 + 2.0 ** -24
+    err = None   # bound on the error of the current input (None: exact)
+    for i, c in enumerate(u["convs"]):
+        w, b, slope = params[c["name"]]
+        last = i == len(u["convs"]) - 1
+        t = _act64(_conv64(x, w, b, c["pad"]), c.get("act", 0), slope)
+        s = _conv64(np.abs(x), np.abs(w), np.abs(b), c["pad"])
+        if err is not None:   # the input's own error through |w|
+            s = s + _conv64(err, np.abs(w), np.zeros_like(b), c["pad"])
+            prop = _conv64(err, np.abs(w), np.zeros_like(b), c["pad"])
+        else:
+            prop = 0.0
+        if last and u["fp32_output"]:   # net_output: the fp32 activation, no pair
+            tol = c_acc * s + prop + np.abs(t) * 2.0 ** -22 + 2.0 ** -30
+        else:
+            tol = c_acc * s + prop + np.abs(t) * 2.0 ** -21 + 2.0 ** -24
+        if not last:
+            lip = 1.0
+            if c.get("act", 0) == 2:
+                lip = max(1.0, float(np.max(np.abs(np.asarray(slope, np.float64)))))
+            err = tol * lip
+            x = t
     if u["pool"] is not None:
         k, st = u["pool"]["kernel_size"], u["pool"]["stride"]
         t, tol = _maxpool64(t, k, st), _maxpool64(tol, k, st)

@@ -175,9 +175,10 @@ def split_net(ctx):
 
 def test_split_launch_log_uses_fused_kernels(split_net):
     """Split precision runs the 8-wave persistent kernel's split instantiations for the 512-position
-    layers (1, 2 and 4 n-blocks of 128, 96 and 64 channels; pool2 / pool3 in the epilogue) and the
-    first conv on conv_image<split>; every conv kernel is a split instantiation and every conv is
-    launched (the 64-channel full-resolution layer as frame runs)."""
+    layers (1, 2 and 4 n-blocks of 128, 96 and 64 channels; pool1 / pool2 / pool3 in the epilogue),
+    the first conv on conv_image<split> and the 1x1 head pairs on conv_head<split>; every conv
+    kernel is a split instantiation and every conv is launched (the 64-channel full-resolution
+    layer as frame runs)."""
     inst = {k for _, k in split_net["log"]}
     for nb in (1, 2, 4):
         assert any(k.startswith("conv3w8_kernel<128,%d,0," % nb) and k.endswith(",split>") for k in inst), nb
@@ -187,9 +188,14 @@ def test_split_launch_log_uses_fused_kernels(split_net):
     assert any(k.startswith("conv3w8_kernel<64,1,1,") and k.endswith(",split>") for k in inst)
     assert any(k.startswith("conv3w8_kernel<96,1,0,") and k.endswith(",split>") for k in inst)
     assert "conv_image_kernel<split>" in inst
-    convk = [k for k in inst if k.startswith(("conv3", "conv_image"))]
+    # the Mconv6 + Mconv7 pairs on conv_head_kernel's split instantiations (N1 = 256 and 512)
+    for n1 in (256, 512):
+        assert any(k.startswith("conv_head_kernel<%d," % n1) and k.endswith(",split>") for k in inst), n1
+    # (and so no conv of the bench net is left on the generic conv3_kernel)
+    assert not any(k.startswith("conv3_kernel") for k in inst), inst
+    convk = [k for k in inst if k.startswith(("conv3", "conv_image", "conv_head"))]
     assert all("split" in k for k in convk), convk
-    assert not any(k.startswith(("conv3w_", "conv_head", "conv1_fused")) for k in inst), inst
+    assert not any(k.startswith(("conv3w_", "conv1_fused")) for k in inst), inst
     # (the full-resolution layers of 130 frames run as frame runs: several launches, one layer)
     named = {c for layer, _ in split_net["log"] for c in layer.split("+") if c != "pool"}
     convs = [l["name"] for l in split_net["graph"] if l["type"] == "Convolution"]

@@ -379,11 +379,16 @@ def test_coco_pose_pipeline_runs_on_the_net(ctx):
     assert pose.peaks_numpy().shape[1] == 18
 
 
-def test_head_fusion_matches_unfused_and_oracle(ctx):
+@pytest.mark.parametrize("precision", ["fp16", "split"])
+def test_head_fusion_matches_unfused_and_oracle(ctx, precision):
     """Mconv6 -> Mconv7 pairs (1x1 to 512 / 256 channels, then 1x1 to <= 64) run as one
     conv_head_kernel: fp16 outputs into a concat read by a later conv and fp32 net-output channels.
     Against the two conv3 launches (HEAD_FUSE=0) only the fp32 summation order of Mconv7 differs
-    (per-wave partials summed in a fixed order); against the fp32 oracle the usual tolerance."""
+    (per-wave partials summed in a fixed order); against the fp32 oracle the usual tolerance.
+    Split precision: conv_head's split instantiations (Mconv6's value split into the pair the
+    unfused layer stores) against the unfused split pair and the oracle at the split tolerance."""
+    from openpose_amd.api import PRECISION_SPLIT
+    split = precision == "split"
     L = conv("c0", "image", 64, 3, "relu") + conv("c1", "c0", 96, 3, "prelu")
     L += conv("m6", "c1", 512, 1, "prelu") + conv("m7", "m6", 52, 1)
     L += conv("n6", "c1", 256, 1, "relu") + conv("n7", "n6", 26, 1)
@@ -400,16 +405,27 @@ def test_head_fusion_matches_unfused_and_oracle(ctx):
     outs = {}
     try:
         for name, sw in {"fused": {}, "unfused": {"HEAD_FUSE": 0}}.items():
-            with dev_switches(**sw):
+            with dev_switches(LAUNCH_LOG=1, **sw):
                 net = Net(ctx, path)
                 net.set_params(params)
+                if split:
+                    net.set_precision(PRECISION_SPLIT)
                 net.forward(torch.from_numpy(x).cuda())
                 outs[name] = net.output_numpy()
+                heads = [k for _, k in net.launch_log() if k.startswith("conv_head")]
+                assert len(heads) == (2 if name == "fused" else 0), heads
+                assert all(k.endswith(",split>") == split for k in heads), heads
                 net.close()
     finally:
         os.unlink(path)
-    assert rel_l2(outs["fused"], outs["unfused"]) < 1e-4
     ref = body25.forward(x, params, graph=graph)
+    if split:
+        d, e = rel_l2(outs["fused"], outs["unfused"]), rel_l2(outs["fused"], ref)
+        print("split heads: fused vs unfused rel-L2 %.3e, vs the fp32 oracle %.3e" % (d, e))
+        assert d < 1e-6 and e < SPLIT_TOL
+        assert channel_errors(outs["fused"], ref).max() < SPLIT_CHANNEL_TOL
+        return
+    assert rel_l2(outs["fused"], outs["unfused"]) < 1e-4
     assert rel_l2(outs["fused"], ref) < SMALL_TOL
     for c in range(ref.shape[1]):
         assert rel_l2(outs["fused"][:, c], ref[:, c]) < CHANNEL_TOL, c
@@ -522,8 +538,9 @@ def test_body25_split_precision_vs_oracle(ctx, n, h, w):
         net.forward(xd)
         kernels = {k for _, k in net.launch_log()}
     got = net.output_numpy()
-    assert all("split" in k for k in kernels if k.startswith(("conv3_kernel", "conv3w8", "conv_image"))), kernels
-    assert not any(k.startswith(("conv3w_", "conv_head", "conv1_fused")) for k in kernels), kernels
+    assert all("split" in k for k in kernels
+               if k.startswith(("conv3_kernel", "conv3w8", "conv_image", "conv_head"))), kernels
+    assert not any(k.startswith(("conv3w_", "conv1_fused")) for k in kernels), kernels
     ref = body25.forward(x, params, graph=graph)
     err, err16 = rel_l2(got, ref), rel_l2(fp16, ref)
     ch = channel_errors(got, ref)
