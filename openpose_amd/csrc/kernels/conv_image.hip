@@ -39,11 +39,16 @@ __device__ __forceinline__ uint16_t f2h_bits_i(float v)
 // lane rows q and q^1 by v_permlane16_swap (as conv3.hip's epilogues), so each lane stores 8
 // consecutive channels (16 bytes) and a store instruction covers 64 contiguous bytes of 16 pixels
 // instead of 32 (half the store instructions; same values)
-template <bool SPLIT, bool WIDE>
+// STAGE (WIDE only): each 16-pixel group's 16-byte pieces go through a per-wave LDS image first
+// (piece column XOR-swizzled by the pixel) and leave as stores of 1 KiB contiguous per instruction
+// -- 8 whole pixels of 128 bytes -- instead of 16 half lines of 64 bytes (CONV_IMAGE_STAGE, A/B)
+template <bool SPLIT, bool WIDE, bool STAGE>
 __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const float* __restrict__ img)
 {
     __shared__ float tile[3 * (TH + 2) * LW];
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    __shared__ uint4 ostage[STAGE ? TH : 1][SPLIT ? 2 : 1][STAGE ? 128 : 1];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // (uniform: row pointers in SGPRs)
     const int H = a.H, W = a.W, B = a.border > 0 ? a.border : 1;
     const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
     int b = blockIdx.x;
@@ -67,7 +72,6 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
     const int r16 = lane & 15, q = lane >> 4;
     // weights (A operand of C^T): rows = output channels g*16 + r16, K = 8q .. 8q+7; row stride 64
     half8_t wf[NG], wl[NG];
-    float4_t bv[NG], mv[NG];
     const float neg = a.act == 1 ? 0.f : 1.f;
 #pragma unroll
     for (int g = 0; g < NG; ++g) {
@@ -77,10 +81,14 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
         if constexpr (SPLIT)
             wl[g] = co < a.cout ? *reinterpret_cast<const half8_t*>(a.w + (size_t)co * 64 + 32 + 8 * q)
                                 : half8_t{0, 0, 0, 0, 0, 0, 0, 0};
-        const int ch = g * 16 + 4 * q;   // bias/slope arrays are zero-padded to 128 channels
-        bv[g] = *reinterpret_cast<const float4_t*>(a.bias + ch);
-        const float4_t sl = *reinterpret_cast<const float4_t*>(a.slope + ch);
-        mv[g] = a.act == 2 ? sl : float4_t{neg, neg, neg, neg};
+    }
+    // bias / negative-side multipliers in LDS, read per fragment (in registers they held 32 VGPRs
+    // and the split kernel to 3 waves per SIMD; bias/slope arrays are zero-padded to 128 channels)
+    __shared__ float4_t sbias[16 * NG / 4], smul[16 * NG / 4];
+    if (tid < 16 * NG / 4) {
+        sbias[tid] = *reinterpret_cast<const float4_t*>(a.bias + 4 * tid);
+        const float4_t sl = *reinterpret_cast<const float4_t*>(a.slope + 4 * tid);
+        smul[tid] = a.act == 2 ? sl : float4_t{neg, neg, neg, neg};
     }
     // this lane's 8 K values: LDS offset of (ci, ky, kx) for k = 8q + e, or -1 past k = 26
     int off[8];
@@ -123,7 +131,8 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
         const int x = x0 + xl;
         if constexpr (WIDE) {
             // lanes (r16, q) and (r16, q ^ 1) hold the same pixel: a column past W skips both
-            if (x >= W) continue;
+            // (STAGE: every lane writes its pieces; the stores skip the columns past W)
+            if (!STAGE && x >= W) continue;
             const int cw = 16 * (q & 1) + 8 * (q >> 1);
 #pragma unroll
             for (int g = 0; g < NG; g += 2) {
@@ -132,10 +141,11 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     float v[4];
+                    const float4_t bq = sbias[(g + h) * 4 + q], mq = smul[(g + h) * 4 + q];
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
-                        const float t = (SPLIT ? acc[g + h][r] * a.wscale : acc[g + h][r]) + bv[g + h][r];
-                        v[r] = t > 0.f ? t : t * mv[g + h][r];
+                        const float t = (SPLIT ? acc[g + h][r] * a.wscale : acc[g + h][r]) + bq[r];
+                        v[r] = t > 0.f ? t : t * mq[r];
                     }
                     pk[h][0] = (uint32_t)f2h_bits_i(v[0]) | ((uint32_t)f2h_bits_i(v[1]) << 16);
                     pk[h][1] = (uint32_t)f2h_bits_i(v[2]) | ((uint32_t)f2h_bits_i(v[3]) << 16);
@@ -153,15 +163,45 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
                 const auto sl = __builtin_amdgcn_permlane16_swap(pk[0][0], pk[1][0], false, false);
                 const auto sh = __builtin_amdgcn_permlane16_swap(pk[0][1], pk[1][1], false, false);
                 const uint4 val = make_uint4(sl[0], sh[0], sl[1], sh[1]);
-                for (int d = 0; d < a.ndst; ++d)
-                    *reinterpret_cast<uint4*>(dbase[d] + (size_t)(x + B) * a.dst_cs[d] + g * 16 + cw) = val;
+                // (STAGE: piece (g * 16 + cw) / 8 of pixel r16, column swizzled by the pixel)
+                const int sp = r16 * 8 + (((g * 16 + cw) >> 3) ^ (r16 & 7));
+                if constexpr (STAGE) ostage[wave][0][sp] = val;
+                else
+                    for (int d = 0; d < a.ndst; ++d)
+                        *reinterpret_cast<uint4*>(dbase[d] + (size_t)(x + B) * a.dst_cs[d] + g * 16 + cw) = val;
                 if constexpr (SPLIT) {
                     const auto ll = __builtin_amdgcn_permlane16_swap(pl[0][0], pl[1][0], false, false);
                     const auto lh = __builtin_amdgcn_permlane16_swap(pl[0][1], pl[1][1], false, false);
                     const uint4 lv = make_uint4(ll[0], lh[0], ll[1], lh[1]);
-                    for (int d = 0; d < a.ndst; ++d)
-                        *reinterpret_cast<uint4*>(dlo[d] + (size_t)(x + B) * a.dst_cs[d] + g * 16 + cw) = lv;
+                    if constexpr (STAGE) ostage[wave][SPLIT ? 1 : 0][sp] = lv;
+                    else
+                        for (int d = 0; d < a.ndst; ++d)
+                            *reinterpret_cast<uint4*>(dlo[d] + (size_t)(x + B) * a.dst_cs[d] + g * 16 + cw) = lv;
                 }
+            }
+            if constexpr (STAGE) {
+                // (one wave writes and reads its own image: LDS operations of a wave stay in order)
+                __builtin_amdgcn_wave_barrier();
+                asm volatile("" ::: "memory");
+                const int npc = a.cout / 8;   // 16-byte pieces per pixel (4 or 8)
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {
+                    const int idx = k * 64 + lane, pp = idx >> 3, pc = idx & 7;
+                    const int xs = x0 + grp * 16 + pp;
+                    const int rd = pp * 8 + (pc ^ (pp & 7));
+                    const uint4 hv = ostage[wave][0][rd];
+                    uint4 lv2 = hv;
+                    if constexpr (SPLIT) lv2 = ostage[wave][SPLIT ? 1 : 0][rd];
+                    if (xs < W && pc < npc) {
+                        for (int d = 0; d < a.ndst; ++d) {
+                            const size_t o = (size_t)(xs + B) * a.dst_cs[d] + pc * 8;
+                            *reinterpret_cast<uint4*>(dbase[d] + o) = hv;
+                            if constexpr (SPLIT) *reinterpret_cast<uint4*>(dlo[d] + o) = lv2;
+                        }
+                    }
+                }
+                asm volatile("" ::: "memory");
+                __builtin_amdgcn_wave_barrier();   // the next group's pieces after these reads
             }
             continue;
         }
@@ -171,11 +211,12 @@ __global__ __launch_bounds__(256) void conv_image_kernel(const ConvArgs a, const
             const int ch = g * 16 + 4 * q;
             if (ch >= a.cout) continue;
             float v[4];
+            const float4_t bq = sbias[g * 4 + q], mq = smul[g * 4 + q];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 // (split: the sums of the 2^e-scaled weights times 2^-e, exact; ConvArgs::wscale)
-                const float t = (SPLIT ? acc[g][r] * a.wscale : acc[g][r]) + bv[g][r];
-                v[r] = t > 0.f ? t : t * mv[g][r];
+                const float t = (SPLIT ? acc[g][r] * a.wscale : acc[g][r]) + bq[r];
+                v[r] = t > 0.f ? t : t * mq[r];
             }
             const uint32_t lo = (uint32_t)f2h_bits_i(v[0]) | ((uint32_t)f2h_bits_i(v[1]) << 16);
             const uint32_t hi = (uint32_t)f2h_bits_i(v[2]) | ((uint32_t)f2h_bits_i(v[3]) << 16);
@@ -211,17 +252,21 @@ void launch_conv_image(const ConvArgs& a, const float* image, hipStream_t stream
     // 16-byte stores (CONV_IMAGE_WIDE=0: the 8-byte epilogue, dev A/B; same values)
     bool wide = a.cout % 32 == 0 && dev_switch("CONV_IMAGE_WIDE", 1) != 0;
     for (int d = 0; d < a.ndst; ++d) wide = wide && ((a.dst_cs[d] | a.dst_coff[d]) & 7) == 0;
-#define OPKI_LAUNCH(SP_, WI_)                                                                    \
-    hipLaunchKernelGGL((conv_image_kernel<SP_, WI_>), dim3((unsigned)blocks), dim3(256), 0, stream, a, image)
+    // whole-pixel stores through the per-wave LDS image (CONV_IMAGE_STAGE=0: direct, dev A/B)
+    const bool stage = wide && dev_switch("CONV_IMAGE_STAGE", 1) != 0;
+#define OPKI_LAUNCH(SP_, WI_, ST_)                                                               \
+    hipLaunchKernelGGL((conv_image_kernel<SP_, WI_, ST_>), dim3((unsigned)blocks), dim3(256), 0, stream, a, image)
     if (a.split) {
         for (int d = 0; d < a.ndst; ++d) OPK_CHECK_ARG(a.dst_lo[d] != nullptr, "conv_image: split needs dst_lo");
         note_launch("conv_image_kernel<split>");
-        if (wide) OPKI_LAUNCH(true, true);
-        else OPKI_LAUNCH(true, false);
+        if (stage) OPKI_LAUNCH(true, true, true);
+        else if (wide) OPKI_LAUNCH(true, true, false);
+        else OPKI_LAUNCH(true, false, false);
     } else {
         note_launch("conv_image_kernel");
-        if (wide) OPKI_LAUNCH(false, true);
-        else OPKI_LAUNCH(false, false);
+        if (stage) OPKI_LAUNCH(false, true, true);
+        else if (wide) OPKI_LAUNCH(false, true, false);
+        else OPKI_LAUNCH(false, false, false);
     }
 #undef OPKI_LAUNCH
     OPK_LAUNCH_CHECK();

@@ -380,6 +380,33 @@ def test_coco_pose_pipeline_runs_on_the_net(ctx):
 
 
 @pytest.mark.parametrize("precision", ["fp16", "split"])
+def test_conv_image_store_paths_bit_identical(ctx, precision):
+    """conv_image's three store paths -- 16-byte pieces staged per wave in LDS and stored as whole
+    pixels (the default), 16-byte pieces stored directly (CONV_IMAGE_STAGE=0) and 8-byte stores
+    (CONV_IMAGE_WIDE=0) -- write the same conv1_1 blob (hi and, split, lo) and the same net output,
+    on a width that leaves a partial 64-column tile (656 = 10 x 64 + 16)."""
+    from openpose_amd.api import PRECISION_SPLIT
+    graph = body25.layers()
+    params = synth.he_weights(graph, seed=61)
+    x = np.random.default_rng(62).uniform(-0.5, 0.5, (2, 3, 64, 656)).astype(np.float32)
+    outs = {}
+    for name, sw in {"stage": {}, "direct": {"CONV_IMAGE_STAGE": 0}, "narrow": {"CONV_IMAGE_WIDE": 0}}.items():
+        with dev_switches(CONV1_FUSED=0, LAUNCH_LOG=1, **sw):
+            net = Net(ctx, "builtin:BODY_25")
+            net.set_params(params)
+            if precision == "split":
+                net.set_precision(PRECISION_SPLIT)
+            net.forward(torch.from_numpy(x).cuda())
+            assert any(k.startswith("conv_image_kernel") for _, k in net.launch_log())
+            outs[name] = (net.blob("conv1_1"), net.output_numpy())
+            net.close()
+    assert np.abs(outs["stage"][0]).max() > 0
+    for name in ("direct", "narrow"):
+        np.testing.assert_array_equal(outs["stage"][0], outs[name][0])
+        np.testing.assert_array_equal(outs["stage"][1], outs[name][1])
+
+
+@pytest.mark.parametrize("precision", ["fp16", "split"])
 def test_head_fusion_matches_unfused_and_oracle(ctx, precision):
     """Mconv6 -> Mconv7 pairs (1x1 to 512 / 256 channels, then 1x1 to <= 64) run as one
     conv_head_kernel: fp16 outputs into a concat read by a later conv and fp32 net-output channels.
