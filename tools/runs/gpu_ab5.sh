@@ -2,7 +2,7 @@
 # dev (round 5): the in-tree build ("new") against variant builds openpose_amd/variants/libopk_<v>.so
 # in one GPU call -- net outputs bit for bit, per-layer + net GPU tests on the new build, the bench
 # interleaved (2 reps), and rocprofv3 kernel statistics of every build
-#   OUT=<dir under gpurun_out> bash tools/gpu_ab5.sh <variant> [<variant> ...]
+#   OUT=<dir under gpurun_out> bash tools/runs/gpu_ab5.sh <variant> [<variant> ...]
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && O=gpurun_out/${OUT:-ab5} && mkdir -p $O || exit 1
 V=$GRAFT_REPO_ROOT/openpose_amd/variants
 timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_layers.py tests/test_gpu_net.py > $O/pytest_layers.log 2>&1 || exit 1
