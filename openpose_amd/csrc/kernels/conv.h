@@ -53,8 +53,9 @@ struct ConvArgs {
     // Split precision (NetHip precision OPK_PRECISION_SPLIT; conv3_kernel only): every activation
     // x is held as two fp16 images, hi = fp16(x) and lo = fp16(x - hi) (in_lo / dst_lo: the lo
     // twins, same layout and offsets), and every weight w as w_hi = fp16(w), w_lo = fp16(w - w_hi).
-    // The K loop runs three products per 32-channel input chunk, chunk-major -- x_hi * w_hi,
-    // x_hi * w_lo (the same staged hi halo), x_lo * w_hi (weights packed
+    // The K loop runs three products per 32-channel input chunk, chunk-major -- x_hi * w_lo,
+    // x_hi * w_hi (the same staged hi halo), x_lo * w_hi (the w_hi tap rows of the product
+    // before, still in their weight slots: conv3w8 stages no weights for it) (weights packed
     // [cout_pad/BN][2 * cin_pad/32][ky][kx][BN][32]: the w_hi chunks, then the w_lo chunks) --
     // each product exact in fp32, so only the fp32 summation and the dropped x_lo * w_lo term
     // (~2^-22 relative) separate the result from an fp32 convolution.  The weights are packed
@@ -68,6 +69,12 @@ struct ConvArgs {
     uint16_t* dst_lo[kConvMaxDst];
     float wscale;
 };
+// the product of a split virtual chunk (3c + k) that reads w_lo: k = 0 (the order above; dev A/B
+// builds: OPK_SPLIT_WLO_K=1, the round-6 order x_hi w_hi, x_hi w_lo, x_lo w_hi, every product
+// staging its weights)
+#ifndef OPK_SPLIT_WLO_K
+#define OPK_SPLIT_WLO_K 0
+#endif
 
 // conv3.hip: 7x7, 3x3 and 1x1, input halo staged once per 32-channel chunk over a "virtual image" of
 // column strips (sw interior columns each).  Tile BM x BN = 256 x 128 / 96 (<= 80 KB LDS, two

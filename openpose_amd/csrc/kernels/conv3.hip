@@ -110,8 +110,9 @@ void conv3_kernel(const ConvArgs a)
     const int lrow = lane >> 2, phys = lane & 3;
     const int cpt = a.cin_pad >> 5;               // 32-channel chunks of the input
     // split precision: three products per input chunk c, chunk-major -- virtual chunk 3c + k,
-    // k = 0 x_hi w_hi, 1 x_hi w_lo (the hi halo of k = 0 again: no DMA), 2 x_lo w_hi (the lo
-    // twin's halo); hi halos in slot 0 (UPC == 1: slots 0 / 2 by chunk parity), lo halos in slot 1
+    // k = 0 x_hi w_lo, 1 x_hi w_hi (the hi halo of k = 0 again: no DMA), 2 x_lo w_hi (the lo
+    // twin's halo; conv.h OPK_SPLIT_WLO_K); hi halos in slot 0 (UPC == 1: slots 0 / 2 by chunk
+    // parity), lo halos in slot 1
     const int cptk = SPLIT ? 3 * cpt : cpt;       // K (virtual) chunks
     const int U = UPC * cptk;                     // units (chunk, taps)
     const ptrdiff_t dlo = SPLIT ? a.in_lo - a.in : 0;   // hi -> lo twin (elements)
@@ -131,12 +132,13 @@ void conv3_kernel(const ConvArgs a)
     const int ai = (API - wave + NW - 1) / NW;
     const int bi = (BPI - wave + NW - 1) / NW;
     // split: the packed weights hold w_hi and w_lo (2 cpt chunks per n-block); virtual chunk
-    // 3c + k reads w_lo chunk c (cpt + c) for k = 1, w_hi chunk c otherwise -- OPK3_WUNIT
+    // 3c + k reads w_lo chunk c (cpt + c) for k = OPK_SPLIT_WLO_K (conv.h), w_hi chunk c
+    // otherwise -- OPK3_WUNIT (the order of conv3w8_kernel, so the two stay bit-identical)
     const uint16_t* wbase = a.w + (size_t)nb * (SPLIT ? 2 * cpt : cpt) * KT * BN * 32;
 #define OPK3_WUNIT(u_)                                                                        \
     (!SPLIT ? (u_) : ({                                                                       \
         const int cc_ = (u_) / UPC;                                                           \
-        const int wc_ = cc_ % 3 == 1 ? cpt + cc_ / 3 : cc_ / 3;                               \
+        const int wc_ = cc_ % 3 == OPK_SPLIT_WLO_K ? cpt + cc_ / 3 : cc_ / 3;                 \
         wc_ * UPC + ((u_) - cc_ * UPC);                                                       \
     }))
     // halo slot of virtual chunk c_ and whether its first unit issues a halo DMA

@@ -61,9 +61,10 @@ typedef unsigned int opk8_u4 __attribute__((ext_vector_type(4)));
 #endif
 
 // SPLIT: split precision (ConvArgs::split, conv.h): K runs chunk-major over three products per
-// input chunk c -- virtual chunk 3c + k: k = 0 x_hi w_hi, 1 x_hi w_lo, 2 x_lo w_hi -- so the hi
+// input chunk c -- virtual chunk 3c + k: k = 0 x_hi w_lo, 1 x_hi w_hi, 2 x_lo w_hi -- so the hi
 // halo of a chunk is staged once for two products (k = 1 issues no halo DMA and reads k = 0's
-// slot; hi halos live in slot 0, lo halos in slot 1), in the order of conv3_kernel<..., SPLIT>;
+// slot; hi halos live in slot 0, lo halos in slot 1) and the w_hi tap rows once for two (k = 2
+// stages no weights: k = 1 left them in its slots), in the order of conv3_kernel<..., SPLIT>;
 // the epilogue writes hi = fp16(v) and lo = fp16(v - hi) of v = act(acc * wscale + bias) --
 // bit-identical to conv3_kernel's split instantiations.
 // split-precision pooling (POOL && SPLIT): of two (hi, lo) fp16 pairs of 8 channels, keep per
@@ -156,7 +157,8 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     const int cptk = SPLIT ? 3 * cpt : cpt;   // K (virtual) chunks (split: three per input chunk)
     const int U = 3 * cptk;
     // the n-block's first K unit in the packed weights (split: w_hi and w_lo, 2 cpt chunks of 3
-    // units; virtual chunk 3c + k reads w_lo chunk c (cpt + c) for k = 1, w_hi chunk c otherwise)
+    // units; virtual chunk 3c + k reads w_lo chunk c (cpt + c) for k = OPK_SPLIT_WLO_K, w_hi chunk
+    // c otherwise)
     const int ublk = nblk * 3 * (SPLIT ? 2 * cpt : cpt);
     const int bi = (BPI - wave + NW - 1) / NW;
     // weight piece of B DMA instruction j (recomputed at each issue: registers)
@@ -182,7 +184,10 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
         _Pragma("unroll") for (int i_ = 0; i_ < AIW; ++i_) dst_[i_] = OPK8_AROW1(mt_, i_);     \
     } while (0)
     // K unit (virtual chunk of product k_ over input chunk dc_, tap row ky_); split: k_ = 1
-    // reuses k_ = 0's hi halo (no DMA), k_ = 2 stages the lo twin's; fp16: k_ = 0, dc_ = chunk
+    // reuses k_ = 0's hi halo (no DMA), k_ = 2 stages the lo twin's; fp16: k_ = 0, dc_ = chunk.
+    // Split, k_ = 2 (x_lo w_hi) with k_ = 1 the w_hi product (OPK_SPLIT_WLO_K 0): its tap row's
+    // weight slot ((u + 2) % 3 = (u - 1) % 3, written last by unit u - 3, k_ = 1 at the same ky)
+    // still holds exactly these w_hi rows, so no weights are staged for it
 #define OPK8_ISSUE(k_, dc_, ky_, aslot_, bslot_, nt_)                                         \
     do {                                                                                      \
         if ((ky_) == 0 && (k_) != 1 && (OPK8_ABLATE != 7 || !dma_ab)) {                       \
@@ -197,10 +202,11 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
                         16, 0, 0);                                                            \
         }                                                                                     \
         const int bs_ = 2 * ASLOT + (bslot_) * BSLOT;                                         \
-        const int wc_ = (k_) == 1 ? cpt + (dc_) : (dc_);                                     \
+        const int wc_ = (SPLIT && (k_) == OPK_SPLIT_WLO_K) ? cpt + (dc_) : (dc_);            \
         const uint16_t* ub_ = a.w + (size_t)(ublk + wc_ * 3 + (ky_)) * BROWS * 32;            \
         _Pragma("unroll") for (int j_ = 0; j_ < BIW; ++j_)                                    \
-            if ((BPI % NW == 0 || j_ * NW + wave < BPI) && (OPK8_ABLATE != 8 || !dma_ab)) {   \
+            if ((BPI % NW == 0 || j_ * NW + wave < BPI) && (OPK8_ABLATE != 8 || !dma_ab) &&   \
+                !(SPLIT && OPK_SPLIT_WLO_K == 0 && (k_) == 2)) {                              \
                 const int bo_ = OPK8_BOFF(j_);                                                \
                 __builtin_amdgcn_global_load_lds(                                             \
                     (const void*)(ub_ + bo_),                                                 \
