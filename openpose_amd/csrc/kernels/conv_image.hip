@@ -10,8 +10,8 @@
 // pixel.  Replaces the im2col image + 1-step GEMM of conv.hip (two passes over HBM).
 // SPLIT (ConvArgs::split, net.h kPrecisionSplit): the weight rows carry w_lo = fp16(w - w_hi) in
 // their second 32 halves, each input value is split as x_hi = fp16(x), x_lo = fp16(x - x_hi) in
-// the gather, the three products x_hi w_hi, x_lo w_hi, x_hi w_lo accumulate in that order (one
-// K = 32 step each: the layer's whole K), and the epilogue scales the sums by wscale (the
+// the gather, the three products x_hi w_hi, x_lo w_hi, x_hi w_lo accumulate in that order (the
+// pass order of conv3_kernel's split K loop), and the epilogue scales the sums by wscale (the
 // weights are packed times 2^e, conv.h) and writes hi = fp16(v) and lo = fp16(v - hi) to dst / dst_lo.
 #include "conv.h"
 
