@@ -33,6 +33,13 @@ using namespace conv3dev;
 
 constexpr int k8_BM = 512, k8_HR = 688, k8_NW = 8;
 
+// Unit u+2's DMA right after the mid-unit barrier (a third of a unit more lead) instead of after
+// tap 2: the split 96- and 64-output tiles (measured 3-3.5 % faster per launch, round 6,
+// profiles/round6/split_dma_early/); the 128-output tiles spill 26-30 VGPRs with it (1.5x slower)
+// and the fp16 tiles keep their measured schedule.  Dev A/B builds: OPK8_DMA_EARLY 0 never, 1 always.
+#ifndef OPK8_DMA_EARLY
+#define OPK8_DMA_EARLY 2
+#endif
 #ifndef OPK8_ABLATE   // dev probe only (tools/conv3w_probe.hip): 1 no mid-unit barrier, 2 no MFMAs,
 #define OPK8_ABLATE 0  // 3 no fragment reads, 4 no DMA after the prologue, 5 no MFMAs in tap 1 of
                        // each unit (a third fewer, replaced by VALU adds), 6 the same with nothing
@@ -155,6 +162,7 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
     const int lrow = lane >> 2, phys = lane & 3;
     const int cpt = a.cin_pad >> 5;
     const int cptk = SPLIT ? 3 * cpt : cpt;   // K (virtual) chunks (split: three per input chunk)
+    constexpr bool kDmaEarly = OPK8_DMA_EARLY == 1 || (OPK8_DMA_EARLY == 2 && SPLIT && BN <= 96);
     const int U = 3 * cptk;
     // the n-block's first K unit in the packed weights (split: w_hi and w_lo, 2 cpt chunks of 3
     // units; virtual chunk 3c + k reads w_lo chunk c (cpt + c) for k = OPK_SPLIT_WLO_K, w_hi chunk
@@ -376,8 +384,9 @@ __global__ __launch_bounds__(64 * k8_NW, 1) void conv3w8_kernel(const ConvArgs a
             if (u == 0 && gc > 0 && (BST || a.ndst == 1)) vm_wait<S1>();   // (BST: one destination)
             else vm_wait<0>();
             if (OPK8_ABLATE != 1) __builtin_amdgcn_s_barrier();
+            if (kDmaEarly && (OPK8_ABLATE != 4 || u + 2 >= U)) OPK8_DMA_U2();
             OPK8_TAP(2, ab2, nab, nbb, 0, fbE, fbO);
-            if (OPK8_ABLATE != 4 || u + 2 >= U) OPK8_DMA_U2();
+            if (!kDmaEarly && (OPK8_ABLATE != 4 || u + 2 >= U)) OPK8_DMA_U2();
 #undef OPK8_DMA_U2
             if (SPLIT && ky == 2) {   // next virtual chunk
                 dcc += vk == 2 ? 1 : 0;
