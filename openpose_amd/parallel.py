@@ -4,9 +4,10 @@ Reference behaviour: one PoseExtractorCaffe + worker thr
 frames from a shared queue (include/openpose/wrapper/wrapperAuxiliary.hpp:328-337,1050-1067) and a
 WQueueOrderer that re-sequences results by frame id (include/openpose/thread/wQueueOrderer.hpp:
 62-141).  Here: one process per GPU under torch.distributed (RCCL on the GPU box, gloo on CPU),
-frames assigned to ranks in contiguous blocks (no data-path collective: every rank runs the whole
-hot path on its own frames), and the per-frame keypoint records gathered to rank 0 in frame order
-(the only collective; a few KB per frame).
+frames assigned to ranks in contiguous blocks, or pulled batch by batch from one queue shared
+through the process group's store (run_sharded(dispatch="queue"), BatchQueue) -- no data-path
+collective either way: every rank runs the whole hot path on its own frames -- and the per-frame
+keypoint records gathered to rank 0 in frame order (the only collective; a few KB per frame).
 """
 import os
 import socket
@@ -51,10 +52,57 @@ def gather_in_order(local, world, rank, dst=0, group=None):
     return [merged[i] for i in ids]
 
 
-def run_sharded(process_batch, n_frames, batch, rank, world):
-    """Run process_batch(list_of_frame_ids) -> {frame_id: record} over this rank's frames."""
-    mine = list(shard(n_frames, rank, world))
+_QUEUE_SEQ = [0]   # queues made so far (every rank makes them in the same order: same keys)
+
+
+class BatchQueue:
+    """One work queue of frame batches shared by every rank -- the reference's per-GPU workers
+    pulling datums from one queue (include/openpose/wrapper/wrapperAuxiliary.hpp:1050-1058) --
+    over the process group's key-value store: batch k (frames k*batch .. min((k+1)*batch, n) - 1)
+    goes to the rank whose atomic store.add on the queue's counter returned k, so a rank that
+    finishes its batches sooner takes more of them and no rank waits for a slower one's share.
+    World size 1 (or no process group): a local counter.  claim() returns the next batch's frame
+    ids, or None once every batch is taken; the caller's ordered gather (gather_in_order /
+    RecordGather.finish) re-sequences the frames, as the reference's WQueueOrderer does."""
+
+    def __init__(self, n_frames, batch, store=None):
+        self.n, self.batch = int(n_frames), max(1, int(batch))
+        self.batches = (self.n + self.batch - 1) // self.batch
+        if store is None and dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            store = dist.distributed_c10d._get_default_store()
+        self.store = store
+        self.key = "opk_batch_queue_%d" % _QUEUE_SEQ[0]
+        _QUEUE_SEQ[0] += 1
+        self.next_local = 0
+        self.taken = 0   # batches this rank claimed
+
+    def claim(self):
+        if self.store is None:
+            k = self.next_local
+            self.next_local += 1
+        else:
+            k = int(self.store.add(self.key, 1)) - 1
+        if k >= self.batches:
+            return None
+        self.taken += 1
+        return list(range(k * self.batch, min((k + 1) * self.batch, self.n)))
+
+
+def run_sharded(process_batch, n_frames, batch, rank, world, dispatch="static"):
+    """Run process_batch(list_of_frame_ids) -> {frame_id: record} over this rank's frames.
+    dispatch "static": the contiguous block of shard(); "queue": batches claimed from a BatchQueue
+    shared by all ranks (uneven per-frame cost: no rank idles while another still holds work)."""
     out = {}
+    if dispatch == "queue":
+        q = BatchQueue(n_frames, batch)
+        while True:
+            ids = q.claim()
+            if ids is None:
+                return out
+            out.update(process_batch(ids))
+    if dispatch != "static":
+        raise ValueError("dispatch: static or queue")
+    mine = list(shard(n_frames, rank, world))
     for i in range(0, len(mine), batch):
         out.update(process_batch(mine[i:i + batch]))
     return out

@@ -60,6 +60,61 @@ def test_frame_parallel_gloo_world2():
             np.testing.assert_array_equal(got["arr_%d" % i], kp)
 
 
+def _queue_worker(rank, world, port, out_path, delay):
+    """dispatch="queue" with rank 1 slowed down per batch: every frame once, in order, and the
+    fast rank takes more batches than its static share."""
+    import time
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    def work(ids):
+        if rank == 1:
+            time.sleep(delay)
+        return {i: (i, rank) + frame_record(i)[1:] for i in ids}
+    local = parallel.run_sharded(work, N_Q, 1, rank, world, dispatch="queue")
+    # a second queue in the same group starts from batch 0 again (its own store key)
+    again = parallel.run_sharded(lambda ids: {i: i for i in ids}, 4, 1, rank, world, dispatch="queue")
+    res = parallel.gather_in_order(local, world, rank)
+    res2 = parallel.gather_in_order(again, world, rank)
+    if rank == 0:
+        np.save(out_path, np.array([[r[0], r[1]] for r in res]))
+        np.savez(out_path + ".npz", *[r[2] for r in res])
+        np.save(out_path + ".again.npy", np.array(res2))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+N_Q = 12
+
+
+def test_queue_dispatch_balances_uneven_ranks_gloo():
+    """run_sharded(dispatch="queue"): batches pulled from one queue in the process group's store
+    (the reference's shared worker queue, wrapperAuxiliary.hpp:1050-1058).  With rank 1 0.25 s
+    slower per batch, rank 0 takes most of the 12 one-frame batches (the static split: 6 each);
+    the ordered gather still returns every frame once, in frame order, with the single-process
+    records; a second queue in the same group is independent of the first."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "q.npy")
+        port = 29500 + (os.getpid() + 7) % 1000
+        mp.spawn(_queue_worker, args=(2, port, out, 0.25), nprocs=2, join=True)
+        rows = np.load(out)
+        assert rows[:, 0].tolist() == list(range(N_Q))
+        by_rank0 = int((rows[:, 1] == 0).sum())
+        assert by_rank0 > N_Q // 2 + 1, rows[:, 1].tolist()
+        got = np.load(out + ".npz")
+        for i in range(N_Q):
+            np.testing.assert_array_equal(got["arr_%d" % i], frame_record(i)[1])
+        assert np.load(out + ".again.npy").tolist() == [0, 1, 2, 3]
+
+
+def test_batch_queue_local():
+    q = parallel.BatchQueue(7, 3)
+    assert [q.claim(), q.claim(), q.claim(), q.claim()] == [[0, 1, 2], [3, 4, 5], [6], None]
+    assert q.taken == 3
+    with pytest.raises(ValueError):
+        parallel.run_sharded(lambda ids: {}, 4, 1, 0, 1, dispatch="random")
+
+
 def test_gather_detects_missing_frames():
     with pytest.raises(RuntimeError, match="missing"):
         parallel.gather_in_order({0: 1, 2: 3}, 1, 0)
